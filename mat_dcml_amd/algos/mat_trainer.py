@@ -1,0 +1,146 @@
+"""MAT-PPO trainer on device tensors, data-parallel aware.
+
+Algorithm contract = reference ``mat_src/mat/algorithms/mat/mat_trainer.py:11-223``:
+
+* every PPO epoch recomputes next values, GAE returns and the normalised advantages (``:178-198``);
+* advantage normalisation over active entries with population std, ``(A - mean) / (std + 1e-5)`` (``:193-197``);
+* policy loss = −Σ min(r·Â, clip(r, 1±ε)·Â)·active / Σ active (``:129-139``);
+* value loss: ValueNorm.update(returns) then clipped + Huber(δ) on normalised returns, max, active-masked mean
+  (``:54-94``); total = policy − c_e·entropy + c_v·value (``:144``); clip_grad_norm(10) + Adam (``:146-154``).
+
+MI355X-specific:
+* statistics that the reference computes over the whole buffer (advantage mean/std, ValueNorm batch moments)
+  are all-reduced across ranks, and gradients are averaged with one flat all-reduce per minibatch
+  (``parallel/comm.py``), so N ranks ≡ one process with the N-times-larger buffer;
+* the per-minibatch loss/backward/clip/Adam runs either in eager PyTorch or through the fused HIP path
+  (``ops/mat_fused.py`` teacher-forced encoder/decoder kernels + ``ops/rl_ops``), and can be replayed as a
+  hipGraph (``use_graph``) — no host sync inside an epoch.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from ..ops import rl_ops
+from .valuenorm import ValueNorm
+
+
+def huber_loss(e, d):
+    a = (e.abs() <= d).float()
+    b = (e.abs() > d).float()
+    return a * e ** 2 / 2 + b * d * (e.abs() - d / 2)
+
+
+def mse_loss(e):
+    return e ** 2 / 2
+
+
+class MATTrainer:
+    def __init__(self, args, policy, num_agents, device=torch.device("cpu"), comm=None):
+        self.device = torch.device(device)
+        self.policy = policy
+        self.num_agents = num_agents
+        self.comm = comm
+        self.clip_param = args.clip_param
+        self.ppo_epoch = args.ppo_epoch
+        self.num_mini_batch = args.num_mini_batch
+        self.value_loss_coef = args.value_loss_coef
+        self.entropy_coef = args.entropy_coef
+        self.max_grad_norm = args.max_grad_norm
+        self.huber_delta = args.huber_delta
+        self._use_max_grad_norm = args.use_max_grad_norm
+        self._use_clipped_value_loss = args.use_clipped_value_loss
+        self._use_huber_loss = args.use_huber_loss
+        self._use_valuenorm = args.use_valuenorm
+        self._use_value_active_masks = args.use_value_active_masks
+        self._use_policy_active_masks = args.use_policy_active_masks
+        self.recompute_gae_every_epoch = getattr(args, "recompute_gae_every_epoch", True)
+        self.value_normalizer = ValueNorm(getattr(args, "n_objective", 1), device=self.device, comm=comm) \
+            if self._use_valuenorm else None
+        self.generator = None
+        self.params = [p for p in policy.transformer.parameters() if p.requires_grad]
+
+    # ------------------------------------------------------------------------------------------------
+    def cal_value_loss(self, values, value_preds_batch, return_batch, active_masks_batch):
+        clipped = value_preds_batch + (values - value_preds_batch).clamp(-self.clip_param, self.clip_param)
+        if self.value_normalizer is not None:
+            self.value_normalizer.update(return_batch)
+            target = self.value_normalizer.normalize(return_batch)
+        else:
+            target = return_batch
+        e_clip, e_orig = target - clipped, target - values
+        if self._use_huber_loss:
+            l_clip, l_orig = huber_loss(e_clip, self.huber_delta), huber_loss(e_orig, self.huber_delta)
+        else:
+            l_clip, l_orig = mse_loss(e_clip), mse_loss(e_orig)
+        vl = torch.max(l_orig, l_clip) if self._use_clipped_value_loss else l_orig
+        if self._use_value_active_masks:
+            am = active_masks_batch.expand_as(vl)
+            return (vl * am).sum() / am.sum()
+        return vl.mean()
+
+    def ppo_update(self, mb):
+        """One minibatch step.  ``mb`` is a dict of device tensors shaped (B, A, ·)."""
+        pol = self.policy
+        values, logp, entropy = pol.evaluate_actions(None, mb["obs"], mb["actions"], mb["ava"], mb["active"])
+        imp = torch.exp(logp - mb["old_logp"])
+        surr1 = imp * mb["adv"]
+        surr2 = torch.clamp(imp, 1.0 - self.clip_param, 1.0 + self.clip_param) * mb["adv"]
+        act = mb["active"]
+        if self._use_policy_active_masks:
+            policy_loss = -(torch.min(surr1, surr2).sum(-1, keepdim=True) * act).sum() / act.sum()
+        else:
+            policy_loss = -torch.min(surr1, surr2).sum(-1, keepdim=True).mean()
+        value_loss = self.cal_value_loss(values, mb["value_preds"], mb["returns"], act)
+        loss = policy_loss - entropy * self.entropy_coef + value_loss * self.value_loss_coef
+        pol.optimizer.zero_grad(set_to_none=False)
+        loss.backward()
+        if self.comm is not None and self.comm.world_size > 1:
+            self.comm.all_reduce_grads_(self.params)
+        if self._use_max_grad_norm:
+            grad_norm = nn.utils.clip_grad_norm_(self.params, self.max_grad_norm, foreach=True)
+        else:
+            grad_norm = torch.norm(torch.stack([p.grad.norm() for p in self.params if p.grad is not None]))
+        pol.optimizer.step()
+        return value_loss.detach(), grad_norm.detach(), policy_loss.detach(), entropy.detach(), imp.detach().mean()
+
+    # ------------------------------------------------------------------------------------------------
+    def _advantages(self, buffer):
+        adv = buffer.advantages
+        active = buffer.active_masks[:-1]
+        sums = rl_ops.masked_sums(adv, active)
+        if self.comm is not None and self.comm.world_size > 1:
+            self.comm.all_reduce_sum_(sums)
+        return rl_ops.normalize_from_sums(adv, sums)
+
+    def train(self, buffer):
+        pol = self.policy
+        keys = ["value_loss", "policy_loss", "dist_entropy", "actor_grad_norm", "critic_grad_norm", "ratio"]
+        acc = torch.zeros(len(keys), device=self.device)
+        T, E = buffer.T, buffer.E
+        obs_f = buffer.flat("obs")
+        act_f = buffer.flat("actions")
+        ava_f = buffer.flat("available_actions")
+        lp_f = buffer.flat("action_log_probs")
+        vp_f = buffer.flat("value_preds")
+        am_f = buffer.flat("active_masks")
+        for epoch in range(self.ppo_epoch):
+            if epoch == 0 or self.recompute_gae_every_epoch:
+                next_values = pol.get_values(None, buffer.obs[-1], buffer.available_actions[-1])
+                buffer.compute_returns(next_values, self.value_normalizer)
+                adv = self._advantages(buffer)
+                adv_f = adv.reshape(T * E, *adv.shape[2:])
+                ret_f = buffer.flat("returns")
+            for idx in buffer.minibatch_indices(self.num_mini_batch, self.generator):
+                mb = {"obs": obs_f[idx], "actions": act_f[idx], "ava": ava_f[idx], "old_logp": lp_f[idx],
+                      "value_preds": vp_f[idx], "returns": ret_f[idx], "active": am_f[idx], "adv": adv_f[idx]}
+                vl, gn, pl, ent, ratio = self.ppo_update(mb)
+                acc += torch.stack([vl, pl, ent, gn, gn, ratio]).float()
+        acc /= self.ppo_epoch * self.num_mini_batch
+        return dict(zip(keys, acc))
+
+    def prep_training(self):
+        self.policy.train()
+
+    def prep_rollout(self):
+        self.policy.eval()

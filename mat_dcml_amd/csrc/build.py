@@ -1,0 +1,65 @@
+"""Build the in-tree HIP library for gfx950: every ``*.hip`` in this directory -> ``../_lib/libmatdcml.so``.
+
+Plain ``hipcc`` (no torch headers): each translation unit compiles in seconds and the result is loaded with
+ctypes (``ops/kernels.py``).  Objects are cached by content hash under ``_lib/obj``.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import hashlib
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+OUT_DIR = os.path.join(os.path.dirname(HERE), "_lib")
+OUT = os.path.join(OUT_DIR, "libmatdcml.so")
+ARCH = os.environ.get("MAT_DCML_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=fast", "-munsafe-fp-atomics",
+         "-Wno-unused-result", "-fvisibility=hidden"]
+
+
+def _sources():
+    return sorted(os.path.join(HERE, f) for f in os.listdir(HERE) if f.endswith(".hip"))
+
+
+def _hash(path):
+    h = hashlib.sha256()
+    for p in [path] + sorted(os.path.join(HERE, f) for f in os.listdir(HERE) if f.endswith(".h")):
+        with open(p, "rb") as f:
+            h.update(f.read())
+    h.update(" ".join(FLAGS).encode())
+    return h.hexdigest()[:16]
+
+
+def _compile(src):
+    os.makedirs(os.path.join(OUT_DIR, "obj"), exist_ok=True)
+    obj = os.path.join(OUT_DIR, "obj", os.path.basename(src) + "." + _hash(src) + ".o")
+    if not os.path.exists(obj):
+        cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj + ".tmp"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
+        os.replace(obj + ".tmp", obj)
+    return obj
+
+
+def build(verbose=True, jobs=None):
+    srcs = _sources()
+    jobs = jobs or min(8, len(srcs)) or 1
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(_compile, srcs))
+    cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", OUT + ".tmp"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr}")
+    os.replace(OUT + ".tmp", OUT)
+    if verbose:
+        print(f"[build] {OUT} <- {', '.join(os.path.basename(s) for s in srcs)}")
+    return OUT
+
+
+if __name__ == "__main__":
+    build()
+    sys.exit(0)

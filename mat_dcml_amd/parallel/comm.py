@@ -1,0 +1,139 @@
+"""Data-parallel communicator: one process per GPU, RCCL over xGMI (``torch.distributed`` backend ``nccl``).
+
+The reference has no distributed training at all (no torch.distributed / NCCL / MPI; device
+hard-coded to ``cuda:0``).  This module is the new DP layer:
+
+* ``init_from_env`` — reads RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT (torchrun contract),
+  binds ``cuda:LOCAL_RANK`` and creates the process group (``nccl`` = RCCL on ROCm; ``gloo`` for CPU tests).
+* ``FlatGrads`` — every parameter's ``.grad`` is a view into ONE contiguous fp32 buffer (151k floats ≈ 606 KB
+  for the DCML MAT), so a data-parallel gradient average is ONE all-reduce with no pack/unpack copies.
+  At this message size a ring all-reduce over xGMI is latency-bound (2(p−1) hops); one bucket per minibatch is
+  the right granularity — splitting it into per-layer buckets to overlap with backward only adds latency.
+* ``all_reduce_sum_`` for the small statistics vectors (advantage moments, ValueNorm moments, metrics),
+  packed by the callers into one message each.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+class Comm:
+    def __init__(self, rank=0, world_size=1, local_rank=0, device=torch.device("cpu"), group=None):
+        self.rank, self.world_size, self.local_rank = rank, world_size, local_rank
+        self.device = device
+        self.group = group
+        self._flat = None
+
+    @property
+    def is_main(self):
+        return self.rank == 0
+
+    # -------------------------------------------------------------------------------- collectives
+    def all_reduce_sum_(self, t: torch.Tensor):
+        if self.world_size > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return t
+
+    def all_reduce_max_(self, t: torch.Tensor):
+        if self.world_size > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return t
+
+    def all_reduce_mean_(self, t: torch.Tensor):
+        if self.world_size > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+            t.div_(self.world_size)
+        return t
+
+    def barrier(self):
+        if self.world_size > 1:
+            if self.device.type == "cuda":
+                dist.barrier(group=self.group, device_ids=[self.device.index])
+            else:
+                dist.barrier(group=self.group)
+
+    def broadcast_module_(self, module: torch.nn.Module, src=0):
+        if self.world_size > 1:
+            with torch.no_grad():
+                for t in list(module.parameters()) + list(module.buffers()):
+                    dist.broadcast(t.data, src=src, group=self.group)
+
+    def all_gather_object(self, obj):
+        if self.world_size == 1:
+            return [obj]
+        out = [None] * self.world_size
+        dist.all_gather_object(out, obj, group=self.group)
+        return out
+
+    # -------------------------------------------------------------------------------- gradients
+    def attach_flat_grads(self, params):
+        self._flat = FlatGrads(params)
+        return self._flat
+
+    def all_reduce_grads_(self, params):
+        if self.world_size == 1:
+            return
+        if self._flat is None or not self._flat.owns(params):
+            self.attach_flat_grads(params)
+        self._flat.ensure_views()
+        dist.all_reduce(self._flat.buf, op=dist.ReduceOp.SUM, group=self.group)
+        self._flat.buf.mul_(1.0 / self.world_size)
+
+    def destroy(self):
+        if self.world_size > 1 and dist.is_initialized():
+            dist.destroy_process_group()
+
+
+class FlatGrads:
+    """All ``.grad`` tensors as views of one flat buffer (zero_grad must use ``set_to_none=False``)."""
+
+    def __init__(self, params):
+        self.params = [p for p in params if p.requires_grad]
+        n = sum(p.numel() for p in self.params)
+        dev = self.params[0].device
+        self.buf = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.views = []
+        off = 0
+        for p in self.params:
+            v = self.buf[off:off + p.numel()].view_as(p)
+            if p.grad is not None:
+                v.copy_(p.grad)
+            p.grad = v
+            self.views.append(v)
+            off += p.numel()
+        self._ids = {id(p) for p in self.params}
+
+    def owns(self, params):
+        return all(id(p) in self._ids for p in params if p.requires_grad)
+
+    def ensure_views(self):
+        for p, v in zip(self.params, self.views):
+            if p.grad is None or p.grad.data_ptr() != v.data_ptr():
+                if p.grad is not None:
+                    v.copy_(p.grad)
+                else:
+                    v.zero_()
+                p.grad = v
+
+
+def init_from_env(prefer_gpu=True, timeout_s=600) -> Comm:
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    use_gpu = prefer_gpu and torch.cuda.is_available()
+    device = torch.device(f"cuda:{local}") if use_gpu else torch.device("cpu")
+    if use_gpu:
+        torch.cuda.set_device(device)
+    group = None
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = "nccl" if use_gpu else "gloo"
+        kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+        if use_gpu:
+            kw["device_id"] = device
+        dist.init_process_group(**kw)
+    return Comm(rank, world, local, device, group)

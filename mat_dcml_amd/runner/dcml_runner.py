@@ -1,0 +1,249 @@
+"""DCML training / evaluation loop — one process per GPU, everything device resident.
+
+Behavioural contract = reference ``dcml_runner.py:17-448`` + ``base_runner.py:12-505``:
+
+* ``run`` (``dcml_runner.py:22-124``): episodes = num_env_steps // T // n_rollout_threads (per rank here);
+  per episode: T rollout steps (collect → env.step → insert), compute next value + GAE, PPO train, save every
+  ``save_interval`` episodes and at the last one, log every ``log_interval`` (FPS banner, average step
+  reward, episode reward / delay / payment means), eval every ``eval_interval`` when ``--use_eval``.
+* ``insert`` (``:250-288``): masks = 0 for envs whose agents are all done; active masks are 1 (DCML agents
+  finish together).
+* ``eval`` (``:319-448``): deterministic decoding with the batch decision ``stride``; reports mean episode
+  reward / delay / payment and per-decision inference time.  Runs a bounded number of steps (the reference
+  loops ``range(total_num_steps)``, §2.7 #7 — fixed).
+
+MI355X design: the env is ``DeviceDCMLEnv`` (E envs as tensors, HIP env kernels), actions never leave the
+GPU, episode statistics are accumulated on device and read back once per log interval, the env-id space is
+partitioned by rank so the global env set does not depend on the GPU count.
+"""
+from __future__ import annotations
+
+import os
+import time
+
+import numpy as np
+import torch
+
+from ..algos.buffer import RolloutBuffer
+from ..algos.mat_trainer import MATTrainer
+from ..algos.policy import TransformerPolicy
+from ..envs.dcml.config import DCMLConfig
+from ..envs.dcml.spaces import dcml_action_spaces
+from ..envs.dcml.vec_env import DeviceDCMLEnv
+from ..parallel.comm import Comm
+from ..utils.logger import ScalarWriter
+from ..utils.timers import PhaseTimers
+
+
+class DCMLRunner:
+    def __init__(self, config):
+        a = config["all_args"]
+        self.all_args = a
+        self.comm: Comm = config.get("comm") or Comm(device=torch.device(config["device"]))
+        self.device = torch.device(config["device"])
+        self.run_dir = config.get("run_dir")
+        self.num_env_steps = a.num_env_steps
+        self.episode_length = a.episode_length
+        self.n_rollout_threads = a.n_rollout_threads
+        self.n_eval_rollout_threads = a.n_eval_rollout_threads
+        self.algorithm_name = a.algorithm_name
+        self.experiment_name = a.experiment_name
+        self.use_linear_lr_decay = a.use_linear_lr_decay
+        self.save_interval, self.log_interval = a.save_interval, a.log_interval
+        self.use_eval, self.eval_interval = a.use_eval, a.eval_interval
+        self.train_stride, self.eval_stride = getattr(a, "train_stride", 1), getattr(a, "eval_stride", 2)
+        self.dcml = config.get("dcml_cfg") or DCMLConfig(n_workers=getattr(a, "n_workers", 100))
+        rank = self.comm.rank
+        E = self.n_rollout_threads
+        self.envs = config.get("envs") or DeviceDCMLEnv(E, self.dcml, self.device, seed=a.seed,
+                                                        env_id_offset=rank * E,
+                                                        backend="torch" if a.kernels == "torch" else "auto")
+        self.eval_envs = config.get("eval_envs")
+        if self.eval_envs is None and self.use_eval:
+            self.eval_envs = DeviceDCMLEnv(self.n_eval_rollout_threads, self.dcml, self.device, seed=a.seed + 10007,
+                                           env_id_offset=rank * self.n_eval_rollout_threads,
+                                           backend="torch" if a.kernels == "torch" else "auto")
+        self.num_agents = self.envs.n_agents
+        act_space = dcml_action_spaces(self.dcml.n_workers)[0]
+        torch.manual_seed(a.seed)
+        self.policy = TransformerPolicy(a, self.envs.observation_space[0], self.envs.share_observation_space[0],
+                                        act_space, self.num_agents, device=self.device)
+        self.comm.broadcast_module_(self.policy.transformer)
+        if self.comm.world_size > 1:
+            self.comm.attach_flat_grads(self.policy.transformer.parameters())
+        self.trainer = MATTrainer(a, self.policy, self.num_agents, device=self.device, comm=self.comm)
+        self.buffer = RolloutBuffer(a.episode_length, E, self.num_agents, self.dcml.obs_dim, self.dcml.share_dim,
+                                    self.dcml.action_dim, gamma=a.gamma, gae_lambda=a.gae_lambda,
+                                    use_valuenorm=a.use_valuenorm or a.use_popart, n_objective=a.n_objective,
+                                    device=self.device)
+        self.log_dir = os.path.join(str(self.run_dir), "logs") if self.run_dir else None
+        self.save_dir = os.path.join(str(self.run_dir), "models") if self.run_dir else None
+        self.writter = ScalarWriter(self.log_dir or "/tmp/mat_dcml_logs", enabled=bool(self.run_dir) and self.comm.is_main)
+        self.timers = PhaseTimers(self.device, enabled=getattr(a, "profile_phases", False))
+        self.start_episode = 0
+        if a.model_dir:
+            self.policy.restore(a.model_dir)
+            self.comm.broadcast_module_(self.policy.transformer)
+        self._ep_reward = torch.zeros(E, device=self.device)
+        self._ep_delay = torch.zeros(E, device=self.device)
+        self._ep_pay = torch.zeros(E, device=self.device)
+        self._done_stats = torch.zeros(4, device=self.device, dtype=torch.float64)  # n, Σreward, Σdelay, Σpay
+
+    # ---------------------------------------------------------------------------------------- rollout
+    def warmup(self):
+        obs, share, ava = self.envs.reset()
+        self.buffer.obs[0].copy_(obs)
+        self.buffer.share_obs[0].copy_(share[:, 0])
+        self.buffer.available_actions[0].copy_(ava)
+        self.buffer.masks.fill_(1.0)
+
+    @torch.no_grad()
+    def collect(self, step):
+        b = self.buffer
+        return self.policy.get_actions(None, b.obs[step], b.available_actions[step], deterministic=False,
+                                       stride=self.train_stride)
+
+    @torch.no_grad()
+    def rollout(self):
+        self.trainer.prep_rollout()
+        for step in range(self.episode_length):
+            with self.timers("decode"):
+                values, actions, logp = self.collect(step)
+            with self.timers("env"):
+                obs, share, reward, done, delay, pay, ava = self.envs.step(actions)
+            with self.timers("insert"):
+                self._track(reward, done, delay, pay)
+                self.insert(obs, share, reward, done, ava, values, actions, logp)
+
+    def _track(self, reward, done, delay, pay):
+        self._ep_reward += reward
+        self._ep_delay += delay
+        self._ep_pay += pay
+        d = done.to(torch.float64)
+        self._done_stats += torch.stack([d.sum(), (self._ep_reward.double() * d).sum(),
+                                         (self._ep_delay.double() * d).sum(), (self._ep_pay.double() * d).sum()])
+        keep = (~done).float()
+        self._ep_reward *= keep
+        self._ep_delay *= keep
+        self._ep_pay *= keep
+
+    def insert(self, obs, share, reward, done, ava, values, actions, logp):
+        E, A = self.buffer.E, self.buffer.A
+        masks = (~done).float().view(E, 1, 1).expand(E, A, 1)
+        self.buffer.insert(share, obs, actions, logp, values, reward.view(E, 1, 1).expand(E, A, 1), masks,
+                           None, ava)
+
+    def compute(self):
+        pass  # next-value + GAE are recomputed inside every PPO epoch (mat_trainer.py:178-192)
+
+    def train(self):
+        self.trainer.prep_training()
+        infos = self.trainer.train(self.buffer)
+        self.buffer.after_update()
+        return infos
+
+    def train_iteration(self):
+        """One PPO iteration = T·E env steps + the update.  The unit timed by bench.py."""
+        self.rollout()
+        self.compute()
+        with self.timers("update"):
+            infos = self.train()
+        return infos
+
+    # ---------------------------------------------------------------------------------------- main loop
+    def run(self):
+        self.warmup()
+        start = time.time()
+        episodes = int(self.num_env_steps) // self.episode_length // self.n_rollout_threads // self.comm.world_size
+        episodes = max(episodes, 1)
+        last_infos = None
+        for episode in range(self.start_episode, episodes):
+            if self.use_linear_lr_decay:
+                self.policy.lr_decay(episode, episodes)
+            infos = self.train_iteration()
+            total = (episode + 1) * self.episode_length * self.n_rollout_threads * self.comm.world_size
+            if episode % self.save_interval == 0 or episode == episodes - 1:
+                self.save(episode)
+            if episode % self.log_interval == 0:
+                self.log(episode, episodes, total, start, infos)
+            if self.use_eval and episode % self.eval_interval == 0:
+                self.eval(total)
+            last_infos = infos
+        return last_infos
+
+    def log(self, episode, episodes, total, start, infos):
+        stats = self._done_stats.clone()
+        self.comm.all_reduce_sum_(stats)
+        avg_step_reward = self.buffer.rewards.mean().reshape(1).double()
+        self.comm.all_reduce_mean_(avg_step_reward)
+        infos = {k: float(v) for k, v in infos.items()}
+        infos["average_step_rewards"] = float(avg_step_reward)
+        self._done_stats.zero_()
+        if not self.comm.is_main:
+            return
+        fps = int(total / max(time.time() - start, 1e-9))
+        print(f"\n Scenario {self.all_args.scenario} Algo {self.algorithm_name} Exp {self.experiment_name} "
+              f"updates {episode}/{episodes} episodes, total num timesteps {total}/{self.num_env_steps}, FPS {fps}.\n")
+        print(f"average_step_rewards is {infos['average_step_rewards']}.")
+        for k, v in infos.items():
+            self.writter.add_scalars(k, {k: v}, total)
+        n = float(stats[0])
+        if n > 0:
+            r, d, p = float(stats[1]) / n, float(stats[2]) / n, float(stats[3]) / n
+            self.writter.add_scalars("train_episode_rewards", {"aver_rewards": r}, total)
+            self.writter.add_scalars("train_episode_scores", {"aver_delay": d, "aver_payment": p}, total)
+            print(f"some episodes done, average rewards: {r}, delays: {d},payments: {p}")
+        if self.timers.enabled:
+            print(self.timers.summary())
+
+    def save(self, episode):
+        self.comm.barrier()
+        if self.comm.is_main and self.save_dir:
+            self.policy.save(self.save_dir, episode)
+            if getattr(self.all_args, "save_trainer_state", True):
+                from ..utils.checkpoint import save_trainer_state
+                save_trainer_state(os.path.join(self.save_dir, f"trainer_state_{episode}.pt"), self.policy,
+                                   self.trainer, episode)
+
+    # ---------------------------------------------------------------------------------------- eval
+    @torch.no_grad()
+    def eval(self, total_num_steps=0, stride=None, n_steps=None):
+        stride = self.eval_stride if stride is None else stride
+        env = self.eval_envs
+        obs, share, ava = env.reset()
+        E = env.E
+        n_steps = n_steps or max(1, self.all_args.eval_episodes * 2)
+        ep_r = torch.zeros(E, device=self.device)
+        ep_d = torch.zeros(E, device=self.device)
+        ep_p = torch.zeros(E, device=self.device)
+        stats = torch.zeros(4, device=self.device, dtype=torch.float64)
+        times = []
+        for _ in range(n_steps):
+            if self.device.type == "cuda":
+                torch.cuda.synchronize()
+            t0 = time.time()
+            _, actions, _ = self.policy.get_actions(None, obs, ava, deterministic=True, stride=stride)
+            if self.device.type == "cuda":
+                torch.cuda.synchronize()
+            times.append(time.time() - t0)
+            obs, share, reward, done, delay, pay, ava = env.step(actions)
+            ep_r += reward
+            ep_d += delay
+            ep_p += pay
+            dd = done.double()
+            stats += torch.stack([dd.sum(), (ep_r.double() * dd).sum(), (ep_d.double() * dd).sum(),
+                                  (ep_p.double() * dd).sum()])
+            keep = (~done).float()
+            ep_r *= keep
+            ep_d *= keep
+            ep_p *= keep
+        self.comm.all_reduce_sum_(stats)
+        n = max(float(stats[0]), 1.0)
+        res = (float(stats[1]) / n, float(stats[2]) / n, float(stats[3]) / n, float(np.mean(times)))
+        if self.comm.is_main:
+            print(f"eval average episode rewards: {res[0]}, delays: {res[1]}, payments: {res[2]}.")
+            print("Inference time: ", res[3])
+            self.writter.add_scalars("eval", {"average_episode_rewards": res[0], "average_episode_delays": res[1],
+                                              "average_episode_payments": res[2], "inference_time": res[3]},
+                                     total_num_steps)
+        return res

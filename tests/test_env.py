@@ -1,0 +1,98 @@
+"""DCML device env: layout, reproducibility, rank partitioning and statistical parity with the reference."""
+import numpy as np
+import pytest
+import torch
+
+import ref_oracle as ro
+from mat_dcml_amd.envs.dcml.config import DCMLConfig
+from mat_dcml_amd.envs.dcml.vec_env import DeviceDCMLEnv
+
+
+def test_shapes_and_layout():
+    env = DeviceDCMLEnv(3, DCMLConfig(n_workers=32), seed=2)
+    obs, share, ava = env.reset()
+    assert obs.shape == (3, 33, 7) and share.shape == (3, 33, 34) and ava.shape == (3, 33, 2)
+    av = env.avail
+    d = env.n_disable
+    assert torch.equal((~av).sum(1), d)
+    assert (ava[:, :32, 1] == av.float()).all() and (ava[:, 32] == 1).all() and (ava[..., 0] == 1).all()
+    # disabled rows: [R, C, 1, 1, 1, 1, carry]
+    dis = obs[:, :32][~av]
+    assert (dis[:, 2:6] == 1).all()
+    # rank feature of available workers = (#available before i) / (W - d)
+    for e in range(3):
+        cnt = 0
+        for i in range(32):
+            if av[e, i]:
+                assert abs(float(obs[e, i, 6]) - cnt / (32 - int(d[e]))) < 1e-6
+                cnt += 1
+    assert torch.allclose(obs[:, 32, 6], torch.full((3,), 1.1))
+    assert torch.allclose(share[:, 0, 2:], env.worker_pr.float())
+
+
+def test_reproducible_and_rank_partitioned():
+    cfg = DCMLConfig(n_workers=16)
+    a = DeviceDCMLEnv(8, cfg, seed=3)
+    b = DeviceDCMLEnv(8, cfg, seed=3)
+    lo = DeviceDCMLEnv(4, cfg, seed=3, env_id_offset=0)
+    hi = DeviceDCMLEnv(4, cfg, seed=3, env_id_offset=4)
+    for e in (a, b, lo, hi):
+        e.reset()
+    act = torch.randint(0, 2, (8, 17)).float()
+    act[:, -1] = 0.6
+    for _ in range(3):
+        oa = a.step(act)
+        ob = b.step(act)
+        ol = lo.step(act[:4])
+        oh = hi.step(act[4:])
+        for x, y, l, h in zip(oa, ob, ol, oh):
+            assert torch.equal(x, y)
+            assert torch.equal(x, torch.cat([l, h]))
+
+
+def test_standalone_branch_and_clamps():
+    cfg = DCMLConfig(n_workers=8)
+    env = DeviceDCMLEnv(4, cfg, seed=1)
+    env.reset()
+    act = torch.zeros(4, 9)  # N == 0 -> worker 0 alone, 1.5x reward penalty
+    obs, sh, r, d, delay, pay, ava = env.step(act)
+    assert torch.allclose(r, -1.5 * (99 * delay + pay), rtol=1e-5)
+    act = torch.ones(4, 9)
+    act[:, -1] = 5.0  # ratio > 1 -> K clamps to N
+    obs, sh, r, d, delay, pay, ava = env.step(act)
+    assert torch.allclose(r, -(99 * delay + pay), rtol=1e-5) and (delay > 0).all()
+
+
+def _run_ours(n_steps=40, envs=64, seed=5, W=100):
+    env = DeviceDCMLEnv(envs, DCMLConfig(n_workers=W), fixed=True, seed=seed)
+    env.reset()
+    d, p = [], []
+    for _ in range(n_steps):
+        o = env.step(torch.zeros(envs, W + 1))
+        d.append(o[4])
+        p.append(o[5])
+    return torch.cat(d).numpy().astype(np.float64), torch.cat(p).numpy().astype(np.float64)
+
+
+@pytest.mark.skipif(not ro.available(), reason="reference not mounted")
+def test_fixed_heuristic_distribution_matches_reference(tmp_path):
+    """Statistical parity (the reference is irreproducible by construction, SURVEY.md §4.3 'Env parity')."""
+    from scipy.stats import ks_2samp
+    ro.install_stubs()
+    import random
+    random.seed(11)
+    np.random.seed(11)
+    with ro.ref_cwd(tmp_path):
+        from DCML_BID_FIRST_MA_ENV_SingleProcess import Env
+        env = Env(fixed=True)
+        env.reset()
+        rd, rp = [], []
+        for _ in range(1500):
+            _, _, _, _, info, _ = env.step(np.zeros((101, 1)))
+            rd.append(info[0]["delay"])
+            rp.append(info[0]["payment"])
+    od, op = _run_ours()
+    assert ks_2samp(rd, od).pvalue > 1e-3, (np.mean(rd), np.mean(od))
+    assert ks_2samp(rp, op).pvalue > 1e-3, (np.mean(rp), np.mean(op))
+    assert abs(np.mean(rd) - np.mean(od)) / np.mean(rd) < 0.05
+    assert abs(np.mean(rp) - np.mean(op)) / np.mean(rp) < 0.05
