@@ -103,3 +103,64 @@ def philox_fill(n, c1, c2, c3, k0, k1, device):
     out = torch.empty(n, 4, dtype=torch.int64, device=device)
     check(lib().mdl_philox_fill(P(out), n, c1, c2, c3, k0, k1, _stream()), "philox_fill")
     return out
+
+
+# ----------------------------------------------------------------------------------------- DCML env
+class EnvCfg(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("E", "W", "A", "P", "obs_dim", "share_dim", "fixed", "preset",
+                                            "max_disable", "max_slot_iters", "preset_rows")] + \
+               [("k0", ctypes.c_uint32), ("k1", ctypes.c_uint32)] + \
+               [(n, ctypes.c_double) for n in ("r_min", "r_max", "c_min", "c_max", "r_hi", "c_hi", "pr_min", "pr_max",
+                                               "rate", "freq", "bit_to_byte", "continue_prob", "alpha", "beta",
+                                               "standalone_penalty", "fixed_k_ratio")] + \
+               [("master_feature", ctypes.c_float)]
+
+
+class EnvState(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("gid", "profiles", "counter", "task_ctr", "R", "C", "master_pr",
+                                               "worker_pr", "avail", "n_disable", "arrive", "lw", "obs", "share",
+                                               "ava", "preset_idx", "preset_master", "preset_prs", "preset_disable")]
+
+
+class StepOut(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("actions", "reward", "done", "delay", "payment")]
+
+
+sig("mdl_dcml_env_reset", ctypes.POINTER(EnvCfg), ctypes.POINTER(EnvState), vp)
+sig("mdl_dcml_env_step", ctypes.POINTER(EnvCfg), ctypes.POINTER(EnvState), ctypes.POINTER(StepOut), vp)
+
+
+def _env_structs(env):
+    c = env.cfg
+    ec = EnvCfg(E=env.E, W=env.W, A=env.A, P=env.P, obs_dim=c.obs_dim, share_dim=c.share_dim, fixed=int(env.fixed),
+                preset=int(env.preset), max_disable=c.max_disable, max_slot_iters=c.max_slot_iters,
+                preset_rows=int(env.preset_master.shape[0]) if env.preset else 0, k0=env.k0, k1=env.k1,
+                r_min=c.r_min, r_max=c.r_max, c_min=c.c_min, c_max=c.c_max, r_hi=c.r_hi, c_hi=c.c_hi,
+                pr_min=c.pr_min, pr_max=c.pr_max, rate=c.data_rate, freq=c.frequency, bit_to_byte=c.bit_to_byte,
+                continue_prob=c.continue_prob, alpha=c.alpha, beta=c.beta, standalone_penalty=c.standalone_penalty,
+                fixed_k_ratio=c.fixed_k_ratio, master_feature=c.master_feature)
+    pm = env.preset_master if env.preset else None
+    pp = env.preset_prs if env.preset else None
+    pd = env.preset_disable if env.preset else None
+    es = EnvState(*[t.data_ptr() if t is not None else None for t in (
+        env.gid, env.profiles, env.counter, env.task_ctr, env.R, env.C, env.master_pr, env.worker_pr, env.avail,
+        env.n_disable, env.arrive, env.lw, env.obs, env.share, env.ava, env.preset_idx, pm, pp, pd)])
+    return ec, es
+
+
+def dcml_env_reset(env, mask=None):
+    ec, es = _env_structs(env)
+    check(lib().mdl_dcml_env_reset(ctypes.byref(ec), ctypes.byref(es), _stream()), "dcml_env_reset")
+
+
+def dcml_env_step(env, actions):
+    if not hasattr(env, "_out"):
+        dev = env.device
+        env._out = (torch.zeros(env.E, device=dev), torch.zeros(env.E, dtype=torch.bool, device=dev),
+                    torch.zeros(env.E, device=dev), torch.zeros(env.E, device=dev))
+    rew, done, delay, pay = env._out
+    actions = actions.contiguous()
+    ec, es = _env_structs(env)
+    so = StepOut(actions.data_ptr(), rew.data_ptr(), done.data_ptr(), delay.data_ptr(), pay.data_ptr())
+    check(lib().mdl_dcml_env_step(ctypes.byref(ec), ctypes.byref(es), ctypes.byref(so), _stream()), "dcml_env_step")
+    return env.obs, env.share_view(), rew, done, delay, pay, env.ava
