@@ -21,7 +21,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from ..ops import rl_ops
+from ..ops import mat_fused, rl_ops
 from .valuenorm import ValueNorm
 
 
@@ -102,6 +102,7 @@ class MATTrainer:
         else:
             grad_norm = torch.norm(torch.stack([p.grad.norm() for p in self.params if p.grad is not None]))
         pol.optimizer.step()
+        mat_fused.bump_version(pol.transformer)
         return value_loss.detach(), grad_norm.detach(), policy_loss.detach(), entropy.detach(), imp.detach().mean()
 
     # ------------------------------------------------------------------------------------------------

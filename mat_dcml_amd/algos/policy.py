@@ -134,6 +134,7 @@ class TransformerPolicy:
     def restore(self, model_dir):
         from ..utils.checkpoint import load_transformer
         load_transformer(self.transformer, model_dir)
+        mat_fused.bump_version(self.transformer)
 
     def train(self):
         self.transformer.train()

@@ -1,0 +1,505 @@
+// mat_decode_persistent — the whole MAT autoregressive action decode in ONE launch (gfx950 / CDNA4).
+//
+// Replaces the reference's rollout hot loop: L full decoder passes per env step, each re-running every row
+// (mat_src/mat/algorithms/utils/transformer_act.py:76-99, 37-75 for the "batch decision" stride mode).
+// Exactness: decoder row i depends only on shifted actions 0..i, so decoding one row (or
+// one block of rows) at a time against a KV cache of the earlier rows reproduces the full recompute.
+//
+// Work decomposition (D = 64, 2 heads x 32, n_block = NB):
+//   * one 256-thread workgroup = 4 waves owns EPW envs; its 16-row MFMA tile holds (env, row) pairs of the
+//     current pass (stochastic rollout: 1 row per env; deterministic stride mode: up to 16/EPW rows per env);
+//   * every 64x64 Linear is a 16x64x64 GEMM on v_mfma_f32_16x16x32_bf16: wave w owns output columns
+//     [16w, 16w+16); its B fragments (all 10·NB+1 decoder weight matrices) are loaded ONCE into VGPRs and stay
+//     register-resident for the whole decode (one wave per SIMD, ~170 VGPRs of weights);
+//   * activations move through LDS; the post-LN residual sums are kept in f32 and LayerNorm is fused into the
+//     NEXT GEMM's A-fragment load (each lane normalises the 16 values it feeds the MFMA, row statistics by two
+//     xor-shuffles), so no separate LN phase/barrier exists;
+//   * the self- and cross-attention K/V caches of every block live in LDS as bf16 with an XOR-swizzled 16-byte
+//     chunk order (conflict-free row gathers); attention over <= L cached rows runs on the VALU,
+//     8 lanes per (tile row, head);
+//   * the action head, availability masking, inverse-CDF categorical sampling / Normal sampling, log-probs and
+//     the next row's action-embedding token are fused into the last phase.
+// Inputs rep (encoder output, f32), ava, and the uniform / normal draws come from HBM; outputs are actions and
+// log-probs (B, L).  Numerics: bf16 MFMA operands, f32 accumulation, f32 LayerNorm / softmax / log-softmax.
+#include "common.h"
+
+using namespace mdl;
+
+struct DecParams {
+  const bf16_t* wpack;   // [(10*NB+1)][4 waves][2 ksteps][64 lanes][8]
+  const float* bias;     // [(10*NB+1)][64]
+  const float* lnp;      // [(3*NB+1)][2][64]  (ln1, ln2, ln3 per block; head LN last)
+  const float* emb;      // [n_tok][64] = LN(GELU(W_a · token)) rows: start, action 0..A-1, zero
+  const float* wh2;      // [act_dim][64]
+  const float* bh2;      // [act_dim]
+  const float* stdv;     // [act_dim]  sigmoid(log_std) * 0.5 (continuous agents)
+  const float* rep;      // [B][L][64]
+  const float* ava;      // [B][L][act_dim] or null
+  const float* rnd_u;    // [B][L]
+  const float* rnd_n;    // [B][L][act_dim]
+  float* out_a;          // [B][L]
+  float* out_lp;         // [B][L]
+  int B, L, act_dim, n_disc, stride, deterministic, epw, rmax, n_tok, tok_start, tok_zero;
+};
+
+constexpr int SP = 68;   // f32 staging row pitch (floats)
+constexpr int XP = 72;   // bf16 A staging row pitch (elements)
+
+__device__ __forceinline__ int kv_off(int b, int kind, int m, int j, int col, int epw, int L) {
+  // 64-element rows of 8 x 16-byte chunks; chunk index XOR (j & 7) spreads row gathers over all banks
+  const int chunk = (col >> 3) ^ (j & 7);
+  return ((((b * 4 + kind) * epw + m) * L + j) << 6) + (chunk << 3) + (col & 7);
+}
+
+__device__ __forceinline__ f32x4 mfma2(const bf16x8 a[2], const bf16x8 w[2], f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], w[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], w[1], acc, 0, 0, 0);
+  return acc;
+}
+
+__device__ __forceinline__ bf16x8 pack8(const float* v) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (short)f2bf(v[j]);
+  return r;
+}
+
+// A fragment from an f32 LDS row with fused LayerNorm.  Lane (g = lane>>4, r = lane&15) owns row r, columns
+// 8g..8g+7 and 32+8g..32+8g+7.  xf receives the normalised f32 values (for the residual copy).
+__device__ __forceinline__ void afrag_ln(const float* S, const float* gam, const float* bet, int lane,
+                                        bf16x8 a[2], float xf[16]) {
+  const int g = lane >> 4, r = lane & 15;
+  const float* row = S + r * SP;
+  float v[16];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { v[j] = row[8 * g + j]; v[8 + j] = row[32 + 8 * g + j]; }
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) s += v[j];
+  s += __shfl_xor(s, 16, 64);
+  s += __shfl_xor(s, 32, 64);
+  const float mean = s * (1.f / 64.f);
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) { const float d = v[j] - mean; q += d * d; }
+  q += __shfl_xor(q, 16, 64);
+  q += __shfl_xor(q, 32, 64);
+  const float rstd = rsqrtf(q * (1.f / 64.f) + 1e-5f);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c0 = 8 * g + j, c1 = 32 + 8 * g + j;
+    xf[j] = (v[j] - mean) * rstd * gam[c0] + bet[c0];
+    xf[8 + j] = (v[8 + j] - mean) * rstd * gam[c1] + bet[c1];
+  }
+  a[0] = pack8(xf);
+  a[1] = pack8(xf + 8);
+}
+
+// A fragment from an f32 row pointer (per lane) without normalisation
+__device__ __forceinline__ void afrag_rowf(const float* row, int lane, bf16x8 a[2], float xf[16]) {
+  const int g = lane >> 4;
+  if (row) {
+    const float4* p0 = (const float4*)(row + 8 * g);
+    const float4* p1 = (const float4*)(row + 32 + 8 * g);
+    float4 x0 = p0[0], x1 = p0[1], y0 = p1[0], y1 = p1[1];
+    xf[0] = x0.x; xf[1] = x0.y; xf[2] = x0.z; xf[3] = x0.w; xf[4] = x1.x; xf[5] = x1.y; xf[6] = x1.z; xf[7] = x1.w;
+    xf[8] = y0.x; xf[9] = y0.y; xf[10] = y0.z; xf[11] = y0.w; xf[12] = y1.x; xf[13] = y1.y; xf[14] = y1.z; xf[15] = y1.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) xf[j] = 0.f;
+  }
+  a[0] = pack8(xf);
+  a[1] = pack8(xf + 8);
+}
+
+__device__ __forceinline__ void afrag_xa(const bf16_t* XA, int lane, bf16x8 a[2]) {
+  const int g = lane >> 4, r = lane & 15;
+  a[0] = *(const bf16x8*)(XA + r * XP + 8 * g);
+  a[1] = *(const bf16x8*)(XA + r * XP + 32 + 8 * g);
+}
+
+// write the normalised/raw f32 A-row values of this lane back to an f32 LDS staging buffer (row r, its cols)
+__device__ __forceinline__ void store_xf(float* X, int lane, const float xf[16]) {
+  const int g = lane >> 4, r = lane & 15;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { X[r * SP + 8 * g + j] = xf[j]; X[r * SP + 32 + 8 * g + j] = xf[8 + j]; }
+}
+
+
+// Causal attention of the pass's tile rows over cached rows 0..i of their env.  8 lanes per (tile row, head):
+// lanes stride over key rows for the scores, then each lane produces 4 of the head's 32 output dims.
+__device__ __forceinline__ void attention_phase(const bf16_t* KV, const float* Q, float* PR, bf16_t* XA,
+                                                const int* ROWI, int R, int EPW, int L, int b, int kind,
+                                                float scale, int tid) {
+  const int pair = tid >> 3, u = tid & 7;
+  const int t = pair >> 1, h = pair & 1;
+  const int i = ROWI[t];
+  const int m = t / R;
+  float* pr = PR + (t * 2 + h) * L;
+  float mx = -INFINITY;
+  if (i >= 0) {
+    float q[32];
+#pragma unroll
+    for (int d = 0; d < 32; ++d) q[d] = Q[t * SP + 32 * h + d];
+    for (int j = u; j <= i; j += 8) {
+      const bf16_t* krow = KV + kv_off(b, kind, m, j, 0, EPW, L) - ((0 ^ (j & 7)) << 3);  // row base
+      float dot = 0.f;
+#pragma unroll
+      for (int lc = 0; lc < 4; ++lc) {
+        const int pc = (4 * h + lc) ^ (j & 7);
+        const bf16x8 kv8 = *(const bf16x8*)(krow + pc * 8);
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) dot += q[lc * 8 + jj] * bf2f((bf16_t)kv8[jj]);
+      }
+      const float sc = dot * scale;
+      pr[j] = sc;
+      mx = fmaxf(mx, sc);
+    }
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 4, 64));
+  float sum = 0.f;
+  if (i >= 0) {
+    for (int j = u; j <= i; j += 8) {
+      const float pj = __expf(pr[j] - mx);
+      pr[j] = pj;
+      sum += pj;
+    }
+  }
+  sum += __shfl_xor(sum, 1, 64);
+  sum += __shfl_xor(sum, 2, 64);
+  sum += __shfl_xor(sum, 4, 64);
+  __syncthreads();
+  bf16_t* xa = XA + t * XP + 32 * h + 4 * u;
+  if (i >= 0) {
+    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
+    const int lc = 4 * h + (u >> 1), off = 4 * (u & 1);
+    for (int j = 0; j <= i; ++j) {
+      const float pj = pr[j];
+      const bf16_t* vrow = KV + kv_off(b, kind + 1, m, j, 0, EPW, L) - ((0 ^ (j & 7)) << 3);
+      const uint2 v4 = *(const uint2*)(vrow + ((lc ^ (j & 7)) << 3) + off);
+      acc0 += pj * __uint_as_float(v4.x << 16);
+      acc1 += pj * __uint_as_float(v4.x & 0xFFFF0000u);
+      acc2 += pj * __uint_as_float(v4.y << 16);
+      acc3 += pj * __uint_as_float(v4.y & 0xFFFF0000u);
+    }
+    const float inv = 1.f / sum;
+    xa[0] = f2bf(acc0 * inv); xa[1] = f2bf(acc1 * inv); xa[2] = f2bf(acc2 * inv); xa[3] = f2bf(acc3 * inv);
+  } else {
+    xa[0] = 0; xa[1] = 0; xa[2] = 0; xa[3] = 0;
+  }
+}
+
+// Action head: LN(head1 output) · W_h2 + b -> logits; availability mask, sampling, log-prob (16 lanes per row).
+__device__ __forceinline__ void head_phase(const DecParams& p, const float* H1, float* LG, const float* lnh,
+                                           const int* ROWI, int* PEND, int R, int s, int e, int env0, int tid) {
+  const int t = tid >> 4, q = tid & 15;
+  const int i = ROWI[t];
+  const int AD = p.act_dim, L = p.L;
+  float v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] = H1[t * SP + 4 * q + k];
+  float sm = v[0] + v[1] + v[2] + v[3];
+  sm += __shfl_xor(sm, 1, 64); sm += __shfl_xor(sm, 2, 64); sm += __shfl_xor(sm, 4, 64); sm += __shfl_xor(sm, 8, 64);
+  const float mean = sm * (1.f / 64.f);
+  float sq = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) { const float d = v[k] - mean; sq += d * d; }
+  sq += __shfl_xor(sq, 1, 64); sq += __shfl_xor(sq, 2, 64); sq += __shfl_xor(sq, 4, 64); sq += __shfl_xor(sq, 8, 64);
+  const float rstd = rsqrtf(sq * (1.f / 64.f) + 1e-5f);
+  float hn[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) hn[k] = (v[k] - mean) * rstd * lnh[4 * q + k] + lnh[64 + 4 * q + k];
+  for (int a = 0; a < AD; ++a) {
+    const float* w = p.wh2 + a * 64 + 4 * q;
+    float part = w[0] * hn[0] + w[1] * hn[1] + w[2] * hn[2] + w[3] * hn[3];
+    part += __shfl_xor(part, 1, 64); part += __shfl_xor(part, 2, 64);
+    part += __shfl_xor(part, 4, 64); part += __shfl_xor(part, 8, 64);
+    if (q == 0) LG[t * SP + a] = part + p.bh2[a];
+  }
+  if (q != 0 || i < 0 || i < s || i >= e) return;
+  const int m = t / R, env = env0 + m;
+  const float* lg = LG + t * SP;
+  const size_t oi = (size_t)env * L + i;
+  if (i < p.n_disc) {
+    const float* av = p.ava ? p.ava + oi * AD : nullptr;
+    float mx = -INFINITY;
+    int amax = 0;
+    for (int a = 0; a < AD; ++a) {
+      const float l = (av && av[a] == 0.f) ? -1e10f : lg[a];
+      if (l > mx) { mx = l; amax = a; }
+    }
+    float se = 0.f;
+    for (int a = 0; a < AD; ++a) se += __expf(((av && av[a] == 0.f) ? -1e10f : lg[a]) - mx);
+    const float lse = mx + __logf(se);
+    int act = amax;
+    if (!p.deterministic) {
+      const float uu = p.rnd_u[oi];
+      float cdf = 0.f;
+      int cnt = 0;
+      for (int a = 0; a < AD; ++a) {
+        cdf += __expf(((av && av[a] == 0.f) ? -1e10f : lg[a]) - lse);
+        cnt += cdf < uu;
+      }
+      act = min(cnt, AD - 1);
+    }
+    const float la = (av && av[act] == 0.f) ? -1e10f : lg[act];
+    p.out_a[oi] = (float)act;
+    p.out_lp[oi] = la - lse;
+    PEND[m * L + i] = act;
+  } else {
+    const int a = AD - 1;
+    const float mean_a = lg[a], sd = p.stdv[a];
+    const float x = p.deterministic ? mean_a : mean_a + sd * p.rnd_n[oi * AD + a];
+    const float z = (x - mean_a) / sd;
+    p.out_a[oi] = x;
+    p.out_lp[oi] = -0.5f * z * z - __logf(sd) - 0.91893853320467274f;
+    PEND[m * L + i] = -1;
+  }
+}
+
+template <int NB>
+__global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NG = 10 * NB + 1;
+  constexpr int NLN = 3 * NB + 1;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g4 = lane >> 4, c16 = lane & 15;
+  const int EPW = p.epw, L = p.L, AD = p.act_dim;
+  const int env0 = blockIdx.x * EPW;
+  const int n_env = min(EPW, p.B - env0);
+  const int RMAX = p.rmax;
+
+  // ---------------------------------------------------------------- LDS carve (16-byte aligned pieces)
+  const size_t kv_elems = (size_t)NB * 4 * EPW * L * 64;
+  bf16_t* KV = (bf16_t*)smem;
+  char* ptr = smem + ((kv_elems * 2 + 15) & ~(size_t)15);
+  float* S = (float*)ptr;   ptr += 16 * SP * 4;
+  float* Q = (float*)ptr;   ptr += 16 * SP * 4;
+  float* XR = (float*)ptr;  ptr += 16 * SP * 4;
+  bf16_t* XA = (bf16_t*)ptr; ptr += 16 * XP * 2;
+  float* LNP = (float*)ptr; ptr += NLN * 128 * 4;
+  float* PR = (float*)ptr;  ptr += ((EPW * RMAX * 2 * L * 4 + 15) & ~15);
+  int* TOK = (int*)ptr;     ptr += ((EPW * L * 4 + 15) & ~15);
+  int* PEND = (int*)ptr;    ptr += ((EPW * L * 4 + 15) & ~15);
+  int* ROWI = (int*)ptr;    ptr += 16 * 4;
+
+  // ---------------------------------------------------------------- one-time loads
+  bf16x8 wb[NG][2];
+#pragma unroll
+  for (int gi = 0; gi < NG; ++gi) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      wb[gi][ks] = *(const bf16x8*)(p.wpack + ((size_t)((gi * 4 + wave) * 2 + ks) * 64 + lane) * 8);
+  }
+  float bcol[NG];
+#pragma unroll
+  for (int gi = 0; gi < NG; ++gi) bcol[gi] = p.bias[gi * 64 + 16 * wave + c16];
+  for (int i = tid; i < NLN * 128; i += 256) LNP[i] = p.lnp[i];
+  for (int i = tid; i < EPW * L; i += 256) { TOK[i] = (i % L == 0) ? p.tok_start : p.tok_zero; PEND[i] = -1; }
+  __syncthreads();
+
+  const float scale = 0.17677669529663687f;  // 1/sqrt(32)
+
+  // ---------------------------------------------------------------- block schedule (transformer_act.py:37-75)
+  int prev_s = -1, s = 0, e = 1;
+  while (true) {
+    int lo = prev_s >= 0 ? prev_s + 1 : 0;
+    if (lo > s) lo = s;
+    for (int plo = lo; plo < e; plo += RMAX) {
+      const int R = min(RMAX, e - plo);
+      if (tid < 16) {
+        const int m = tid / R, rr = tid % R;
+        ROWI[tid] = (m < n_env && rr < R && tid < EPW * R) ? plo + rr : -1;
+      }
+      __syncthreads();
+      // per-lane tile rows for the C layout (rows 4*g4 + r) and the A layout (row c16)
+      int crow_i[4], crow_m[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { crow_i[r] = ROWI[4 * g4 + r]; crow_m[r] = (4 * g4 + r) / R; }
+      const int arow_i = ROWI[c16], arow_m = c16 / R;
+
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        bf16x8 a[2];
+        float xf[16];
+        // ---------------- [A] x = emb(token) (b == 0) or LN3(S) ; q1, k1, v1
+        if (b == 0) {
+          const float* row = nullptr;
+          if (arow_i >= 0) row = p.emb + (size_t)TOK[arow_m * L + arow_i] * 64;
+          afrag_rowf(row, lane, a, xf);
+        } else {
+          afrag_ln(S, LNP + (3 * (b - 1) + 2) * 128, LNP + (3 * (b - 1) + 2) * 128 + 64, lane, a, xf);
+        }
+        if (wave == 0) store_xf(XR, lane, xf);
+        {
+          f32x4 q1 = mfma2(a, wb[b * 10 + 0], f32x4{0, 0, 0, 0});
+          f32x4 k1 = mfma2(a, wb[b * 10 + 1], f32x4{0, 0, 0, 0});
+          f32x4 v1 = mfma2(a, wb[b * 10 + 2], f32x4{0, 0, 0, 0});
+          const int col = 16 * wave + c16;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = 4 * g4 + r;
+            Q[row * SP + col] = q1[r] + bcol[b * 10 + 0];
+            if (crow_i[r] >= 0) {
+              KV[kv_off(b, 0, crow_m[r], crow_i[r], col, EPW, L)] = f2bf(k1[r] + bcol[b * 10 + 1]);
+              KV[kv_off(b, 1, crow_m[r], crow_i[r], col, EPW, L)] = f2bf(v1[r] + bcol[b * 10 + 2]);
+            }
+          }
+        }
+        __syncthreads();
+        // ---------------- [B] causal self-attention over cached rows 0..i
+        attention_phase(KV, Q, PR, XA, ROWI, R, EPW, L, b, 0, scale, tid);
+        __syncthreads();
+        // ---------------- [C] proj1 + bias + residual x -> S
+        afrag_xa(XA, lane, a);
+        {
+          f32x4 acc = mfma2(a, wb[b * 10 + 3], f32x4{0, 0, 0, 0});
+          const int col = 16 * wave + c16;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = 4 * g4 + r;
+            S[row * SP + col] = acc[r] + bcol[b * 10 + 3] + XR[row * SP + col];
+          }
+        }
+        __syncthreads();
+        // ---------------- [D] x1 = LN1(S); k2, v2 from x1; q2 from rep_i
+        afrag_ln(S, LNP + (3 * b + 0) * 128, LNP + (3 * b + 0) * 128 + 64, lane, a, xf);
+        {
+          bf16x8 ar[2];
+          float rf[16];
+          const float* rrow = arow_i >= 0 ? p.rep + ((size_t)(env0 + arow_m) * L + arow_i) * 64 : nullptr;
+          afrag_rowf(rrow, lane, ar, rf);
+          f32x4 k2 = mfma2(a, wb[b * 10 + 5], f32x4{0, 0, 0, 0});
+          f32x4 v2 = mfma2(a, wb[b * 10 + 6], f32x4{0, 0, 0, 0});
+          f32x4 q2 = mfma2(ar, wb[b * 10 + 4], f32x4{0, 0, 0, 0});
+          const int col = 16 * wave + c16;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = 4 * g4 + r;
+            Q[row * SP + col] = q2[r] + bcol[b * 10 + 4];
+            if (crow_i[r] >= 0) {
+              KV[kv_off(b, 2, crow_m[r], crow_i[r], col, EPW, L)] = f2bf(k2[r] + bcol[b * 10 + 5]);
+              KV[kv_off(b, 3, crow_m[r], crow_i[r], col, EPW, L)] = f2bf(v2[r] + bcol[b * 10 + 6]);
+            }
+          }
+        }
+        __syncthreads();
+        // ---------------- [E] causal cross-attention (q = rep rows, k/v = x1 rows)
+        attention_phase(KV, Q, PR, XA, ROWI, R, EPW, L, b, 2, scale, tid);
+        __syncthreads();
+        // ---------------- [F] proj2 + bias + rep_i -> S
+        afrag_xa(XA, lane, a);
+        {
+          f32x4 acc = mfma2(a, wb[b * 10 + 7], f32x4{0, 0, 0, 0});
+          const int col = 16 * wave + c16;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = 4 * g4 + r;
+            float res = 0.f;
+            if (crow_i[r] >= 0) res = p.rep[((size_t)(env0 + crow_m[r]) * L + crow_i[r]) * 64 + col];
+            S[row * SP + col] = acc[r] + bcol[b * 10 + 7] + res;
+          }
+        }
+        __syncthreads();
+        // ---------------- [G] x2 = LN2(S) -> XR ; h = GELU(mlp1(x2)) -> XA
+        afrag_ln(S, LNP + (3 * b + 1) * 128, LNP + (3 * b + 1) * 128 + 64, lane, a, xf);
+        if (wave == 0) store_xf(XR, lane, xf);
+        {
+          f32x4 acc = mfma2(a, wb[b * 10 + 8], f32x4{0, 0, 0, 0});
+          const int col = 16 * wave + c16;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) XA[(4 * g4 + r) * XP + col] = f2bf(gelu_erf(acc[r] + bcol[b * 10 + 8]));
+        }
+        __syncthreads();
+        // ---------------- [H] mlp2 + bias + residual x2 -> S
+        afrag_xa(XA, lane, a);
+        {
+          f32x4 acc = mfma2(a, wb[b * 10 + 9], f32x4{0, 0, 0, 0});
+          const int col = 16 * wave + c16;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = 4 * g4 + r;
+            S[row * SP + col] = acc[r] + bcol[b * 10 + 9] + XR[row * SP + col];
+          }
+        }
+        __syncthreads();
+      }
+      // ---------------- [I] head1: GELU(W_h1 · LN3(S) + b) -> Q (f32 staging)
+      {
+        bf16x8 a[2];
+        float xf[16];
+        afrag_ln(S, LNP + (3 * (NB - 1) + 2) * 128, LNP + (3 * (NB - 1) + 2) * 128 + 64, lane, a, xf);
+        f32x4 acc = mfma2(a, wb[NG - 1], f32x4{0, 0, 0, 0});
+        const int col = 16 * wave + c16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Q[(4 * g4 + r) * SP + col] = gelu_erf(acc[r] + bcol[NG - 1]);
+      }
+      __syncthreads();
+      // ---------------- [J] head LN + W_h2 -> logits; mask, sample, log-prob; record pending tokens
+      head_phase(p, Q, S, LNP + 3 * NB * 128, ROWI, PEND, R, s, e, env0, tid);
+      __syncthreads();
+    }
+    // apply the block's actions to the token rows of the next passes (in-block rows kept at zero, as the reference)
+    for (int idx = tid; idx < n_env * L; idx += 256) {
+      const int m = idx / L, i = idx % L;
+      if (i >= s && i < e) {
+        const int a = PEND[m * L + i];
+        if (a >= 0 && i + 1 < L) TOK[m * L + i + 1] = 1 + a;
+      }
+    }
+    __syncthreads();
+    prev_s = s;
+    if (e >= L) break;
+    if (e < p.n_disc) { s = e; e = min(e + p.stride, p.n_disc); }
+    else { s = e; e = min(e + 1, L); }
+  }
+}
+
+size_t mat_decode_lds_bytes(int NB, int epw, int rmax, int L) {
+  size_t kv = (size_t)NB * 4 * epw * L * 64 * 2;
+  kv = (kv + 15) & ~(size_t)15;
+  size_t rest = 3 * 16 * SP * 4 + 16 * XP * 2 + (3 * NB + 1) * 128 * 4 + ((epw * rmax * 2 * L * 4 + 15) & ~15) +
+                2 * ((epw * L * 4 + 15) & ~15) + 16 * 4;
+  return kv + rest;
+}
+
+// Tile geometry: EPW envs per workgroup (largest power of two <= min(16, B) that fits the 160 KiB LDS of a CU
+// with one row per env), then RMAX rows per env per pass (largest <= 16/EPW that still fits).
+// Returns EPW | (RMAX << 8), or 0 if even one env does not fit.
+MDL_API int mdl_mat_decode_geometry(int NB, int L, int B) {
+  int cap = 16;
+  while (cap > 1 && cap > B) cap >>= 1;
+  for (int epw = cap; epw >= 1; epw >>= 1) {
+    if (mat_decode_lds_bytes(NB, epw, 1, L) <= 160 * 1024) {
+      int rmax = 16 / epw;
+      while (rmax > 1 && mat_decode_lds_bytes(NB, epw, rmax, L) > 160 * 1024) --rmax;
+      return epw | (rmax << 8);
+    }
+  }
+  return 0;
+}
+
+MDL_API int mdl_mat_decode(const DecParams* p, int NB, hipStream_t st) {
+  const int epw = p->epw;
+  if (epw <= 0 || p->act_dim > 64 || p->act_dim < 1) return -1;
+  if (p->rmax < 1 || p->rmax * epw > 16) return -4;
+  const size_t lds = mat_decode_lds_bytes(NB, epw, p->rmax, p->L);
+  if (lds > 160 * 1024) return -2;
+  const int grid = (p->B + epw - 1) / epw;
+  switch (NB) {
+    case 1:
+      hipFuncSetAttribute((const void*)mat_decode_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(mat_decode_kernel<1>, dim3(grid), dim3(256), lds, st, *p); break;
+    case 2:
+      hipFuncSetAttribute((const void*)mat_decode_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(mat_decode_kernel<2>, dim3(grid), dim3(256), lds, st, *p); break;
+    case 3:
+      hipFuncSetAttribute((const void*)mat_decode_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(mat_decode_kernel<3>, dim3(grid), dim3(256), lds, st, *p); break;
+    default: return -3;
+  }
+  MDL_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,5 +1,140 @@
-"""Fused HIP MAT kernels (placeholder)."""
+"""Fused HIP MAT paths (gfx950): persistent autoregressive decode (+ fused encoder later in this module).
+
+``get_actions`` runs the MAT rollout policy step as:
+  1. the encoder (values + obs representations),
+  2. ONE ``mat_decode_persistent`` launch (``csrc/mat_decode.hip``) that decodes all L agents of all envs:
+     register-resident decoder weights, LDS KV caches, fused head + masking + sampling + log-probs.
+Weights are repacked into the kernel's MFMA B-fragment order once per optimizer step (cached on the model
+and keyed by ``model._mdl_version``, bumped by the trainer after every update).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import kernels
+from .kernels import P, check, lib, sig
+
+vp, i32 = ctypes.c_void_p, ctypes.c_int
 
 
-def supports(model):
-    return False
+class DecParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("wpack", "bias", "lnp", "emb", "wh2", "bh2", "stdv", "rep", "ava",
+                                               "rnd_u", "rnd_n", "out_a", "out_lp")] + \
+               [(n, ctypes.c_int) for n in ("B", "L", "act_dim", "n_disc", "stride", "deterministic", "epw", "rmax", "n_tok",
+                                            "tok_start", "tok_zero")]
+
+
+sig("mdl_mat_decode", ctypes.POINTER(DecParams), i32, vp)
+sig("mdl_mat_decode_geometry", i32, i32, i32)
+
+
+def _n_disc(model, L):
+    if model.action_type == "Discrete":
+        return L
+    return L + model.semi_index if model.semi_index < 0 else model.semi_index
+
+
+def supports(model, L=None) -> bool:
+    if not kernels.available():
+        return False
+    if model.action_type not in ("Semi_Discrete", "Discrete") or model.decoder.dec_actor:
+        return False
+    if model.n_embd != 64 or model.n_head != 2 or model.n_block not in (1, 2, 3) or model.action_dim > 64:
+        return False
+    if model.action_type == "Semi_Discrete" and model.semi_index != -1:
+        return False
+    L = L or model.n_agent
+    return lib().mdl_mat_decode_geometry(model.n_block, L, 1) > 0
+
+
+def bump_version(model):
+    model._mdl_version = getattr(model, "_mdl_version", 0) + 1
+
+
+def _bfrag(W):
+    """torch Linear weight (64 out, 64 in) -> [4 waves][2 ksteps][64 lanes][8] bf16 (lane = 16*(k//8 % 4) + n%16)."""
+    return W.detach().reshape(4, 16, 2, 4, 8).permute(0, 2, 3, 1, 4).contiguous().to(torch.bfloat16)
+
+
+@torch.no_grad()
+def decoder_pack(model):
+    ver = getattr(model, "_mdl_version", 0)
+    cache = getattr(model, "_mdl_dec_pack", None)
+    if cache is not None and cache[0] == ver:
+        return cache[1]
+    dec = model.decoder
+    mats, biases, lns = [], [], []
+    for blk in dec.blocks:
+        a1, a2 = blk.attn1, blk.attn2
+        for lin in (a1.query, a1.key, a1.value, a1.proj, a2.query, a2.key, a2.value, a2.proj, blk.mlp[0], blk.mlp[2]):
+            mats.append(_bfrag(lin.weight))
+            biases.append(lin.bias.detach().float())
+        for ln in (blk.ln1, blk.ln2, blk.ln3):
+            lns.append(torch.stack([ln.weight.detach().float(), ln.bias.detach().float()]))
+    mats.append(_bfrag(dec.head[0].weight))
+    biases.append(dec.head[0].bias.detach().float())
+    lns.append(torch.stack([dec.head[2].weight.detach().float(), dec.head[2].bias.detach().float()]))
+    A = model.action_dim
+    dev = dec.ln.weight.device
+    # token table: 0 = start [1,0..], 1+a = one-hot action a, A+1 = zero row (in-block rows of the stride mode)
+    toks = torch.zeros(A + 2, A + 1, device=dev)
+    toks[0, 0] = 1
+    toks[torch.arange(1, A + 1), torch.arange(1, A + 1)] = 1
+    emb = dec.ln(dec.action_encoder(toks)).float()
+    std = model.action_std().float() if model.action_type != "Discrete" else torch.ones(A, device=dev)
+    pack = dict(wpack=torch.stack(mats).contiguous(), bias=torch.stack(biases).contiguous(),
+                lnp=torch.stack(lns).contiguous(), emb=emb.contiguous(),
+                wh2=dec.head[3].weight.detach().float().contiguous(), bh2=dec.head[3].bias.detach().float().contiguous(),
+                stdv=std.contiguous(), n_tok=A + 2)
+    model._mdl_dec_pack = (ver, pack)
+    return pack
+
+
+def decode(model, rep, ava=None, deterministic=False, stride=1, rand=None):
+    """rep (B, L, 64) f32 -> actions (B, L, 1), log-probs (B, L, 1)."""
+    B, L, D = rep.shape
+    A = model.action_dim
+    pk = decoder_pack(model)
+    rep = rep.float().contiguous()
+    dev = rep.device
+    if rand is None and not deterministic:
+        rand = {"u": torch.rand(B, L, device=dev), "n": torch.randn(B, L, A, device=dev)}
+    u = rand["u"].float().contiguous() if rand is not None else None
+    n = rand["n"].float().contiguous() if rand is not None else None
+    ava_c = ava.float().contiguous() if ava is not None else None
+    out_a = torch.empty(B, L, device=dev)
+    out_lp = torch.empty(B, L, device=dev)
+    geo = lib().mdl_mat_decode_geometry(model.n_block, L, B)
+    epw, rmax = geo & 0xFF, geo >> 8
+    if epw <= 0:
+        raise RuntimeError(f"mat_decode: L={L} does not fit in LDS")
+    prm = DecParams(P(pk["wpack"]).value, P(pk["bias"]).value, P(pk["lnp"]).value, P(pk["emb"]).value,
+                    P(pk["wh2"]).value, P(pk["bh2"]).value, P(pk["stdv"]).value, P(rep).value, P(ava_c).value,
+                    P(u).value, P(n).value, P(out_a).value, P(out_lp).value,
+                    B, L, A, _n_disc(model, L), int(stride if deterministic else 1), int(bool(deterministic)), epw, rmax,
+                    pk["n_tok"], 0, A + 1)
+    check(lib().mdl_mat_decode(ctypes.byref(prm), model.n_block, kernels._stream()), "mat_decode")
+    return out_a.unsqueeze(-1), out_lp.unsqueeze(-1)
+
+
+def get_actions(model, obs, ava=None, deterministic=False, stride=1, rand=None):
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        v, rep = model.encoder(None, obs)
+    a, lp = decode(model, rep.float(), ava, deterministic, stride, rand)
+    return v.float(), a, lp
+
+
+def get_values(model, obs):
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        v, _ = model.encoder(None, obs)
+    return v.float()
+
+
+def evaluate_actions(model, obs, actions, ava=None):
+    from ..models import act as act_mod
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        v, rep = model.encoder(None, obs)
+        logp, ent = act_mod.parallel_act(model, rep, obs, actions, ava)
+    return v.float(), logp, ent

@@ -1,0 +1,92 @@
+"""Persistent HIP decode kernel vs the PyTorch fp32 autoregressive decode (same random draws)."""
+import pytest
+import torch
+
+from mat_dcml_amd.models import act
+from mat_dcml_amd.models.mat import MultiAgentTransformer
+from mat_dcml_amd.ops import mat_fused
+
+pytestmark = pytest.mark.gpu
+
+
+def make(L, dev, atype="Semi_Discrete", A=2, seed=0, scale=0.3, nb=2):
+    torch.manual_seed(seed)
+    m = MultiAgentTransformer(L + 1, 7, A, L, nb, 64, 2, action_type=atype, semi_index=-1).to(dev)
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_((torch.randn(p.shape, generator=g) * scale).to(dev))
+    return m
+
+
+def inputs(m, B, L, dev, A=2, seed=1):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    obs = torch.rand(B, L, 7, device=dev, generator=g)
+    ava = torch.ones(B, L, A, device=dev)
+    ava[:, 1::3, -1] = 0
+    with torch.no_grad():
+        v, rep = m.encoder(None, obs)
+    rand = {"u": torch.rand(B, L, device=dev, generator=g), "n": torch.randn(B, L, A, device=dev, generator=g)}
+    return obs, ava, rep, rand
+
+
+@pytest.mark.parametrize("L,B", [(33, 256), (5, 64), (101, 16), (129, 8), (33, 3)])
+@pytest.mark.parametrize("det", [False, True])
+def test_decode_matches_torch(gpu, L, B, det):
+    m = make(L, gpu)
+    assert mat_fused.supports(m)
+    obs, ava, rep, rand = inputs(m, B, L, gpu)
+    a_ref, lp_ref = act.autoregressive_act(m, rep, obs, ava, det, 1, rand)
+    a_k, lp_k = mat_fused.decode(m, rep, ava, det, 1, rand)
+    torch.cuda.synchronize()
+    disc = slice(0, L - 1)
+    agree = (a_ref[:, disc] == a_k[:, disc]).float().mean().item()
+    assert agree > 0.97, agree
+    assert (a_k[:, disc][ava[:, disc, 1:] == 0] == 0).all()  # masked workers never selected
+    # kernel log-probs are the teacher-forced log-probs of the kernel's own actions
+    with torch.no_grad():
+        lp_tf, _ = act.parallel_act(m, rep, obs, a_k, ava)
+    err = (lp_tf - lp_k).abs()
+    assert err.mean().item() < 2e-2 and err.max().item() < 0.2, (err.mean().item(), err.max().item())
+    if det:
+        assert torch.allclose(a_ref[:, -1], a_k[:, -1], atol=5e-2)
+
+
+@pytest.mark.parametrize("stride", [2, 10])
+def test_decode_stride_mode(gpu, stride):
+    L, B = 101, 4
+    m = make(L, gpu, seed=3)
+    obs, ava, rep, rand = inputs(m, B, L, gpu)
+    a_ref, lp_ref = act.autoregressive_act(m, rep, obs, ava, True, stride, None)
+    a_k, lp_k = mat_fused.decode(m, rep, ava, True, stride, None)
+    agree = (a_ref[:, :-1] == a_k[:, :-1]).float().mean().item()
+    assert agree > 0.97, agree
+    assert (lp_ref - lp_k).abs().mean().item() < 3e-2
+
+
+def test_decode_discrete_smac_shape(gpu):
+    L, B, A = 27, 32, 36
+    m = make(L, gpu, atype="Discrete", A=A, seed=5)
+    obs, ava, rep, rand = inputs(m, B, L, gpu, A=A)
+    a_ref, _ = act.autoregressive_act(m, rep, obs, ava, False, 1, rand)
+    a_k, lp_k = mat_fused.decode(m, rep, ava, False, 1, rand)
+    assert (a_ref == a_k).float().mean().item() > 0.95
+    with torch.no_grad():
+        lp_tf, _ = act.parallel_act(m, rep, obs, a_k, ava)
+    assert (lp_tf - lp_k).abs().mean().item() < 3e-2
+
+
+def test_decode_latency(gpu):
+    L, B = 33, 256
+    m = make(L, gpu)
+    obs, ava, rep, rand = inputs(m, B, L, gpu)
+    for _ in range(3):
+        mat_fused.decode(m, rep, ava, False, 1, rand)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(20):
+        mat_fused.decode(m, rep, ava, False, 1, rand)
+    e.record()
+    torch.cuda.synchronize()
+    print(f"mat_decode B=256 L=33: {s.elapsed_time(e) / 20 * 1e3:.1f} us per env step")
