@@ -24,6 +24,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.linear import Linear
+
 NORMAL_STD = 0.5  # transformer_act.py:6
 
 
@@ -44,10 +46,10 @@ class SelfAttention(nn.Module):
         assert n_embd % n_head == 0
         self.masked = masked
         self.n_head = n_head
-        self.key = _init(nn.Linear(n_embd, n_embd))
-        self.query = _init(nn.Linear(n_embd, n_embd))
-        self.value = _init(nn.Linear(n_embd, n_embd))
-        self.proj = _init(nn.Linear(n_embd, n_embd))
+        self.key = _init(Linear(n_embd, n_embd))
+        self.query = _init(Linear(n_embd, n_embd))
+        self.value = _init(Linear(n_embd, n_embd))
+        self.proj = _init(Linear(n_embd, n_embd))
         self.register_buffer("mask", torch.tril(torch.ones(n_agent + 1, n_agent + 1)).view(1, 1, n_agent + 1, n_agent + 1))
 
     def forward(self, key, value, query):
@@ -71,8 +73,8 @@ class EncodeBlock(nn.Module):
         self.ln1 = nn.LayerNorm(n_embd)
         self.ln2 = nn.LayerNorm(n_embd)
         self.attn = SelfAttention(n_embd, n_head, n_agent, masked=False)
-        self.mlp = nn.Sequential(_init(nn.Linear(n_embd, n_embd), activate=True), nn.GELU(),
-                                 _init(nn.Linear(n_embd, n_embd)))
+        self.mlp = nn.Sequential(_init(Linear(n_embd, n_embd), activate=True), nn.GELU(),
+                                 _init(Linear(n_embd, n_embd)))
 
     def forward(self, x):
         x = self.ln1(x + self.attn(x, x, x))
@@ -87,8 +89,8 @@ class DecodeBlock(nn.Module):
         self.ln3 = nn.LayerNorm(n_embd)
         self.attn1 = SelfAttention(n_embd, n_head, n_agent, masked=True)
         self.attn2 = SelfAttention(n_embd, n_head, n_agent, masked=True)
-        self.mlp = nn.Sequential(_init(nn.Linear(n_embd, n_embd), activate=True), nn.GELU(),
-                                 _init(nn.Linear(n_embd, n_embd)))
+        self.mlp = nn.Sequential(_init(Linear(n_embd, n_embd), activate=True), nn.GELU(),
+                                 _init(Linear(n_embd, n_embd)))
 
     def forward(self, x, rep_enc):
         x = self.ln1(x + self.attn1(x, x, x))
@@ -101,12 +103,12 @@ class Encoder(nn.Module):
         super().__init__()
         self.state_dim, self.obs_dim, self.n_embd, self.n_agent = state_dim, obs_dim, n_embd, n_agent
         self.encode_state = encode_state
-        self.state_encoder = nn.Sequential(nn.LayerNorm(state_dim), _init(nn.Linear(state_dim, n_embd), activate=True), nn.GELU())
-        self.obs_encoder = nn.Sequential(nn.LayerNorm(obs_dim), _init(nn.Linear(obs_dim, n_embd), activate=True), nn.GELU())
+        self.state_encoder = nn.Sequential(nn.LayerNorm(state_dim), _init(Linear(state_dim, n_embd), activate=True), nn.GELU())
+        self.obs_encoder = nn.Sequential(nn.LayerNorm(obs_dim), _init(Linear(obs_dim, n_embd), activate=True), nn.GELU())
         self.ln = nn.LayerNorm(n_embd)
         self.blocks = nn.Sequential(*[EncodeBlock(n_embd, n_head, n_agent) for _ in range(n_block)])
-        self.head = nn.Sequential(_init(nn.Linear(n_embd, n_embd), activate=True), nn.GELU(), nn.LayerNorm(n_embd),
-                                  _init(nn.Linear(n_embd, n_objective)))
+        self.head = nn.Sequential(_init(Linear(n_embd, n_embd), activate=True), nn.GELU(), nn.LayerNorm(n_embd),
+                                  _init(Linear(n_embd, n_objective)))
 
     def forward(self, state, obs):
         x = self.state_encoder(state) if self.encode_state else self.obs_encoder(obs)
@@ -124,20 +126,20 @@ class Decoder(nn.Module):
             self.log_std = nn.Parameter(torch.ones(action_dim))
         if dec_actor:
             def actor():
-                return nn.Sequential(nn.LayerNorm(obs_dim), _init(nn.Linear(obs_dim, n_embd), activate=True), nn.GELU(),
-                                     nn.LayerNorm(n_embd), _init(nn.Linear(n_embd, n_embd), activate=True), nn.GELU(),
-                                     nn.LayerNorm(n_embd), _init(nn.Linear(n_embd, action_dim)))
+                return nn.Sequential(nn.LayerNorm(obs_dim), _init(Linear(obs_dim, n_embd), activate=True), nn.GELU(),
+                                     nn.LayerNorm(n_embd), _init(Linear(n_embd, n_embd), activate=True), nn.GELU(),
+                                     nn.LayerNorm(n_embd), _init(Linear(n_embd, action_dim)))
             self.mlp = actor() if share_actor else nn.ModuleList([actor() for _ in range(n_agent)])
         else:
             if action_type in ("Discrete", "Semi_Discrete"):
-                self.action_encoder = nn.Sequential(_init(nn.Linear(action_dim + 1, n_embd, bias=False), activate=True), nn.GELU())
+                self.action_encoder = nn.Sequential(_init(Linear(action_dim + 1, n_embd, bias=False), activate=True), nn.GELU())
             else:
-                self.action_encoder = nn.Sequential(_init(nn.Linear(action_dim, n_embd), activate=True), nn.GELU())
-            self.obs_encoder = nn.Sequential(nn.LayerNorm(obs_dim), _init(nn.Linear(obs_dim, n_embd), activate=True), nn.GELU())
+                self.action_encoder = nn.Sequential(_init(Linear(action_dim, n_embd), activate=True), nn.GELU())
+            self.obs_encoder = nn.Sequential(nn.LayerNorm(obs_dim), _init(Linear(obs_dim, n_embd), activate=True), nn.GELU())
             self.ln = nn.LayerNorm(n_embd)
             self.blocks = nn.Sequential(*[DecodeBlock(n_embd, n_head, n_agent) for _ in range(n_block)])
-            self.head = nn.Sequential(_init(nn.Linear(n_embd, n_embd), activate=True), nn.GELU(), nn.LayerNorm(n_embd),
-                                      _init(nn.Linear(n_embd, action_dim)))
+            self.head = nn.Sequential(_init(Linear(n_embd, n_embd), activate=True), nn.GELU(), nn.LayerNorm(n_embd),
+                                      _init(Linear(n_embd, action_dim)))
 
     def zero_std(self):
         if self.action_type != "Discrete":

@@ -34,3 +34,18 @@ def test_train_iteration_on_gpu(gpu):
     infos = r.train_iteration()
     torch.cuda.synchronize()
     assert all(torch.isfinite(torch.as_tensor(float(v))) for v in infos.values())
+
+
+def test_splitk_linear_grad(gpu):
+    from mat_dcml_amd.ops.linear import linear
+    x = torch.randn(40000, 64, device=gpu, requires_grad=True)
+    w = torch.randn(64, 64, device=gpu, requires_grad=True)
+    b = torch.randn(64, device=gpu, requires_grad=True)
+    y = linear(x, w, b)
+    g = torch.randn_like(y)
+    y.backward(g)
+    x2, w2, b2 = x.detach().clone().requires_grad_(), w.detach().clone().requires_grad_(), b.detach().clone().requires_grad_()
+    torch.nn.functional.linear(x2, w2, b2).backward(g)
+    assert torch.allclose(x.grad, x2.grad, rtol=1e-3, atol=1e-2)
+    assert torch.allclose(w.grad, w2.grad, rtol=1e-3, atol=1e-1)
+    assert torch.allclose(b.grad, b2.grad, rtol=1e-3, atol=1e-2)
