@@ -93,11 +93,20 @@ class MATTrainer:
             policy_loss = -torch.min(surr1, surr2).sum(-1, keepdim=True).mean()
         value_loss = self.cal_value_loss(values, mb["value_preds"], mb["returns"], act)
         loss = policy_loss - entropy * self.entropy_coef + value_loss * self.value_loss_coef
-        pol.optimizer.zero_grad(set_to_none=False)
+        flat = self.comm._flat if self.comm is not None else None
+        if flat is not None:
+            flat.ensure_views()
+            flat.buf.zero_()
+        else:
+            pol.optimizer.zero_grad(set_to_none=False)
         loss.backward()
         if self.comm is not None and self.comm.world_size > 1:
             self.comm.all_reduce_grads_(self.params)
-        if self._use_max_grad_norm:
+        if flat is not None:
+            grad_norm = flat.buf.norm()
+            if self._use_max_grad_norm:   # clip_grad_norm_ semantics: scale = max / (norm + 1e-6), capped at 1
+                flat.buf.mul_(torch.clamp(self.max_grad_norm / (grad_norm + 1e-6), max=1.0))
+        elif self._use_max_grad_norm:
             grad_norm = nn.utils.clip_grad_norm_(self.params, self.max_grad_norm, foreach=True)
         else:
             grad_norm = torch.norm(torch.stack([p.grad.norm() for p in self.params if p.grad is not None]))

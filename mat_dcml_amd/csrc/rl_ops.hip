@@ -53,3 +53,25 @@ MDL_API int mdl_philox_fill(int64_t* out, int n, uint32_t c1, uint32_t c2, uint3
   MDL_CHECK_LAUNCH();
   return 0;
 }
+
+// Repack fp32 Linear weights (64 x 64, [out][in]) into the MFMA B-fragment order used by the fused kernels, for W
+// (forward) and W^T (backward) — all matrices of the model in ONE launch after each optimizer step.
+// fragment element (ct, ks, lane, j) = M[16*ct + (lane & 15)][32*ks + 8*(lane >> 4) + j]
+struct PackEnt { const float* src; unsigned short* fw; unsigned short* bw; };
+
+__global__ __launch_bounds__(256) void pack_weights_kernel(const PackEnt* tab) {
+  const PackEnt e = tab[blockIdx.x];
+  for (int idx = threadIdx.x; idx < 4096; idx += 256) {
+    const int j = idx & 7, lane = (idx >> 3) & 63, ks = (idx >> 9) & 1, ct = idx >> 10;
+    const int n = 16 * ct + (lane & 15), k = 32 * ks + 8 * (lane >> 4) + j;
+    if (e.fw) e.fw[idx] = mdl::f2bf(e.src[n * 64 + k]);
+    if (e.bw) e.bw[idx] = mdl::f2bf(e.src[k * 64 + n]);
+  }
+}
+
+MDL_API int mdl_pack_weights(const void* tab, int n, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(pack_weights_kernel, dim3(n), dim3(256), 0, s, (const PackEnt*)tab);
+  MDL_CHECK_LAUNCH();
+  return 0;
+}

@@ -53,29 +53,28 @@ def bump_version(model):
     model._mdl_version = getattr(model, "_mdl_version", 0) + 1
 
 
-def _bfrag(W):
+def _bfrag(W):  # (reference packing in torch; the kernels use csrc/rl_ops.hip:pack_weights)
     """torch Linear weight (64 out, 64 in) -> [4 waves][2 ksteps][64 lanes][8] bf16 (lane = 16*(k//8 % 4) + n%16)."""
     return W.detach().reshape(4, 16, 2, 4, 8).permute(0, 2, 3, 1, 4).contiguous().to(torch.bfloat16)
 
 
 @torch.no_grad()
 def decoder_pack(model):
+    """Decode-kernel operands: the decoder's B fragments (shared ModelPack), stacked biases / LN params and the
+    action-embedding token table, rebuilt once per optimizer step."""
+    from . import mat_train
     ver = getattr(model, "_mdl_version", 0)
     cache = getattr(model, "_mdl_dec_pack", None)
     if cache is not None and cache[0] == ver:
         return cache[1]
+    mp = mat_train.model_pack(model)
     dec = model.decoder
-    mats, biases, lns = [], [], []
+    lins = mat_train.decoder_linears(model)
+    lns = []
     for blk in dec.blocks:
-        a1, a2 = blk.attn1, blk.attn2
-        for lin in (a1.query, a1.key, a1.value, a1.proj, a2.query, a2.key, a2.value, a2.proj, blk.mlp[0], blk.mlp[2]):
-            mats.append(_bfrag(lin.weight))
-            biases.append(lin.bias.detach().float())
         for ln in (blk.ln1, blk.ln2, blk.ln3):
-            lns.append(torch.stack([ln.weight.detach().float(), ln.bias.detach().float()]))
-    mats.append(_bfrag(dec.head[0].weight))
-    biases.append(dec.head[0].bias.detach().float())
-    lns.append(torch.stack([dec.head[2].weight.detach().float(), dec.head[2].bias.detach().float()]))
+            lns.append(torch.stack([ln.weight.detach(), ln.bias.detach()]))
+    lns.append(torch.stack([dec.head[2].weight.detach(), dec.head[2].bias.detach()]))
     A = model.action_dim
     dev = dec.ln.weight.device
     # token table: 0 = start [1,0..], 1+a = one-hot action a, A+1 = zero row (in-block rows of the stride mode)
@@ -84,8 +83,8 @@ def decoder_pack(model):
     toks[torch.arange(1, A + 1), torch.arange(1, A + 1)] = 1
     emb = dec.ln(dec.action_encoder(toks)).float()
     std = model.action_std().float() if model.action_type != "Discrete" else torch.ones(A, device=dev)
-    pack = dict(wpack=torch.stack(mats).contiguous(), bias=torch.stack(biases).contiguous(),
-                lnp=torch.stack(lns).contiguous(), emb=emb.contiguous(),
+    pack = dict(wpack=mp.decoder_fw, bias=torch.stack([l.bias.detach() for l in lins]).float().contiguous(),
+                lnp=torch.stack(lns).float().contiguous(), emb=emb.contiguous(),
                 wh2=dec.head[3].weight.detach().float().contiguous(), bh2=dec.head[3].bias.detach().float().contiguous(),
                 stdv=std.contiguous(), n_tok=A + 2)
     model._mdl_dec_pack = (ver, pack)
@@ -119,20 +118,31 @@ def decode(model, rep, ava=None, deterministic=False, stride=1, rand=None):
     return out_a.unsqueeze(-1), out_lp.unsqueeze(-1)
 
 
-def get_actions(model, obs, ava=None, deterministic=False, stride=1, rand=None):
+def _encode(model, obs):
+    from . import mat_train
+    if mat_train.encoder_supported(model):
+        return mat_train.encode(model, obs)
     with torch.autocast("cuda", dtype=torch.bfloat16):
         v, rep = model.encoder(None, obs)
-    a, lp = decode(model, rep.float(), ava, deterministic, stride, rand)
-    return v.float(), a, lp
+    return v.float(), rep.float()
 
 
+@torch.no_grad()
+def get_actions(model, obs, ava=None, deterministic=False, stride=1, rand=None):
+    v, rep = _encode(model, obs)
+    a, lp = decode(model, rep, ava, deterministic, stride, rand)
+    return v, a, lp
+
+
+@torch.no_grad()
 def get_values(model, obs):
-    with torch.autocast("cuda", dtype=torch.bfloat16):
-        v, _ = model.encoder(None, obs)
-    return v.float()
+    return _encode(model, obs)[0]
 
 
 def evaluate_actions(model, obs, actions, ava=None):
+    from . import mat_train
+    if mat_train.supported(model):
+        return mat_train.evaluate_actions(model, obs, actions, ava)
     from ..models import act as act_mod
     with torch.autocast("cuda", dtype=torch.bfloat16):
         v, rep = model.encoder(None, obs)

@@ -1,0 +1,387 @@
+"""Bindings of the fused MAT kernels: training forward/backward (``csrc/mat_train.hip``) and the weight packs.
+
+* ``ModelPack`` — every 64x64 Linear of the MAT in MFMA B-fragment order, for W (forward) and Wᵀ (backward), in
+  two persistent bf16 buffers.  One ``pack_weights`` launch refreshes all of them after an optimizer step
+  (tracked by ``model._mdl_version``).  Biases / LayerNorm parameters are read in place (fp32).
+* ``EncoderFused`` / ``DecoderFused`` — the whole-encoder / whole-decoder (teacher-forced) forward with the
+  activations the backward needs, and the backward, which writes parameter gradients straight into ``.grad``
+  (fp32 atomics; the grads are views of one flat buffer, see ``parallel/comm.FlatGrads``).
+* ``evaluate_actions`` — autograd entry used by the PPO trainer: (values, log-probs, entropy) of stored actions.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import kernels
+from .kernels import P, check, lib, sig
+
+VP = ctypes.c_void_p
+
+
+class Mat(ctypes.Structure):
+    _fields_ = [("fw", VP), ("bw", VP), ("b", VP), ("dW", VP), ("db", VP)]
+
+
+class LNp(ctypes.Structure):
+    _fields_ = [("g", VP), ("b", VP), ("dg", VP), ("db", VP)]
+
+
+class Blk(ctypes.Structure):
+    _fields_ = [("m", Mat * 10), ("ln", LNp * 3)]
+
+
+class Sv(ctypes.Structure):
+    _fields_ = [(n, VP) for n in ("xin", "a1", "lse1", "x1", "a2", "lse2", "x2", "h")]
+
+
+class EncP(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("Bs", "L", "od", "SQ", "NRP", "n_obj")] + \
+               [(n, VP) for n in ("obs", "lno_g", "lno_b", "we", "be", "ln0_g", "ln0_b", "d_lno_g", "d_lno_b", "d_we",
+                                  "d_be", "d_ln0_g", "d_ln0_b")] + \
+               [("blk", Blk * 3), ("h1", Mat), ("lnh", LNp), ("wh2", VP), ("bh2", VP), ("d_wh2", VP), ("rep", VP),
+                ("v", VP), ("sv", Sv * 3), ("drep", VP), ("dv", VP)]
+
+
+class DecP(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("Bs", "L", "A", "SQ", "NRP", "n_disc")] + \
+               [(n, VP) for n in ("act", "ava", "wa", "d_wa", "lnd_g", "lnd_b", "d_lnd_g", "d_lnd_b")] + \
+               [("blk", Blk * 3), ("h1", Mat), ("lnh", LNp)] + \
+               [(n, VP) for n in ("wh2", "bh2", "d_wh2", "d_bh2", "stdv", "log_std", "d_log_std", "rep", "logp",
+                                  "ent")] + \
+               [("sv", Sv * 3)] + [(n, VP) for n in ("dlogp", "dent", "drep", "sv_head")]
+
+
+sig("mdl_mat_train_geometry", ctypes.c_int)
+sig("mdl_mat_enc_fwd", ctypes.POINTER(EncP), ctypes.c_int, ctypes.c_int, VP)
+sig("mdl_mat_enc_bwd", ctypes.POINTER(EncP), ctypes.c_int, VP)
+sig("mdl_mat_dec_fwd", ctypes.POINTER(DecP), ctypes.c_int, ctypes.c_int, VP)
+sig("mdl_mat_dec_bwd", ctypes.POINTER(DecP), ctypes.c_int, VP)
+sig("mdl_pack_weights", VP, ctypes.c_int, VP)
+
+
+def geometry(L):
+    v = lib().mdl_mat_train_geometry(L)
+    return v & 0xFFFF, v >> 16
+
+
+def _ptr(t):
+    return t.data_ptr() if t is not None else None
+
+
+def _gptr(t):
+    return t.grad.data_ptr() if t.grad is not None else None
+
+
+# ------------------------------------------------------------------------------------------------- packs
+def decoder_linears(model):
+    dec = model.decoder
+    out = []
+    for blk in dec.blocks:
+        a1, a2 = blk.attn1, blk.attn2
+        out += [a1.query, a1.key, a1.value, a1.proj, a2.query, a2.key, a2.value, a2.proj, blk.mlp[0], blk.mlp[2]]
+    out.append(dec.head[0])
+    return out
+
+
+def encoder_linears(model):
+    enc = model.encoder
+    out = []
+    for blk in enc.blocks:
+        a = blk.attn
+        out += [a.query, a.key, a.value, a.proj, blk.mlp[0], blk.mlp[2]]
+    out.append(enc.head[0])
+    return out
+
+
+class ModelPack:
+    def __init__(self, model):
+        self.model = model
+        lins = decoder_linears(model) + encoder_linears(model)
+        self.n = len(lins)
+        self.n_dec = len(decoder_linears(model))
+        dev = lins[0].weight.device
+        self.fw = torch.empty(self.n, 4096, dtype=torch.bfloat16, device=dev)
+        self.bw = torch.empty(self.n, 4096, dtype=torch.bfloat16, device=dev)
+        self.index = {id(l): i for i, l in enumerate(lins)}
+        tab = [[l.weight.data_ptr(), self.fw[i].data_ptr(), self.bw[i].data_ptr()] for i, l in enumerate(lins)]
+        self.table = torch.tensor(tab, dtype=torch.int64, device=dev)
+        self.version = None
+
+    def refresh(self):
+        ver = getattr(self.model, "_mdl_version", 0)
+        if ver != self.version:
+            check(lib().mdl_pack_weights(P(self.table), self.n, kernels._stream()), "pack_weights")
+            self.version = ver
+
+    def mat(self, lin):
+        i = self.index[id(lin)]
+        return Mat(self.fw[i].data_ptr(), self.bw[i].data_ptr(), lin.bias.data_ptr(), _gptr(lin.weight),
+                   _gptr(lin.bias))
+
+    @property
+    def decoder_fw(self):
+        return self.fw[: self.n_dec]
+
+
+def model_pack(model):
+    mp = getattr(model, "_mdl_pack", None)
+    if mp is None:
+        mp = ModelPack(model)
+        model._mdl_pack = mp
+    mp.refresh()
+    return mp
+
+
+def _ln(ln):
+    return LNp(ln.weight.data_ptr(), ln.bias.data_ptr(), _gptr(ln.weight), _gptr(ln.bias))
+
+
+def _grad_sig(model):
+    p = next(model.parameters())
+    return p.grad.data_ptr() if p.grad is not None else 0
+
+
+# ------------------------------------------------------------------------------------------------- support
+def encoder_supported(model):
+    enc = model.encoder
+    return (kernels.available() and model.n_embd == 64 and model.n_head == 2 and model.n_block in (1, 2, 3)
+            and not enc.encode_state and enc.obs_dim <= 16 and model.n_objective <= 2
+            and geometry(model.n_agent)[0] > 0)
+
+
+def decoder_supported(model):
+    dec = model.decoder
+    return (kernels.available() and not dec.dec_actor and model.action_type in ("Semi_Discrete", "Discrete")
+            and model.action_dim <= 8 and model.n_embd == 64 and model.n_head == 2 and model.n_block in (1, 2, 3)
+            and (model.action_type == "Discrete" or model.semi_index == -1) and geometry(model.n_agent)[0] > 0)
+
+
+def supported(model):
+    return encoder_supported(model) and decoder_supported(model)
+
+
+# ------------------------------------------------------------------------------------------------- encoder
+class EncoderFused:
+    def __init__(self, model):
+        self.model = model
+        self.p = None
+        self.sig = None
+
+    def _build(self):
+        m = self.model
+        s = _grad_sig(m)
+        if self.p is not None and self.sig == s:
+            return
+        mp = model_pack(m)
+        enc = m.encoder
+        p = EncP()
+        ln_o, lin_e = enc.obs_encoder[0], enc.obs_encoder[1]
+        for name, t in (("lno_g", ln_o.weight), ("lno_b", ln_o.bias), ("we", lin_e.weight), ("be", lin_e.bias),
+                        ("ln0_g", enc.ln.weight), ("ln0_b", enc.ln.bias)):
+            setattr(p, name, t.data_ptr())
+            setattr(p, "d_" + name, _gptr(t))
+        for bi, blk in enumerate(enc.blocks):
+            a = blk.attn
+            for slot, lin in ((0, a.query), (1, a.key), (2, a.value), (3, a.proj), (8, blk.mlp[0]), (9, blk.mlp[2])):
+                p.blk[bi].m[slot] = mp.mat(lin)
+            p.blk[bi].ln[0] = _ln(blk.ln1)
+            p.blk[bi].ln[1] = _ln(blk.ln2)
+        p.h1 = mp.mat(enc.head[0])
+        p.lnh = _ln(enc.head[2])
+        p.wh2, p.bh2, p.d_wh2 = enc.head[3].weight.data_ptr(), enc.head[3].bias.data_ptr(), _gptr(enc.head[3].weight)
+        self.p, self.sig = p, s
+
+    def forward(self, obs, save=True):
+        """obs (B, L, od) -> (v (B, L, n_obj), rep (B, L, 64) f32)."""
+        m = self.model
+        model_pack(m)
+        self._build()
+        B, L, od = obs.shape
+        dev = obs.device
+        SQ, NRP = geometry(L)
+        n_tok = B * L
+        obs = obs.float().contiguous()
+        rep = torch.empty(B, L, 64, device=dev)
+        v = torch.empty(B, L, m.n_objective, device=dev)
+        p = self.p
+        p.Bs, p.L, p.od, p.SQ, p.NRP, p.n_obj = B, L, od, SQ, NRP, m.n_objective
+        p.obs, p.rep, p.v = obs.data_ptr(), rep.data_ptr(), v.data_ptr()
+        saves = []
+        if save:
+            for bi in range(m.n_block):
+                t = torch.empty(4, n_tok, 64, device=dev, dtype=torch.bfloat16)
+                lse = torch.empty(n_tok, 2, device=dev)
+                saves += [t, lse]
+                p.sv[bi] = Sv(t[0].data_ptr(), t[1].data_ptr(), lse.data_ptr(), t[2].data_ptr(), None, None, None,
+                              t[3].data_ptr())
+        check(lib().mdl_mat_enc_fwd(ctypes.byref(p), m.n_block, int(save), kernels._stream()), "mat_enc_fwd")
+        self.ctx = (obs, rep, v, saves, [Sv.from_buffer_copy(p.sv[i]) for i in range(m.n_block)])
+        return v, rep
+
+    def backward(self, drep, dv):
+        m = self.model
+        obs, rep, v, saves, svs = self.ctx
+        self._build()
+        p = self.p
+        drep = drep.float().contiguous()
+        dv = dv.float().contiguous()
+        B, L, od = obs.shape
+        SQ, NRP = geometry(L)
+        p.Bs, p.L, p.od, p.SQ, p.NRP, p.n_obj = B, L, od, SQ, NRP, m.n_objective
+        p.obs, p.rep, p.v, p.drep, p.dv = obs.data_ptr(), rep.data_ptr(), v.data_ptr(), drep.data_ptr(), dv.data_ptr()
+        for i, s in enumerate(svs):
+            p.sv[i] = s
+        check(lib().mdl_mat_enc_bwd(ctypes.byref(p), m.n_block, kernels._stream()), "mat_enc_bwd")
+        b = m.encoder.head[3].bias
+        if b.grad is not None:
+            b.grad.add_(dv.reshape(-1, dv.shape[-1]).sum(0))
+
+
+# ------------------------------------------------------------------------------------------------- decoder
+class DecoderFused:
+    def __init__(self, model):
+        self.model = model
+        self.p = None
+        self.sig = None
+
+    def _build(self):
+        m = self.model
+        s = _grad_sig(m)
+        if self.p is not None and self.sig == s:
+            return
+        mp = model_pack(m)
+        dec = m.decoder
+        p = DecP()
+        p.wa, p.d_wa = dec.action_encoder[0].weight.data_ptr(), _gptr(dec.action_encoder[0].weight)
+        p.lnd_g, p.lnd_b, p.d_lnd_g, p.d_lnd_b = dec.ln.weight.data_ptr(), dec.ln.bias.data_ptr(), \
+            _gptr(dec.ln.weight), _gptr(dec.ln.bias)
+        for bi, blk in enumerate(dec.blocks):
+            a1, a2 = blk.attn1, blk.attn2
+            for slot, lin in ((0, a1.query), (1, a1.key), (2, a1.value), (3, a1.proj), (4, a2.query), (5, a2.key),
+                              (6, a2.value), (7, a2.proj), (8, blk.mlp[0]), (9, blk.mlp[2])):
+                p.blk[bi].m[slot] = mp.mat(lin)
+            p.blk[bi].ln[0] = _ln(blk.ln1)
+            p.blk[bi].ln[1] = _ln(blk.ln2)
+            p.blk[bi].ln[2] = _ln(blk.ln3)
+        p.h1 = mp.mat(dec.head[0])
+        p.lnh = _ln(dec.head[2])
+        h3 = dec.head[3]
+        p.wh2, p.bh2, p.d_wh2, p.d_bh2 = h3.weight.data_ptr(), h3.bias.data_ptr(), _gptr(h3.weight), _gptr(h3.bias)
+        if m.action_type != "Discrete":
+            self.std = torch.empty(m.action_dim, device=h3.weight.device)
+            p.log_std, p.stdv, p.d_log_std = dec.log_std.data_ptr(), self.std.data_ptr(), _gptr(dec.log_std)
+        else:
+            self.std = torch.ones(m.action_dim, device=h3.weight.device)
+            p.log_std, p.stdv, p.d_log_std = self.std.data_ptr(), self.std.data_ptr(), None
+        self.p, self.sig = p, s
+
+    def _n_disc(self, L):
+        m = self.model
+        return L if m.action_type == "Discrete" else L + m.semi_index
+
+    def _geom(self, B, L):
+        SQ, NRP = geometry(L)
+        p = self.p
+        p.Bs, p.L, p.A, p.SQ, p.NRP, p.n_disc = B, L, self.model.action_dim, SQ, NRP, self._n_disc(L)
+
+    def forward(self, rep, actions, ava=None, save=True):
+        m = self.model
+        model_pack(m)
+        self._build()
+        if m.action_type != "Discrete":
+            with torch.no_grad():
+                self.std.copy_(m.action_std())
+        B, L, _ = rep.shape
+        dev = rep.device
+        n_tok = B * L
+        rep = rep.float().contiguous()
+        act = actions.reshape(B, L).float().contiguous()
+        ava_c = ava.float().contiguous() if ava is not None else None
+        logp = torch.empty(B, L, 1, device=dev)
+        ent = torch.empty(B, L, 1, device=dev)
+        self._geom(B, L)
+        p = self.p
+        p.act, p.ava, p.rep, p.logp, p.ent = act.data_ptr(), _ptr(ava_c), rep.data_ptr(), logp.data_ptr(), ent.data_ptr()
+        saves = []
+        if save:
+            for bi in range(m.n_block):
+                t = torch.empty(6, n_tok, 64, device=dev, dtype=torch.bfloat16)
+                lse = torch.empty(2, n_tok, 2, device=dev)
+                saves += [t, lse]
+                p.sv[bi] = Sv(t[0].data_ptr(), t[1].data_ptr(), lse[0].data_ptr(), t[2].data_ptr(), t[3].data_ptr(),
+                              lse[1].data_ptr(), t[4].data_ptr(), t[5].data_ptr())
+            head = torch.empty(n_tok, 64, device=dev, dtype=torch.bfloat16)
+            saves.append(head)
+            p.sv_head = head.data_ptr()
+        check(lib().mdl_mat_dec_fwd(ctypes.byref(p), m.n_block, int(save), kernels._stream()), "mat_dec_fwd")
+        self.ctx = (rep, act, ava_c, logp, ent, saves, [Sv.from_buffer_copy(p.sv[i]) for i in range(m.n_block)],
+                    p.sv_head)
+        return logp, ent
+
+    def backward(self, dlogp, dent):
+        m = self.model
+        rep, act, ava_c, logp, ent, saves, svs, head = self.ctx
+        self._build()
+        B, L = act.shape
+        self._geom(B, L)
+        p = self.p
+        dlogp = dlogp.reshape(-1).float().contiguous()
+        dent = dent.reshape(-1).float().contiguous()
+        drep = torch.zeros_like(rep)
+        p.act, p.ava, p.rep = act.data_ptr(), _ptr(ava_c), rep.data_ptr()
+        p.dlogp, p.dent, p.drep, p.sv_head = dlogp.data_ptr(), dent.data_ptr(), drep.data_ptr(), head
+        for i, s in enumerate(svs):
+            p.sv[i] = s
+        check(lib().mdl_mat_dec_bwd(ctypes.byref(p), m.n_block, kernels._stream()), "mat_dec_bwd")
+        return drep
+
+
+class _MATFusedFn(torch.autograd.Function):
+    """(anchor, obs, actions, ava) -> (logp, values, entropy); backward runs the fused decoder then encoder
+    backward kernels, which write the parameter gradients straight into ``.grad``."""
+
+    @staticmethod
+    def forward(ctx, anchor, obs, actions, ava, enc, dec):
+        v, rep = enc.forward(obs, save=True)
+        logp, ent = dec.forward(rep, actions, ava, save=True)
+        ctx.enc, ctx.dec = enc, dec
+        return logp, v, ent
+
+    @staticmethod
+    def backward(ctx, dlogp, dv, dent):
+        dec, enc = ctx.dec, ctx.enc
+        logp, ent = dec.ctx[3], dec.ctx[4]
+        drep = dec.backward(dlogp if dlogp is not None else torch.zeros_like(logp),
+                            dent if dent is not None else torch.zeros_like(ent))
+        enc.backward(drep, dv if dv is not None else torch.zeros_like(enc.ctx[2]))
+        dec.ctx = None
+        enc.ctx = None
+        return torch.zeros((), device=drep.device), None, None, None, None, None
+
+
+def _state(model, dev):
+    st = getattr(model, "_mdl_train_state", None)
+    if st is None:
+        st = (EncoderFused(model), DecoderFused(model), torch.zeros((), device=dev, requires_grad=True))
+        model._mdl_train_state = st
+    return st
+
+
+def evaluate_actions(model, obs, actions, ava=None):
+    """Fused teacher-forced MAT forward with autograd support: (values, log-probs, entropy) like
+    ``MultiAgentTransformer.forward``; gradients flow into the parameters' ``.grad``."""
+    enc, dec, anchor = _state(model, obs.device)
+    for p_ in model.parameters():
+        if p_.grad is None:
+            p_.grad = torch.zeros_like(p_)
+    logp, v, ent = _MATFusedFn.apply(anchor, obs, actions, ava, enc, dec)
+    return v, logp, ent
+
+
+@torch.no_grad()
+def encode(model, obs):
+    """Inference-only fused encoder: (values, rep)."""
+    enc, _, _ = _state(model, obs.device)
+    return enc.forward(obs, save=False)

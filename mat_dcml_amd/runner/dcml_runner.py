@@ -69,8 +69,9 @@ class DCMLRunner:
         self.policy = TransformerPolicy(a, self.envs.observation_space[0], self.envs.share_observation_space[0],
                                         act_space, self.num_agents, device=self.device)
         self.comm.broadcast_module_(self.policy.transformer)
-        if self.comm.world_size > 1:
-            self.comm.attach_flat_grads(self.policy.transformer.parameters())
+        # every .grad is a view of ONE flat fp32 buffer: one memset to zero, one all-reduce under DP, and the fused
+        # backward kernels accumulate straight into it
+        self.comm.attach_flat_grads(self.policy.transformer.parameters())
         self.trainer = MATTrainer(a, self.policy, self.num_agents, device=self.device, comm=self.comm)
         self.buffer = RolloutBuffer(a.episode_length, E, self.num_agents, self.dcml.obs_dim, self.dcml.share_dim,
                                     self.dcml.action_dim, gamma=a.gamma, gae_lambda=a.gae_lambda,

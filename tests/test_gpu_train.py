@@ -1,0 +1,121 @@
+"""Fused HIP training kernels vs PyTorch fp32 autograd of the same MAT."""
+import pytest
+import torch
+
+from mat_dcml_amd.models.mat import MultiAgentTransformer
+from mat_dcml_amd.ops import mat_train
+
+pytestmark = pytest.mark.gpu
+
+
+def make(L, dev, seed=0, scale=0.2, od=7, nobj=1):
+    torch.manual_seed(seed)
+    m = MultiAgentTransformer(L + 1, od, 2, L, 2, 64, 2, action_type="Semi_Discrete", semi_index=-1,
+                              n_objective=nobj).to(dev)
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if "ln" in n or "head.2" in n or "obs_encoder.0" in n:
+                p.copy_((1.0 + 0.1 * torch.randn(p.shape, generator=g)).to(dev) if n.endswith("weight")
+                        else (0.1 * torch.randn(p.shape, generator=g)).to(dev))
+            else:
+                p.copy_((torch.randn(p.shape, generator=g) * scale).to(dev))
+    return m
+
+
+def rel(a, b):
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("L,B", [(33, 40), (5, 77), (101, 6)])
+def test_encoder_forward(gpu, L, B):
+    m = make(L, gpu)
+    obs = torch.rand(B, L, 7, device=gpu)
+    enc = mat_train.EncoderFused(m)
+    v, rep = enc.forward(obs, save=False)
+    with torch.no_grad():
+        v_ref, rep_ref = m.encoder(None, obs)
+    assert rel(rep, rep_ref) < 2e-2, rel(rep, rep_ref)
+    assert rel(v, v_ref) < 3e-2, rel(v, v_ref)
+
+
+@pytest.mark.parametrize("L,B", [(33, 40), (5, 77), (101, 6)])
+def test_encoder_backward(gpu, L, B):
+    m = make(L, gpu)
+    obs = torch.rand(B, L, 7, device=gpu)
+    g = torch.Generator(device=gpu).manual_seed(1)
+    drep = torch.randn(B, L, 64, device=gpu, generator=g)
+    dv = torch.randn(B, L, 1, device=gpu, generator=g)
+    # reference grads
+    m.zero_grad()
+    v_ref, rep_ref = m.encoder(None, obs)
+    ((rep_ref * drep).sum() + (v_ref * dv).sum()).backward()
+    ref = {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
+    # fused
+    for p_ in m.parameters():
+        p_.grad = torch.zeros_like(p_)
+    enc = mat_train.EncoderFused(m)
+    enc.forward(obs, save=True)
+    enc.backward(drep, dv)
+    torch.cuda.synchronize()
+    bad = []
+    for n, r in ref.items():
+        if not n.startswith("encoder.") or "state_encoder" in n:
+            continue
+        gg = dict(m.named_parameters())[n].grad
+        if "key.bias" in n:  # exactly 0 in theory (softmax is shift invariant): compare absolutely
+            e = (gg - r).abs().max().item() / (ref[n.replace("key.bias", "key.weight")].abs().max().item() + 1e-6)
+        else:
+            e = rel(gg, r)
+        if e > 5e-2:
+            bad.append((n, round(e, 4)))
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("L,B", [(33, 40), (5, 77), (101, 6)])
+def test_full_mat_fused_grads(gpu, L, B):
+    """Teacher-forced log-prob / entropy / value and ALL parameter gradients of a PPO-like loss."""
+    from mat_dcml_amd.models import act as act_mod
+    m = make(L, gpu, seed=2)
+    g = torch.Generator(device=gpu).manual_seed(3)
+    obs = torch.rand(B, L, 7, device=gpu, generator=g)
+    ava = torch.ones(B, L, 2, device=gpu)
+    ava[:, 1::4, 1] = 0
+    actions = (torch.rand(B, L, 1, device=gpu, generator=g) < 0.5).float()
+    actions[ava[..., 1:] == 0] = 0
+    actions[:, -1, 0] = torch.rand(B, device=gpu, generator=g)
+    w1 = torch.randn(B, L, 1, device=gpu, generator=g)
+    w2 = torch.randn(B, L, 1, device=gpu, generator=g)
+    w3 = torch.randn(B, L, 1, device=gpu, generator=g)
+    m.zero_grad()
+    lp_r, v_r, ent_r = m(None, obs, actions, ava)
+    ((lp_r * w1).sum() + (v_r * w2).sum() + (ent_r * w3).sum()).backward()
+    ref = {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
+    m.zero_grad()
+    with torch.autocast("cuda", dtype=torch.bfloat16):   # bf16 autocast gradients as the precision yardstick
+        lp_b, v_b, ent_b = m(None, obs, actions, ava)
+        ((lp_b.float() * w1).sum() + (v_b.float() * w2).sum() + (ent_b.float() * w3).sum()).backward()
+    refb = {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
+    for p_ in m.parameters():
+        p_.grad = torch.zeros_like(p_)
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):  # bf16 yardstick
+        lp_b, v_b, ent_b = m(None, obs, actions, ava)
+    tol = lambda a, b: max(3e-2, 2.5 * rel(a.float(), b))  # noqa: E731
+    v_k, lp_k, ent_k = mat_train.evaluate_actions(m, obs, actions, ava)
+    assert rel(lp_k, lp_r) < tol(lp_b, lp_r), (rel(lp_k, lp_r), rel(lp_b.float(), lp_r))
+    assert rel(v_k, v_r) < tol(v_b, v_r) and rel(ent_k, ent_r) < tol(ent_b, ent_r)
+    ((lp_k * w1).sum() + (v_k * w2).sum() + (ent_k * w3).sum()).backward()
+    torch.cuda.synchronize()
+    bad = []
+    params = dict(m.named_parameters())
+    for n, r in ref.items():
+        gg = params[n].grad
+        if "key.bias" in n:
+            e = (gg - r).abs().max().item() / (ref[n.replace("key.bias", "key.weight")].abs().max().item() + 1e-6)
+            lim = 8e-2
+        else:
+            e = rel(gg, r)
+            lim = max(6e-2, 2.5 * rel(refb[n], r)) if n != "decoder.log_std" else max(0.1, 10 * rel(refb[n], r))
+        if e > lim:
+            bad.append((n, round(e, 4), round(rel(refb[n], r), 4)))
+    assert not bad, bad
