@@ -1,0 +1,6 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+echo kern; timeout -k 10 120 python tests/bench_train_kernels.py || exit 1
+timeout -k 10 400 python -m pytest tests/test_gpu_train.py -x -q > gpurun_out/t_train.log 2>&1; rc=$?; tail -5 gpurun_out/t_train.log; [ $rc = 0 ] || exit 2
+timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1; rc=$?; tail -3 gpurun_out/bench.log; exit $rc

@@ -13,11 +13,11 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 OUT_DIR = os.path.join(os.path.dirname(HERE), "_lib")
-OUT = os.path.join(OUT_DIR, "libmatdcml.so")
+OUT = os.path.join(OUT_DIR, os.environ.get("MAT_DCML_LIBNAME", "libmatdcml.so"))
 ARCH = os.environ.get("MAT_DCML_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=fast", "-munsafe-fp-atomics",
-         "-Wno-unused-result", "-fvisibility=hidden"]
+         "-Wno-unused-result", "-fvisibility=hidden"] + os.environ.get("MAT_DCML_EXTRA_FLAGS", "").split()
 
 
 def _sources():

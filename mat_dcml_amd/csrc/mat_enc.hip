@@ -1,0 +1,269 @@
+// Fused MAT encoder forward / backward kernels (see mat_train_common.h for the design).
+#include "mat_train_common.h"
+
+// ============================================================================================== encoder forward
+template <int NB, bool SAVE>
+__global__ __launch_bounds__(256, 1) void mat_enc_fwd(EncP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const Ctx c = make_ctx(p, smem);
+  if (c.nseq <= 0) return;
+  zero_lds(smem, mat_train_lds_bytes(p.NRP, p.SQ, p.L), c.tid);
+  __syncthreads();
+  const int lane = c.lane, g = lane >> 4, c16 = lane & 15;
+  RT xr[MAXRT];
+#pragma unroll
+  for (int k = 0; k < MAXRT; ++k) {
+    const int rt = c.wave + 4 * k;
+    if (rt < c.NT) {
+      RT pre, xh;
+      EmbRow er[4];
+      embed_pre(p, rt, pre, er, c);
+      gelu_rt(pre);
+      f32x4 mu, rs;
+      ln_fwd(pre, xh, xr[k], mu, rs, p.ln0_g, p.ln0_b, lane);
+    }
+  }
+#pragma unroll 1
+  for (int b = 0; b < NB; ++b) {
+    const Blk& B = p.blk[b];
+    Ctx cc = c;   // opaque per-iteration lane id: keeps hipcc from hoisting (and spilling) every LDS address
+    asm volatile("" : "+v"(cc.lane), "+v"(cc.tid));
+    attn_self_fwd<SAVE>(B.m, B.ln[0], xr, p.sv[b], false, p.sv[b].xin, p.sv[b].a1, p.sv[b].lse1, cc);
+    mlp_fwd<SAVE>(B.m[8], B.m[9], B.ln[1], xr, p.sv[b].x1, p.sv[b].h, cc);
+  }
+  // value head: v = W_v2 · LN(GELU(W_v1 · rep + b)) + b   (ma_transformer.py:138-139,152)
+  BFr Bh;
+  loadB(Bh, p.h1.fw, lane);
+#pragma unroll
+  for (int k = 0; k < MAXRT; ++k) {
+    const int rt = c.wave + 4 * k;
+    if (rt < c.NT) {
+      st_tm_m(c.XB, rt, xr[k], row_mask(rt, c.NR, lane), lane);
+      if (p.rep) st_g_f(p.rep, c.tok0, rt, c.NR, xr[k], lane);
+      wave_lds_sync();
+      RT hh, xh, n;
+      gemm_rt(hh, c.XB, rt, Bh, lane, false);
+      add_bias(hh, p.h1.b, lane);
+      gelu_rt(hh);
+      f32x4 mu, rs;
+      ln_fwd(hh, xh, n, mu, rs, p.lnh.g, p.lnh.b, lane);
+      for (int o = 0; o < p.n_obj; ++o) {
+        RT t;
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) {
+          const float w = p.wh2[o * 64 + 16 * ct + c16];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) t.v[ct][r] = n.v[ct][r] * w;
+        }
+        const f32x4 vs = rowsum(t);
+        if (c16 == 0) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = rt * 16 + 4 * g + r;
+            if (row < c.NR) p.v[(size_t)(c.tok0 + row) * p.n_obj + o] = vs[r] + p.bh2[o];
+          }
+        }
+      }
+    }
+  }
+}
+
+// ============================================================================================== encoder backward
+template <int NB>
+__global__ __launch_bounds__(256, 1) void mat_enc_bwd(EncP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const Ctx c = make_ctx(p, smem);
+  if (c.nseq <= 0) return;
+  zero_lds(smem, mat_train_lds_bytes(p.NRP, p.SQ, p.L), c.tid);
+  __syncthreads();
+  const int lane = c.lane, g = lane >> 4, c16 = lane & 15;
+  RT dx[MAXRT];
+  // ---------------- value head backward (+ incoming d rep from the decoder)
+  {
+    f32x4 dlg = {0, 0, 0, 0}, dlb = {0, 0, 0, 0}, dbh = {0, 0, 0, 0}, dw2[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+    BFr Bf, Bb;
+    loadB(Bf, p.h1.fw, lane);
+    loadB(Bb, p.h1.bw, lane);
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) {
+        const f32x4 vm = row_mask(rt, c.NR, lane);
+        RT rep;
+        ld_g_f(p.rep, c.tok0, rt, c.NR, rep, lane);
+        st_tm_m(c.XB, rt, rep, vm, lane);   // X of dW_h1
+        wave_lds_sync();
+        RT hh, gl, xh, n, dn, dg;
+        gemm_rt(hh, c.XB, rt, Bf, lane, false);
+        add_bias(hh, p.h1.b, lane);
+        gl = hh;
+        gelu_rt(gl);
+        f32x4 mu, rs;
+        ln_fwd(gl, xh, n, mu, rs, p.lnh.g, p.lnh.b, lane);
+        rt_zero(dn);
+#pragma unroll
+        for (int o = 0; o < 2; ++o) {
+          if (o >= p.n_obj) break;
+          f32x4 dvv;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = rt * 16 + 4 * g + r;
+            dvv[r] = row < c.NR ? p.dv[(size_t)(c.tok0 + row) * p.n_obj + o] : 0.f;
+          }
+#pragma unroll
+          for (int ct = 0; ct < 4; ++ct) {
+            const float w = p.wh2[o * 64 + 16 * ct + c16];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              dn.v[ct][r] += dvv[r] * w;
+              dw2[o][ct] += dvv[r] * n.v[ct][r];
+            }
+          }
+        }
+        ln_bwd(dn, xh, rs, p.lnh.g, dg, dlg, dlb, vm, lane);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dg.v[ct][r] *= gelu_erf_grad(hh.v[ct][r]) * vm[r];
+        colsum_acc(dg, dbh, vm);
+        st_tm_m(c.DQ, rt, dg, vm, lane);    // dY of dW_h1
+        wave_lds_sync();
+        RT t, dr;
+        gemm_rt(t, c.DQ, rt, Bb, lane, false);
+        ld_g_f(p.drep, c.tok0, rt, c.NR, dr, lane);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) dx[k].v[ct] = dr.v[ct] + t.v[ct];
+      }
+    }
+    flush_ln(dlg, dlb, p.lnh, lane);
+    flush_cols(dbh, p.h1.db, lane);
+    flush_cols(dw2[0], p.d_wh2, lane);
+    if (p.n_obj > 1) flush_cols(dw2[1], p.d_wh2 ? p.d_wh2 + 64 : nullptr, lane);
+    __syncthreads();
+    wgrad_tm(c.DQ, c.XB, c.NRP, p.h1.dW, c.wave, lane);
+    __syncthreads();
+  }
+  // ---------------- blocks in reverse
+#pragma unroll 1
+  for (int bb = NB - 1; bb >= 0; --bb) {
+    const Blk& B = p.blk[bb];
+    Ctx cc = c;
+    asm volatile("" : "+v"(cc.lane), "+v"(cc.tid));
+    mlp_bwd(B.m[8], B.m[9], B.ln[1], dx, p.sv[bb].x1, p.sv[bb].h, cc);
+    attn_self_bwd(B.m, B.ln[0], dx, p.sv[bb].xin, p.sv[bb].a1, p.sv[bb].lse1, false, cc);
+  }
+  // ---------------- embedding backward: x0 = LN0(GELU(W_e · LN_obs(obs) + b_e))
+  {
+    f32x4 dlg = {0, 0, 0, 0}, dlb = {0, 0, 0, 0}, dbe = {0, 0, 0, 0};
+    float dwe[4][16], dlog[16], dlob[16];
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) dwe[ct][kk] = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) { dlog[kk] = 0.f; dlob[kk] = 0.f; }
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) {
+        const f32x4 vm = row_mask(rt, c.NR, lane);
+        RT pre, e, xh, y, de;
+        EmbRow er[4];
+        embed_pre(p, rt, pre, er, c);
+        e = pre;
+        gelu_rt(e);
+        f32x4 mu, rs;
+        ln_fwd(e, xh, y, mu, rs, p.ln0_g, p.ln0_b, lane);
+        ln_bwd(dx[k], xh, rs, p.ln0_g, de, dlg, dlb, vm, lane);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) de.v[ct][r] *= gelu_erf_grad(pre.v[ct][r]) * vm[r];
+        colsum_acc(de, dbe, vm);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int kk = 0; kk < 16; ++kk) dwe[ct][kk] += de.v[ct][r] * er[r].oh[kk];
+        // d(LN_obs output)[row][kk] = sum_col dpre * W_e[col][kk]  -> LN_obs affine-parameter grads
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+#pragma unroll
+          for (int kk = 0; kk < 16; ++kk) {
+            if (kk < p.od) {
+              float t = 0.f;
+#pragma unroll
+              for (int ct = 0; ct < 4; ++ct) t += de.v[ct][r] * p.we[(16 * ct + c16) * p.od + kk];
+              t += __shfl_xor(t, 1, 64);
+              t += __shfl_xor(t, 2, 64);
+              t += __shfl_xor(t, 4, 64);
+              t += __shfl_xor(t, 8, 64);
+              if (c16 == 0) { dlog[kk] += t * er[r].ohat[kk]; dlob[kk] += t; }
+            }
+          }
+        }
+      }
+    }
+    flush_ln(dlg, dlb, LNp{nullptr, nullptr, p.d_ln0_g, p.d_ln0_b}, lane);
+    flush_cols(dbe, p.d_be, lane);
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) {
+        if (kk < p.od) {
+          float x = dwe[ct][kk];
+          x += __shfl_xor(x, 16, 64);
+          x += __shfl_xor(x, 32, 64);
+          if (g == 0 && p.d_we) atomicAdd(p.d_we + (16 * ct + c16) * p.od + kk, x);
+        }
+      }
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      if (kk < p.od) {
+        float a = dlog[kk], b2 = dlob[kk];
+        a += __shfl_xor(a, 16, 64);
+        a += __shfl_xor(a, 32, 64);
+        b2 += __shfl_xor(b2, 16, 64);
+        b2 += __shfl_xor(b2, 32, 64);
+        if (lane == 0) {
+          if (p.d_lno_g) atomicAdd(p.d_lno_g + kk, a);
+          if (p.d_lno_b) atomicAdd(p.d_lno_b + kk, b2);
+        }
+      }
+    }
+  }
+}
+
+
+
+// ============================================================================================== host API
+MDL_API int mdl_mat_train_geometry(int L) {
+  // sequences per tile: rows = SQ*L <= 4*MAXRT*16 = 192, LDS-padded rows a multiple of 32; returns SQ | NRP << 16
+  int SQ = 192 / L;
+  if (SQ < 1) return 0;
+  int NRP = ((SQ * L + 31) / 32) * 32;
+  while (SQ > 1 && (NRP > 192 || mat_train_lds_bytes(NRP, SQ, L) > 160 * 1024)) {
+    --SQ;
+    NRP = ((SQ * L + 31) / 32) * 32;
+  }
+  if (mat_train_lds_bytes(NRP, SQ, L) > 160 * 1024 || (SQ * L + 15) / 16 > 4 * MAXRT) return 0;
+  return SQ | (NRP << 16);
+}
+
+MDL_API int mdl_mat_enc_fwd(const EncP* p, int NB, int save, hipStream_t st) {
+  if (p->od > 16 || p->od < 1 || p->n_obj > 2) return -1;
+  if (NB == 1) return save ? launch(mat_enc_fwd<1, true>, p, st) : launch(mat_enc_fwd<1, false>, p, st);
+  if (NB == 2) return save ? launch(mat_enc_fwd<2, true>, p, st) : launch(mat_enc_fwd<2, false>, p, st);
+  if (NB == 3) return save ? launch(mat_enc_fwd<3, true>, p, st) : launch(mat_enc_fwd<3, false>, p, st);
+  return -3;
+}
+
+MDL_API int mdl_mat_enc_bwd(const EncP* p, int NB, hipStream_t st) {
+  if (p->od > 16 || p->od < 1 || p->n_obj > 2) return -1;
+  if (NB == 1) return launch(mat_enc_bwd<1>, p, st);
+  if (NB == 2) return launch(mat_enc_bwd<2>, p, st);
+  if (NB == 3) return launch(mat_enc_bwd<3>, p, st);
+  return -3;
+}
+

@@ -1,0 +1,628 @@
+// Fused MAT training kernels for gfx950: whole-encoder forward / backward over tiles of whole sequences.
+//
+// Replaces the eager forward/backward of the reference's Encoder (mat_src/mat/algorithms/mat/algorithm/
+// ma_transformer.py:72-92,119-154) used by TransformerPolicy.evaluate_actions / get_values
+// (transformer_policy.py:158-217) inside MATTrainer.ppo_update (mat_trainer.py:96-156).
+//
+// One 256-thread workgroup owns SQ whole sequences (NR = SQ*L token rows, NT 16-row MFMA tiles; wave w owns tiles
+// w, w+4, w+8).  Everything between two attention phases is wave-local: each wave computes full 64-column rows on
+// v_mfma_f32_16x16x32_bf16 (weights streamed as pre-packed B fragments from L2), keeps the f32 residual stream in
+// registers and runs bias / residual / LayerNorm / GELU on the accumulator layout (tile.h).  Attention over a
+// sequence (L <= ~200 rows) runs on the VALU with packed bf16 dot products (v_dot2c_f32_bf16) and an online softmax.
+// Only the attention phases and the weight-gradient GEMMs need workgroup barriers.
+//
+// Backward: activations saved by the forward (block inputs, attention outputs, MLP inputs / pre-GELU, per-row
+// log-sum-exp) are reloaded; LayerNorm statistics, projections, q/k/v and P are recomputed.  Weight gradients
+// dW = dYᵀ·X reduce over the token axis straight from token-major LDS tiles with ds_read_b64_tr_b16 transpose
+// reads and are flushed with one fp32 atomic per element per workgroup.
+#pragma once
+#include "tile.h"
+
+using namespace mdl;
+
+namespace {
+
+constexpr int MAXRT = 3;  // row tiles per wave (NT <= 12)
+
+struct Mat { const bf16_t* fw; const bf16_t* bw; const float* b; float* dW; float* db; };
+struct LNp { const float* g; const float* b; float* dg; float* db; };
+struct Blk { Mat m[10]; LNp ln[3]; };
+struct Sv { bf16_t* xin; bf16_t* a1; float* lse1; bf16_t* x1; bf16_t* a2; float* lse2; bf16_t* x2; bf16_t* h; };
+
+struct EncP {
+  int Bs, L, od, SQ, NRP, n_obj;
+  const float* obs;
+  const float *lno_g, *lno_b, *we, *be, *ln0_g, *ln0_b;
+  float *d_lno_g, *d_lno_b, *d_we, *d_be, *d_ln0_g, *d_ln0_b;
+  Blk blk[3];
+  Mat h1;
+  LNp lnh;
+  const float* wh2;
+  const float* bh2;
+  float* d_wh2;
+  float* rep;
+  float* v;
+  Sv sv[3];
+  const float* drep;
+  const float* dv;
+};
+
+struct DecP {
+  int Bs, L, A, SQ, NRP, n_disc;
+  const float* act;      // [tok] stored action (discrete index, or the continuous value for continuous agents)
+  const float* ava;      // [tok][A] availability (or null)
+  const float* wa;       // action_encoder weight [64][A+1]
+  float* d_wa;
+  const float *lnd_g, *lnd_b;
+  float *d_lnd_g, *d_lnd_b;
+  Blk blk[3];
+  Mat h1;
+  LNp lnh;
+  const float* wh2;      // [A][64]
+  const float* bh2;      // [A]
+  float* d_wh2;
+  float* d_bh2;
+  const float* stdv;     // [A] sigmoid(log_std) * 0.5
+  const float* log_std;  // [A]
+  float* d_log_std;
+  const float* rep;      // [tok][64] encoder output
+  float* logp;           // [tok]
+  float* ent;            // [tok]
+  Sv sv[3];
+  const float* dlogp;
+  const float* dent;
+  float* drep;           // [tok][64] accumulated (pre-zeroed)
+  bf16_t* sv_head;       // [tok][64] head input (last block output)
+};
+
+struct Ctx {
+  int tid, lane, wave, L, nseq, NR, NT, NRP, tok0;
+  bf16_t *QB, *KB, *VB, *DA, *DQ, *XB;
+  float *LSE, *DEL;
+};
+
+typedef __bf16 bf2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2v, a), __builtin_bit_cast(bf2v, b), c, false);
+}
+__device__ __forceinline__ float lo_bf(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float hi_bf(uint32_t u) { return __uint_as_float(u & 0xFFFF0000u); }
+
+__device__ __forceinline__ void ld_head_u(const bf16_t* buf, int row, int h, uint32_t* o) {
+#pragma unroll
+  for (int lc = 0; lc < 4; ++lc) {
+    const uint4 v = *(const uint4*)(buf + (row << 6) + ((((4 * h + lc) ^ ((row >> 1) & 7))) << 3));
+    o[4 * lc + 0] = v.x; o[4 * lc + 1] = v.y; o[4 * lc + 2] = v.z; o[4 * lc + 3] = v.w;
+  }
+}
+__device__ __forceinline__ void st_head_f(bf16_t* buf, int row, int h, const float* v) {
+#pragma unroll
+  for (int lc = 0; lc < 4; ++lc) {
+    uint4 u;
+    u.x = (uint32_t)f2bf(v[8 * lc + 0]) | ((uint32_t)f2bf(v[8 * lc + 1]) << 16);
+    u.y = (uint32_t)f2bf(v[8 * lc + 2]) | ((uint32_t)f2bf(v[8 * lc + 3]) << 16);
+    u.z = (uint32_t)f2bf(v[8 * lc + 4]) | ((uint32_t)f2bf(v[8 * lc + 5]) << 16);
+    u.w = (uint32_t)f2bf(v[8 * lc + 6]) | ((uint32_t)f2bf(v[8 * lc + 7]) << 16);
+    *(uint4*)(buf + (row << 6) + ((((4 * h + lc) ^ ((row >> 1) & 7))) << 3)) = u;
+  }
+}
+
+constexpr float ATT_SCALE = 0.17677669529663687f;  // 1/sqrt(32)
+
+// ------------------------------------------------------------------------------------------ attention (VALU)
+// items (s, h, i): online softmax over the keys of sequence s; O may alias Q (each item reads only its own q row)
+__device__ __forceinline__ void attn_fwd(const bf16_t* Q, const bf16_t* K, const bf16_t* V, bf16_t* O, bool causal, float* lse_g,
+                         const Ctx& c) {
+  const int L = c.L, n_items = c.nseq * 2 * L;
+  for (int it = c.tid; it < n_items; it += 256) {
+    const int s = it / (2 * L), rem = it - s * 2 * L, h = rem / L, i = rem - h * L;
+    const int row = s * L + i;
+    uint32_t q[16];
+    ld_head_u(Q, row, h, q);
+    float m = -1e30f, l = 0.f, acc[32];
+#pragma unroll
+    for (int d = 0; d < 32; ++d) acc[d] = 0.f;
+    const int jn = causal ? i + 1 : L;
+    for (int j = 0; j < jn; ++j) {
+      const int kr = s * L + j;
+      uint32_t k[16];
+      ld_head_u(K, kr, h, k);
+      float d = 0.f;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) d = dot2(q[t], k[t], d);
+      d *= ATT_SCALE;
+      if (d > m + 8.f) {  // lazy rescale: exp(d - m) stays <= e^8 between rescales
+        const float cf = __expf(m - d);
+        l *= cf;
+#pragma unroll
+        for (int e = 0; e < 32; ++e) acc[e] *= cf;
+        m = d;
+      }
+      const float pj = __expf(d - m);
+      l += pj;
+      uint32_t v[16];
+      ld_head_u(V, kr, h, v);
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        acc[2 * t] += pj * lo_bf(v[t]);
+        acc[2 * t + 1] += pj * hi_bf(v[t]);
+      }
+    }
+    const float inv = 1.f / l;
+#pragma unroll
+    for (int d = 0; d < 32; ++d) acc[d] *= inv;
+    st_head_f(O, row, h, acc);
+    if (lse_g) lse_g[(size_t)(c.tok0 + row) * 2 + h] = m + __logf(l);
+  }
+}
+
+// backward pass 1 (by query row): recompute P from the saved log-sum-exp, delta_i = dO_i·O_i, dq_i
+__device__ __forceinline__ void attn_bwd_q(const bf16_t* Q, const bf16_t* K, const bf16_t* V, const bf16_t* DA, bf16_t* DQ,
+                           bool causal, const Ctx& c) {
+#ifdef MDL_ABLATE_ATTN
+  return;
+#endif
+  const int L = c.L, n_items = c.nseq * 2 * L;
+  for (int it = c.tid; it < n_items; it += 256) {
+    const int s = it / (2 * L), rem = it - s * 2 * L, h = rem / L, i = rem - h * L;
+    const int row = s * L + i;
+    uint32_t q[16], da[16];
+    ld_head_u(Q, row, h, q);
+    ld_head_u(DA, row, h, da);
+    const float lse = c.LSE[it];
+    const int jn = causal ? i + 1 : L;
+    float o[32];
+#pragma unroll
+    for (int d = 0; d < 32; ++d) o[d] = 0.f;
+    for (int j = 0; j < jn; ++j) {
+      const int kr = s * L + j;
+      uint32_t k[16], v[16];
+      ld_head_u(K, kr, h, k);
+      float d = 0.f;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) d = dot2(q[t], k[t], d);
+      const float p = __expf(d * ATT_SCALE - lse);
+      ld_head_u(V, kr, h, v);
+#pragma unroll
+      for (int t = 0; t < 16; ++t) { o[2 * t] += p * lo_bf(v[t]); o[2 * t + 1] += p * hi_bf(v[t]); }
+    }
+    float delta = 0.f;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) delta += lo_bf(da[t]) * o[2 * t] + hi_bf(da[t]) * o[2 * t + 1];
+    c.DEL[it] = delta;
+    float dq[32];
+#pragma unroll
+    for (int d = 0; d < 32; ++d) dq[d] = 0.f;
+    for (int j = 0; j < jn; ++j) {
+      const int kr = s * L + j;
+      uint32_t k[16], v[16];
+      ld_head_u(K, kr, h, k);
+      ld_head_u(V, kr, h, v);
+      float d = 0.f, dp = 0.f;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) { d = dot2(q[t], k[t], d); dp = dot2(da[t], v[t], dp); }
+      const float p = __expf(d * ATT_SCALE - lse);
+      const float ds = p * (dp - delta);
+#pragma unroll
+      for (int t = 0; t < 16; ++t) { dq[2 * t] += ds * lo_bf(k[t]); dq[2 * t + 1] += ds * hi_bf(k[t]); }
+    }
+#pragma unroll
+    for (int d = 0; d < 32; ++d) dq[d] *= ATT_SCALE;
+    st_head_f(DQ, row, h, dq);
+  }
+}
+
+// backward pass 2 (by key row): dk_j, dv_j, written in place over K / V
+__device__ __forceinline__ void attn_bwd_kv(const bf16_t* Q, bf16_t* K, bf16_t* V, const bf16_t* DA, bool causal, const Ctx& c) {
+#ifdef MDL_ABLATE_ATTN
+  return;
+#endif
+  const int L = c.L, n_items = c.nseq * 2 * L;
+  for (int it = c.tid; it < n_items; it += 256) {
+    const int s = it / (2 * L), rem = it - s * 2 * L, h = rem / L, j = rem - h * L;
+    const int row = s * L + j;
+    uint32_t k[16], v[16];
+    ld_head_u(K, row, h, k);
+    ld_head_u(V, row, h, v);
+    float dk[32], dv[32];
+#pragma unroll
+    for (int d = 0; d < 32; ++d) { dk[d] = 0.f; dv[d] = 0.f; }
+    const int base = (s * 2 + h) * L;
+    for (int i = causal ? j : 0; i < L; ++i) {
+      const int qr = s * L + i;
+      uint32_t q[16], da[16];
+      ld_head_u(Q, qr, h, q);
+      ld_head_u(DA, qr, h, da);
+      float d = 0.f, dp = 0.f;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) { d = dot2(q[t], k[t], d); dp = dot2(da[t], v[t], dp); }
+      const float p = __expf(d * ATT_SCALE - c.LSE[base + i]);
+      const float ds = p * (dp - c.DEL[base + i]);
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        dk[2 * t] += ds * lo_bf(q[t]); dk[2 * t + 1] += ds * hi_bf(q[t]);
+        dv[2 * t] += p * lo_bf(da[t]); dv[2 * t + 1] += p * hi_bf(da[t]);
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < 32; ++d) dk[d] *= ATT_SCALE;
+    st_head_f(K, row, h, dk);
+    st_head_f(V, row, h, dv);
+  }
+}
+
+// ------------------------------------------------------------------------------------------ helpers
+// copy the valid rows of row tile rt of a swizzled LDS buffer to a plain global [tok][64] bf16 tensor
+__device__ __forceinline__ void tile2g(bf16_t* dst, const bf16_t* buf, int rt, const Ctx& c) {
+  for (int i = c.lane; i < 16 * 8; i += 64) {
+    const int row = rt * 16 + (i >> 3), lc = i & 7;
+    if (row < c.NR)
+      *(uint4*)(dst + (size_t)(c.tok0 + row) * 64 + lc * 8) =
+          *(const uint4*)(buf + (row << 6) + ((lc ^ ((row >> 1) & 7)) << 3));
+  }
+}
+
+__device__ __forceinline__ void g2tile(bf16_t* buf, const bf16_t* src, int rt, const Ctx& c) {
+  for (int i = c.lane; i < 16 * 8; i += 64) {
+    const int row = rt * 16 + (i >> 3), lc = i & 7;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (row < c.NR) v = *(const uint4*)(src + (size_t)(c.tok0 + row) * 64 + lc * 8);
+    *(uint4*)(buf + (row << 6) + ((lc ^ ((row >> 1) & 7)) << 3)) = v;
+  }
+}
+
+// load a saved bf16 activation tile as an RT via LDS staging (vector global loads; buf rows of tile rt are
+// overwritten and keep the activation, usable as a GEMM / weight-gradient operand afterwards)
+__device__ __forceinline__ void ld_saved(bf16_t* buf, const bf16_t* src, int rt, RT& t, const Ctx& c) {
+  g2tile(buf, src, rt, c);
+  wave_lds_sync();
+  ld_tm(buf, rt, t, c.lane);
+}
+
+__device__ __forceinline__ void gelu_rt(RT& t) {
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) t.v[ct][r] = gelu_erf(t.v[ct][r]);
+}
+
+__device__ __forceinline__ void zero_lds(char* smem, size_t bytes, int tid) {
+  for (size_t i = (size_t)tid * 16; i < bytes; i += 256 * 16) *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
+}
+
+__device__ __forceinline__ void flush_ln(f32x4 dg, f32x4 db, const LNp& ln, int lane) {
+  flush_cols(dg, ln.dg, lane);
+  flush_cols(db, ln.db, lane);
+}
+
+// ------------------------------------------------------------------------------------------ sublayers (forward)
+template <bool SAVE>
+__device__ __forceinline__ void attn_self_fwd(const Mat* m, const LNp& ln, RT* xr, const Sv& sv, bool causal, bf16_t* sv_xin,
+                              bf16_t* sv_a, float* sv_lse, const Ctx& c) {
+  const int lane = c.lane;
+#pragma unroll
+  for (int k = 0; k < MAXRT; ++k) {
+    const int rt = c.wave + 4 * k;
+    if (rt < c.NT) {
+      st_tm_m(c.XB, rt, xr[k], row_mask(rt, c.NR, lane), lane);
+      if (SAVE) { wave_lds_sync(); tile2g(sv_xin, c.XB, rt, c); }
+    }
+  }
+  wave_lds_sync();
+  bf16_t* outs[3] = {c.QB, c.KB, c.VB};
+#pragma unroll
+  for (int mi = 0; mi < 3; ++mi) {
+    BFr B;
+    loadB(B, m[mi].fw, lane);
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) {
+        RT t;
+        gemm_rt(t, c.XB, rt, B, lane, false);
+        add_bias(t, m[mi].b, lane);
+        st_tm_m(outs[mi], rt, t, row_mask(rt, c.NR, lane), lane);
+      }
+    }
+  }
+  __syncthreads();
+  attn_fwd(c.QB, c.KB, c.VB, c.QB, causal, SAVE ? sv_lse : nullptr, c);
+  __syncthreads();
+  BFr B;
+  loadB(B, m[3].fw, lane);
+#pragma unroll
+  for (int k = 0; k < MAXRT; ++k) {
+    const int rt = c.wave + 4 * k;
+    if (rt < c.NT) {
+      if (SAVE) tile2g(sv_a, c.QB, rt, c);
+      RT t, xh, y;
+      gemm_rt(t, c.QB, rt, B, lane, false);
+      add_bias(t, m[3].b, lane);
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) t.v[ct] += xr[k].v[ct];
+      f32x4 mu, rs;
+      ln_fwd(t, xh, y, mu, rs, ln.g, ln.b, lane);
+      xr[k] = y;
+    }
+  }
+}
+
+template <bool SAVE>
+__device__ __forceinline__ void mlp_fwd(const Mat& m1, const Mat& m2, const LNp& ln, RT* xr, bf16_t* sv_x, bf16_t* sv_h,
+                        const Ctx& c) {
+  const int lane = c.lane;
+  BFr B1, B2;
+  loadB(B1, m1.fw, lane);
+  loadB(B2, m2.fw, lane);
+#pragma unroll
+  for (int k = 0; k < MAXRT; ++k) {
+    const int rt = c.wave + 4 * k;
+    if (rt < c.NT) {
+      const f32x4 vm = row_mask(rt, c.NR, lane);
+      st_tm_m(c.XB, rt, xr[k], vm, lane);
+      wave_lds_sync();
+      if (SAVE) tile2g(sv_x, c.XB, rt, c);
+      RT h;
+      gemm_rt(h, c.XB, rt, B1, lane, false);
+      add_bias(h, m1.b, lane);
+      if (SAVE) {
+        st_tm_m(c.XB, rt, h, vm, lane);
+        wave_lds_sync();
+        tile2g(sv_h, c.XB, rt, c);
+      }
+      gelu_rt(h);
+      st_tm_m(c.XB, rt, h, vm, lane);
+      wave_lds_sync();
+      RT mo, xh, y;
+      gemm_rt(mo, c.XB, rt, B2, lane, false);
+      add_bias(mo, m2.b, lane);
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) mo.v[ct] += xr[k].v[ct];
+      f32x4 mu, rs;
+      ln_fwd(mo, xh, y, mu, rs, ln.g, ln.b, lane);
+      xr[k] = y;
+    }
+  }
+}
+
+// obs embedding (VALU; obs_dim <= 16): x0 = LN0(GELU(W_e · LN_obs(obs) + b_e))  — ma_transformer.py:133-134,151
+struct EmbRow { float oh[16]; float ohat[16]; };
+
+__device__ __forceinline__ void obs_ln_row(const EncP& p, int tok, bool valid, EmbRow& er) {
+  const int od = p.od;
+  float o[16];
+  float mean = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) { o[k] = (valid && k < od) ? p.obs[(size_t)tok * od + k] : 0.f; mean += o[k]; }
+  mean /= (float)od;
+  float var = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) if (k < od) { const float d = o[k] - mean; var += d * d; }
+  const float rstd = rsqrtf(var / (float)od + 1e-5f);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    er.ohat[k] = k < od ? (o[k] - mean) * rstd : 0.f;
+    er.oh[k] = k < od ? er.ohat[k] * p.lno_g[k] + p.lno_b[k] : 0.f;
+  }
+}
+
+__device__ __forceinline__ void embed_pre(const EncP& p, int rt, RT& pre, EmbRow* er, const Ctx& c) {
+  const int g = c.lane >> 4, c16 = c.lane & 15;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = rt * 16 + 4 * g + r;
+    obs_ln_row(p, c.tok0 + row, row < c.NR, er[r]);
+  }
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) {
+    const int col = 16 * ct + c16;
+    float w[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) w[k] = k < p.od ? p.we[col * p.od + k] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float s = p.be[col];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) s += w[k] * er[r].oh[k];
+      pre.v[ct][r] = s;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------ sublayers (backward)
+__device__ __forceinline__ void mlp_bwd(const Mat& m1, const Mat& m2, const LNp& ln, RT* dx, const bf16_t* sv_x, const bf16_t* sv_h,
+                        const Ctx& c) {
+  const int lane = c.lane;
+  f32x4 dlg = {0, 0, 0, 0}, dlb = {0, 0, 0, 0}, db1 = {0, 0, 0, 0}, db2 = {0, 0, 0, 0};
+  {
+    BFr B2f, B2b, B1b;
+    loadB(B2f, m2.fw, lane);
+    loadB(B2b, m2.bw, lane);
+    loadB(B1b, m1.bw, lane);
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) {
+        const f32x4 vm = row_mask(rt, c.NR, lane);
+        RT x, h, gl;
+        ld_saved(c.QB, sv_x, rt, x, c);     // QB rows = X of dW1
+        ld_saved(c.XB, sv_h, rt, h, c);
+        gl = h;
+        gelu_rt(gl);
+        st_tm_m(c.XB, rt, gl, vm, lane);   // X of dW2
+        wave_lds_sync();
+        RT mo, xh, y, ds;
+        gemm_rt(mo, c.XB, rt, B2f, lane, false);
+        add_bias(mo, m2.b, lane);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) mo.v[ct] += x.v[ct];
+        f32x4 mu, rs;
+        ln_fwd(mo, xh, y, mu, rs, ln.g, ln.b, lane);
+        ln_bwd(dx[k], xh, rs, ln.g, ds, dlg, dlb, vm, lane);
+        colsum_acc(ds, db2, vm);
+        st_tm_m(c.DA, rt, ds, vm, lane);   // dY of dW2
+        wave_lds_sync();
+        RT dg;
+        gemm_rt(dg, c.DA, rt, B2b, lane, false);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dg.v[ct][r] *= gelu_erf_grad(h.v[ct][r]) * vm[r];
+        colsum_acc(dg, db1, vm);
+        st_tm_m(c.KB, rt, dg, vm, lane);   // dY of dW1
+        wave_lds_sync();
+        RT t;
+        gemm_rt(t, c.KB, rt, B1b, lane, false);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) dx[k].v[ct] = ds.v[ct] + t.v[ct];
+      }
+    }
+  }
+  flush_ln(dlg, dlb, ln, lane);
+  flush_cols(db1, m1.db, lane);
+  flush_cols(db2, m2.db, lane);
+  __syncthreads();
+  wgrad_tm(c.DA, c.XB, c.NRP, m2.dW, c.wave, lane);
+  wgrad_tm(c.KB, c.QB, c.NRP, m1.dW, c.wave, lane);
+  __syncthreads();
+}
+
+// attention sublayer backward: out = LN(res + proj(attn(q(qin), k(kvin), v(kvin))))
+// self: qin = kvin = res = saved block input (sv_xin);  grads w.r.t. the input accumulate into dx.
+__device__ __forceinline__ void attn_self_bwd(const Mat* m, const LNp& ln, RT* dx, const bf16_t* sv_xin, const bf16_t* sv_a,
+                              const float* sv_lse, bool causal, const Ctx& c) {
+  const int lane = c.lane;
+  f32x4 dlg = {0, 0, 0, 0}, dlb = {0, 0, 0, 0}, dbp = {0, 0, 0, 0};
+  {
+    BFr Bpf, Bpb;
+    loadB(Bpf, m[3].fw, lane);
+    loadB(Bpb, m[3].bw, lane);
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) {
+        const f32x4 vm = row_mask(rt, c.NR, lane);
+        RT a, xin;
+        g2tile(c.XB, sv_a, rt, c);          // X of dWp
+        ld_saved(c.DA, sv_xin, rt, xin, c);
+        RT s, xh, y, ds;
+        gemm_rt(s, c.XB, rt, Bpf, lane, false);
+        add_bias(s, m[3].b, lane);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) s.v[ct] += xin.v[ct];
+        f32x4 mu, rs;
+        ln_fwd(s, xh, y, mu, rs, ln.g, ln.b, lane);
+        ln_bwd(dx[k], xh, rs, ln.g, ds, dlg, dlb, vm, lane);
+        colsum_acc(ds, dbp, vm);
+        st_tm_m(c.DQ, rt, ds, vm, lane);   // dY of dWp (= d proj output)
+        wave_lds_sync();
+        RT da;
+        gemm_rt(da, c.DQ, rt, Bpb, lane, false);
+        st_tm_m(c.DA, rt, da, vm, lane);
+        dx[k] = ds;                          // residual path
+      }
+    }
+  }
+  flush_ln(dlg, dlb, ln, lane);
+  flush_cols(dbp, m[3].db, lane);
+  __syncthreads();
+  wgrad_tm(c.DQ, c.XB, c.NRP, m[3].dW, c.wave, lane);
+  __syncthreads();
+  // recompute q, k, v from the saved input (whole tile, cooperative copy)
+  g2lds_rows(c.XB, sv_xin, c.tok0, c.NR, c.NT * 16, c.tid);
+  for (int it = c.tid; it < c.nseq * 2 * c.L; it += 256) {
+    const int s = it / (2 * c.L), rem = it - s * 2 * c.L, h = rem / c.L, i = rem - h * c.L;
+    c.LSE[it] = sv_lse[(size_t)(c.tok0 + s * c.L + i) * 2 + h];
+  }
+  __syncthreads();
+  {
+    bf16_t* outs[3] = {c.QB, c.KB, c.VB};
+#pragma unroll
+    for (int mi = 0; mi < 3; ++mi) {
+      BFr B;
+      loadB(B, m[mi].fw, lane);
+#pragma unroll
+      for (int k = 0; k < MAXRT; ++k) {
+        const int rt = c.wave + 4 * k;
+        if (rt < c.NT) {
+          RT t;
+          gemm_rt(t, c.XB, rt, B, lane, false);
+          add_bias(t, m[mi].b, lane);
+          st_tm_m(outs[mi], rt, t, row_mask(rt, c.NR, lane), lane);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  attn_bwd_q(c.QB, c.KB, c.VB, c.DA, c.DQ, causal, c);
+  __syncthreads();
+  attn_bwd_kv(c.QB, c.KB, c.VB, c.DA, causal, c);
+  __syncthreads();
+  wgrad_tm(c.DQ, c.XB, c.NRP, m[0].dW, c.wave, lane);
+  wgrad_tm(c.KB, c.XB, c.NRP, m[1].dW, c.wave, lane);
+  wgrad_tm(c.VB, c.XB, c.NRP, m[2].dW, c.wave, lane);
+  const bf16_t* dsrc[3] = {c.DQ, c.KB, c.VB};
+#pragma unroll
+  for (int mi = 0; mi < 3; ++mi) {
+    BFr B;
+    loadB(B, m[mi].bw, lane);
+    f32x4 dbb = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) {
+        const f32x4 vm = row_mask(rt, c.NR, lane);
+        RT g, t;
+        ld_tm(dsrc[mi], rt, g, lane);
+        colsum_acc(g, dbb, vm);
+        gemm_rt(t, dsrc[mi], rt, B, lane, false);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) dx[k].v[ct] += t.v[ct];
+      }
+    }
+    flush_cols(dbb, m[mi].db, lane);
+  }
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------------------------------ context
+template <typename PT>
+__device__ __forceinline__ Ctx make_ctx(const PT& p, char* smem) {
+  Ctx c;
+  c.tid = threadIdx.x;
+  c.lane = c.tid & 63;
+  c.wave = c.tid >> 6;
+  c.L = p.L;
+  const int seq0 = blockIdx.x * p.SQ;
+  c.nseq = min(p.SQ, p.Bs - seq0);
+  c.NR = c.nseq * p.L;
+  c.NT = (c.NR + 15) >> 4;
+  c.NRP = p.NRP;
+  c.tok0 = seq0 * p.L;
+  const size_t bs = (size_t)p.NRP * 64;
+  bf16_t* base = (bf16_t*)smem;
+  c.QB = base; c.KB = base + bs; c.VB = base + 2 * bs; c.DA = base + 3 * bs; c.DQ = base + 4 * bs; c.XB = base + 5 * bs;
+  c.LSE = (float*)(base + 6 * bs);
+  c.DEL = c.LSE + p.SQ * 2 * p.L;
+  return c;
+}
+
+}  // namespace
+
+__host__ __device__ inline size_t mat_train_lds_bytes(int NRP, int SQ, int L) {
+  return (size_t)NRP * 64 * 2 * 6 + (size_t)SQ * 2 * L * 4 * 2;
+}
+
+
+template <typename K, typename PT>
+static int launch(K kern, const PT* p, hipStream_t st) {
+  const size_t lds = mat_train_lds_bytes(p->NRP, p->SQ, p->L);
+  if (lds > 160 * 1024) return -2;
+  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return (int)e;
+  const int grid = (p->Bs + p->SQ - 1) / p->SQ;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, *p);
+  MDL_CHECK_LAUNCH();
+  return 0;
+}
+

@@ -295,6 +295,9 @@ __device__ __forceinline__ bf16x8 ld_frag_T(const bf16_t* buf, int k0, int n0, i
 // padded rows zero).  Wave w produces dW rows n in [16w, 16w+16); fp32 atomics into the gradient.
 __device__ __forceinline__ void wgrad_tm(const bf16_t* Y, const bf16_t* X, int KP, float* dW, int wave, int lane) {
   if (!dW) return;
+#ifdef MDL_ABLATE_WGRAD
+  return;
+#endif
   const int g = lane >> 4, c16 = lane & 15;
   RT acc;
   rt_zero(acc);

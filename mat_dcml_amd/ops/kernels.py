@@ -15,7 +15,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "_lib", "libmatdcml.so")
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "_lib", os.environ.get("MAT_DCML_LIBNAME", "libmatdcml.so"))
 _lib = None
 _load_error = None
 

@@ -1,0 +1,38 @@
+"""Micro-benchmark of the fused training kernels on the bench minibatch shape (3200 sequences x 33 agents)."""
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, "/root/repo/tests")
+sys.path.insert(0, "/root/repo")
+from test_gpu_train import make  # noqa: E402
+from mat_dcml_amd.ops import mat_train  # noqa: E402
+
+
+def main(B=3200, L=33, iters=10):
+    dev = torch.device("cuda")
+    m = make(L, dev, seed=0, scale=0.05)
+    obs = torch.rand(B, L, 7, device=dev)
+    ava = torch.ones(B, L, 2, device=dev)
+    actions = (torch.rand(B, L, 1, device=dev) < 0.5).float()
+    for p in m.parameters():
+        p.grad = torch.zeros_like(p)
+    enc, dec = mat_train.EncoderFused(m), mat_train.DecoderFused(m)
+    ev = {k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for k in
+          ("enc_fwd", "dec_fwd", "dec_bwd", "enc_bwd")}
+    tot = {k: 0.0 for k in ev}
+    for it in range(iters + 2):
+        ev["enc_fwd"][0].record(); v, rep = enc.forward(obs); ev["enc_fwd"][1].record()
+        ev["dec_fwd"][0].record(); lp, ent = dec.forward(rep, actions, ava); ev["dec_fwd"][1].record()
+        ev["dec_bwd"][0].record(); drep = dec.backward(torch.ones_like(lp), torch.ones_like(ent)); ev["dec_bwd"][1].record()
+        ev["enc_bwd"][0].record(); enc.backward(drep, torch.ones_like(v)); ev["enc_bwd"][1].record()
+        torch.cuda.synchronize()
+        if it >= 2:
+            for k, (s, e) in ev.items():
+                tot[k] += s.elapsed_time(e)
+    print(" | ".join(f"{k} {v / iters * 1e3:.0f} us" for k, v in tot.items()), flush=True)
+
+
+if __name__ == "__main__":
+    main()
