@@ -119,6 +119,8 @@ _DCML_FLAGS = [
 # framework (new)
 _FRAMEWORK_FLAGS = [
     ("n_workers", int, 100, "DCML worker count W (agents = W + 1); 4 / 32 / 100 / 128 in the BASELINE configs"),
+    ("shannon", "true", F, "Shannon-capacity links in the DCML env (shannon_enable, Shannon.py)"),
+    ("central_execution", int, 1, "1: one Semi_Discrete space for all agents; 0: per-agent spaces (Env(central_execution=False))"),
     ("kernels", str, "auto", "auto|hip|torch — fused HIP kernels on GPU (auto) or the PyTorch reference path"),
     ("dtype", str, "bf16", "bf16|fp32 compute dtype (master weights and optimizer state are fp32)"),
     ("train_stride", int, 1, "decision stride for rollouts (1 = exact per-agent sampling, the reference)"),

@@ -41,7 +41,7 @@ __host__ __device__ __forceinline__ float u01_open_f(uint32_t u) { return ((floa
 
 enum Purpose : uint32_t {
   P_MASTER = 1, P_ARRIVE = 2, P_WORKER_PR = 3, P_NOISE = 4, P_DISABLE = 5, P_DOWNLOAD = 6, P_UPLOAD = 7,
-  P_DONE = 8, P_POLICY = 16
+  P_DONE = 8, P_SHANNON = 9, P_POLICY = 16
 };
 
 // ------------------------------------------------------------------------------------------ wave64 reductions

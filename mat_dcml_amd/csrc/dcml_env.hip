@@ -14,10 +14,12 @@ using namespace mdl;
 
 struct EnvCfg {
   int E, W, A, P, obs_dim, share_dim;
-  int fixed, preset, max_disable, max_slot_iters, preset_rows;
+  int fixed, preset, max_disable, max_slot_iters, preset_rows, shannon;
   uint32_t k0, k1;
   double r_min, r_max, c_min, c_max, r_hi, c_hi, pr_min, pr_max;
   double rate, freq, bit_to_byte, continue_prob, alpha, beta, standalone_penalty, fixed_k_ratio;
+  // Shannon links (Shannon.py:6-21): band = B_total / W, noise in mW, uniform ranges, path-loss exponent
+  double band, noise, mp_lo, mp_hi, wp_lo, wp_hi, d_lo, d_hi, ple;
   float master_feature;
 };
 
@@ -39,6 +41,8 @@ struct EnvState {
   const double* preset_master;   // (rows, 3)
   const double* preset_prs;      // (rows, W)
   const int64_t* preset_disable; // (rows)
+  double* rate;              // (E, W) download rate per link (constant unless Shannon)
+  double* up_rate;           // (E, W) upload rate per link (only reported in share_obs)
 };
 
 struct StepOut {
@@ -103,6 +107,20 @@ __device__ void env_reset(const EnvCfg& c, const EnvState& s, int e) {
     if (w < W) wpr = s.preset_prs[idx * W + w];
     dis = s.preset_disable[idx];
   }
+  double rate_dn = c.rate, rate_up = c.rate;
+  if (c.shannon) {   // DCML_Master.get_transmission_rate (:41-45) + Shannon.upload/download (:14-21)
+    mpr = 0.0;
+    u4 um2 = philox4x32_10(ctr, g, 0xFFFFu, P_SHANNON, c.k0, c.k1);
+    const double mp = c.mp_lo + u01_open(um2.x) * (c.mp_hi - c.mp_lo);
+    if (w < W) {
+      u4 us = philox4x32_10(ctr, g, (uint32_t)w, P_SHANNON, c.k0, c.k1);
+      const double d = c.d_lo + u01_open(us.x) * (c.d_hi - c.d_lo);
+      const double wp = c.wp_lo + u01_open(us.y) * (c.wp_hi - c.wp_lo);
+      const double gain = pow(d, c.ple) / c.noise;
+      rate_dn = c.band * log2(1.0 + mp * gain);
+      rate_up = c.band * log2(1.0 + wp * gain);
+    }
+  }
   if (dis < 0) dis = 0;
   if (dis > W - 1) dis = W - 1;
   if (w < W) s_key[w] = key;
@@ -158,7 +176,14 @@ __device__ void env_reset(const EnvCfg& c, const EnvState& s, int e) {
     }
     s.worker_pr[(size_t)e * W + w] = wpr;
     s.avail[(size_t)e * W + w] = av;
-    s.share[(size_t)e * c.share_dim + 2 + w] = (float)wpr;
+    if (c.shannon) {   // share = R, C, upload/1e7, download/1e7 (ENV_SingleProcess.py:253-255)
+      s.share[(size_t)e * c.share_dim + 2 + w] = (float)(rate_up / 1e7);
+      s.share[(size_t)e * c.share_dim + 2 + W + w] = (float)(rate_dn / 1e7);
+      s.rate[(size_t)e * W + w] = rate_dn;
+      s.up_rate[(size_t)e * W + w] = rate_up;
+    } else {
+      s.share[(size_t)e * c.share_dim + 2 + w] = (float)wpr;
+    }
     float* a = s.ava + ((size_t)e * c.A + w) * 2;
     a[0] = 1.f; a[1] = av ? 1.f : 0.f;
   }
@@ -223,10 +248,11 @@ __global__ __launch_bounds__(MAXW) void dcml_env_step_kernel(EnvCfg c, EnvState 
   int tp0 = 0;
   if (valid) {
     const double pr = s.worker_pr[(size_t)e * W + w];
+    const double rate = c.shannon ? s.rate[(size_t)e * W + w] : c.rate;  // Worker.process: download rate, both legs
     double need = ceil((9.0 * r - 3.0) * cc) / c.freq;
     u4 ud = philox4x32_10(ctr, g, (uint32_t)w, P_DOWNLOAD, c.k0, c.k1);
     double n = 1.0 + geom_extra(ud.x, pr);
-    const double transmit = ((ceil((r + 1.0) * cc) * c.bit_to_byte) / c.rate + 0.001) * n;
+    const double transmit = ((ceil((r + 1.0) * cc) * c.bit_to_byte) / rate + 0.001) * n;
     price0 = floor(transmit) * 0.1;
     const double arrive_slot = floor(transmit + arrive);
     int tp = (int)fmod(arrive_slot, (double)P);
@@ -235,7 +261,7 @@ __global__ __launch_bounds__(MAXW) void dcml_env_step_kernel(EnvCfg c, EnvState 
     const double lwt = (double)lw[tp];
     if (frac > lwt) need = need + frac - lwt;
     double availability = 0.0;
-    const double up_unit = (r * c.bit_to_byte) / c.rate + 0.001;
+    const double up_unit = (r * c.bit_to_byte) / rate + 0.001;
     int it = 0;
     while (availability < need && it < c.max_slot_iters) {
       const double a = 1.0 - (double)lw[tp];

@@ -38,6 +38,13 @@ class DCMLConfig:
     master_feature: float = 1.1          # last feature of the master row (ENV_SingleProcess.py:236)
     fixed_k_ratio: float = 0.7           # fixed heuristic K = floor(0.7 N) (ENV_SingleProcess.py:58-62)
     max_slot_iters: int = 512            # bound on the timeslot loop (measured max 15)
+    shannon: bool = False                # shannon_enable: per-worker Shannon-capacity links (Shannon.py:6-21)
+    bandwidth_total: float = 100e9       # B_total, split evenly over the workers (DCML_Master.py:27-28)
+    noise_dbm: float = -50.0             # Shannon(noise=-50) (Shannon.py:7-9)
+    master_power: tuple = (50.0, 60.0)   # TRANSMISSION_POWER_{LOWER,UPPER}_BOUND (DCML_Master.py:11-12)
+    worker_power: tuple = (10.0, 20.0)   # MIN/MAX_WORKER_POWER (DCML_Config.py:10-11)
+    distance: tuple = (10.0, 100.0)      # DISTANCE_{LOWER,UPPER}_BOUND (DCML_Master.py:13-14)
+    path_loss_exp: float = -4.0          # PATH_LOSS_EXPONENT (Shannon.py:4)
     obs_dim: int = 7                     # LOCAL_OBS_DIM
     action_dim: int = 2                  # ACTION_DIM
     workload_file: str = os.path.join(DATA_DIR, "workloads.txt")
@@ -49,8 +56,8 @@ class DCMLConfig:
         return self.n_workers + self.extra_agents
 
     @property
-    def share_dim(self) -> int:          # SOB_DIM = 2 + W (DCML_Config.py:12)
-        return 2 + self.n_workers
+    def share_dim(self) -> int:          # SOB_DIM = 2 + W (DCML_Config.py:12); Shannon: R, C, up/1e7, down/1e7
+        return 2 + self.n_workers * (2 if self.shannon else 1)
 
     @property
     def max_disable(self) -> int:

@@ -61,11 +61,14 @@ class DeviceDCMLEnv:
         self.n_disable = torch.zeros(E, dtype=i64, device=dev)
         self.arrive = torch.zeros(E, dtype=i64, device=dev)
         self.lw = torch.zeros(E, W, P, dtype=f32, device=dev)
+        self.rate = torch.full((E, W), self.cfg.data_rate, dtype=f64, device=dev)   # download rate per link
+        self.up_rate = torch.full((E, W), self.cfg.data_rate, dtype=f64, device=dev)
         self.obs = torch.zeros(E, A, self.cfg.obs_dim, dtype=f32, device=dev)
         self.share = torch.zeros(E, self.cfg.share_dim, dtype=f32, device=dev)
         self.ava = torch.zeros(E, A, 2, dtype=f32, device=dev)
         # preset replay tables (Sample_1 by default)
         self.preset_idx = torch.zeros(E, dtype=i64, device=dev)
+        self.preset_start = torch.zeros(E, dtype=i64, device=dev)   # first preset row per env (benchmark sharding)
         if preset:
             m, prs, dis = load_preset(self.cfg)
             self.preset_master = torch.tensor(m, dtype=f64, device=dev)
@@ -103,10 +106,23 @@ class DeviceDCMLEnv:
         if Pr is not None:
             self.preset_prs[:] = float(Pr)
 
+    def set_preset_tables(self, master, worker_prs, disable, start):
+        """Install stacked preset tables (G sweep points x rows) and each env's first row.
+
+        Used by the benchmark to run every sweep point (and several shards of each point's episode sequence) as
+        independent envs of ONE batched env, instead of the reference's one-env-per-point Python loop.
+        """
+        assert self.preset
+        dev = self.device
+        self.preset_master = torch.as_tensor(master, dtype=torch.float64, device=dev).contiguous()
+        self.preset_prs = torch.as_tensor(worker_prs, dtype=torch.float64, device=dev).contiguous()
+        self.preset_disable = torch.as_tensor(disable, dtype=torch.int64, device=dev).contiguous()
+        self.preset_start = torch.as_tensor(start, dtype=torch.int64, device=dev).contiguous()
+
     # ------------------------------------------------------------------ public API
     def reset(self):
         self.counter.zero_()
-        self.preset_idx.zero_()
+        self.preset_idx.copy_(self.preset_start)
         self._reset(torch.ones(self.E, dtype=torch.bool, device=self.device))
         return self.obs, self.share_view(), self.ava
 
@@ -149,6 +165,9 @@ class DeviceDCMLEnv:
             mpr = self.preset_master[idx, 2].clone()
             wpr = self.preset_prs[idx].clone()
             dis = self.preset_disable[idx].clone()
+        if cfg.shannon:
+            rate_dn, rate_up = self._shannon_rates(ctr, wi)
+            mpr = torch.zeros_like(mpr)                        # DCML_Master.reset: Pr = 0 under Shannon
         dis = dis.clamp(0, W - 1)
         # disabled subset = the `dis` workers with the smallest random keys (ties by index)
         kk = key.view(E, W, 1)
@@ -179,7 +198,25 @@ class DeviceDCMLEnv:
         self.worker_pr = torch.where(m2, wpr, self.worker_pr)
         self.avail = torch.where(m2, avail, self.avail)
         self.lw = torch.where(m.view(E, 1, 1), lw, self.lw)
+        if cfg.shannon:
+            self.rate = torch.where(m2, rate_dn, self.rate)
+            self.up_rate = torch.where(m2, rate_up, self.up_rate)
         self._build_obs()
+
+    def _shannon_rates(self, ctr, wi):
+        """Shannon-capacity links (``Shannon.py:14-21``, ``DCML_Master.get_transmission_rate`` ``:41-45``):
+        rate = B log2(1 + P d^-4 / noise) with B = B_total / W, master power ~ U(50,60) per task, worker power
+        ~ U(10,20) and distance ~ U(10,100) per worker.  Returns (download, upload) in bytes/s."""
+        cfg, E = self.cfg, self.E
+        us = px.philox4x32(ctr.view(E, 1), self.gid.view(E, 1), wi, px.P_SHANNON, self.k0, self.k1)
+        dist = cfg.distance[0] + px.u01_open(us[0]) * (cfg.distance[1] - cfg.distance[0])
+        wpow = cfg.worker_power[0] + px.u01_open(us[1]) * (cfg.worker_power[1] - cfg.worker_power[0])
+        um = px.philox4x32(ctr, self.gid, 0xFFFF, px.P_SHANNON, self.k0, self.k1)
+        mpow = (cfg.master_power[0] + px.u01_open(um[0]) * (cfg.master_power[1] - cfg.master_power[0])).view(E, 1)
+        band = cfg.bandwidth_total / self.W
+        noise = 10.0 ** (cfg.noise_dbm / 10.0)
+        gain = torch.pow(dist, cfg.path_loss_exp) / noise
+        return band * torch.log2(1.0 + mpow * gain), band * torch.log2(1.0 + wpow * gain)
 
     def _build_obs(self):
         cfg, E, W, P = self.cfg, self.E, self.W, self.P
@@ -210,7 +247,11 @@ class DeviceDCMLEnv:
         master = torch.stack([Rn, Cn, mu0, mu1, mu2, mpr.to(torch.float32),
                               torch.full_like(Rn, cfg.master_feature)], -1)
         self.obs = torch.cat([obs_w, master.view(E, 1, -1)], 1).contiguous()
-        self.share = torch.cat([Rn.view(E, 1), Cn.view(E, 1), self.worker_pr.to(torch.float32)], 1).contiguous()
+        if cfg.shannon:   # ENV_SingleProcess.py:253-255
+            self.share = torch.cat([Rn.view(E, 1), Cn.view(E, 1), (self.up_rate / 1e7).to(torch.float32),
+                                    (self.rate / 1e7).to(torch.float32)], 1).contiguous()
+        else:
+            self.share = torch.cat([Rn.view(E, 1), Cn.view(E, 1), self.worker_pr.to(torch.float32)], 1).contiguous()
         ava = torch.ones(E, self.A, 2, dtype=torch.float32, device=dev)
         ava[:, :W, 1] = avf
         self.ava = ava
@@ -249,7 +290,8 @@ class DeviceDCMLEnv:
         need = torch.ceil((9 * rr - 3) * cc) / cfg.frequency                   # SECOND_TO_CENTSEC * ceil(.)/freq
         ud = px.philox4x32(ctr.view(E, 1), self.gid.view(E, 1), wi, px.P_DOWNLOAD, self.k0, self.k1)
         n = 1 + self._geom(ud[0], pr)
-        transmit = ((torch.ceil((rr + 1) * cc) * cfg.bit_to_byte) / cfg.data_rate + 0.001) * n
+        rate = self.rate                                       # Worker.process uses the download rate for both legs
+        transmit = ((torch.ceil((rr + 1) * cc) * cfg.bit_to_byte) / rate + 0.001) * n
         price0 = torch.floor(transmit) * 0.1
         arrive = self.arrive.view(E, 1).to(f64)
         arrive_slot = torch.floor(transmit + arrive)
@@ -260,7 +302,7 @@ class DeviceDCMLEnv:
         need = torch.where(frac > lw_tp, need + frac - lw_tp, need)
         availability = torch.zeros_like(need)
         nslots = torch.zeros_like(need)
-        up_unit = (rr * cfg.bit_to_byte) / cfg.data_rate + 0.001
+        up_unit = (rr * cfg.bit_to_byte) / rate + 0.001
         active = availability < need
         it = 0
         while bool(active.any()) and it < cfg.max_slot_iters:
@@ -314,7 +356,8 @@ class DeviceDCMLEnv:
     def _state_ptrs(self):
         return dict(R=self.R, C=self.C, master_pr=self.master_pr, worker_pr=self.worker_pr,
                     n_disable=self.n_disable, arrive=self.arrive, lw=self.lw, obs=self.obs,
-                    share=self.share, ava=self.ava, counter=self.counter, task_ctr=self.task_ctr)
+                    share=self.share, ava=self.ava, counter=self.counter, task_ctr=self.task_ctr, rate=self.rate,
+                    up_rate=self.up_rate)
 
     def _reset_hip(self, mask):
         from ...ops import kernels

@@ -108,18 +108,20 @@ def philox_fill(n, c1, c2, c3, k0, k1, device):
 # ----------------------------------------------------------------------------------------- DCML env
 class EnvCfg(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in ("E", "W", "A", "P", "obs_dim", "share_dim", "fixed", "preset",
-                                            "max_disable", "max_slot_iters", "preset_rows")] + \
+                                            "max_disable", "max_slot_iters", "preset_rows", "shannon")] + \
                [("k0", ctypes.c_uint32), ("k1", ctypes.c_uint32)] + \
                [(n, ctypes.c_double) for n in ("r_min", "r_max", "c_min", "c_max", "r_hi", "c_hi", "pr_min", "pr_max",
                                                "rate", "freq", "bit_to_byte", "continue_prob", "alpha", "beta",
-                                               "standalone_penalty", "fixed_k_ratio")] + \
+                                               "standalone_penalty", "fixed_k_ratio", "band", "noise", "mp_lo",
+                                               "mp_hi", "wp_lo", "wp_hi", "d_lo", "d_hi", "ple")] + \
                [("master_feature", ctypes.c_float)]
 
 
 class EnvState(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in ("gid", "profiles", "counter", "task_ctr", "R", "C", "master_pr",
                                                "worker_pr", "avail", "n_disable", "arrive", "lw", "obs", "share",
-                                               "ava", "preset_idx", "preset_master", "preset_prs", "preset_disable")]
+                                               "ava", "preset_idx", "preset_master", "preset_prs", "preset_disable",
+                                               "rate", "up_rate")]
 
 
 class StepOut(ctypes.Structure):
@@ -138,13 +140,17 @@ def _env_structs(env):
                 r_min=c.r_min, r_max=c.r_max, c_min=c.c_min, c_max=c.c_max, r_hi=c.r_hi, c_hi=c.c_hi,
                 pr_min=c.pr_min, pr_max=c.pr_max, rate=c.data_rate, freq=c.frequency, bit_to_byte=c.bit_to_byte,
                 continue_prob=c.continue_prob, alpha=c.alpha, beta=c.beta, standalone_penalty=c.standalone_penalty,
-                fixed_k_ratio=c.fixed_k_ratio, master_feature=c.master_feature)
+                fixed_k_ratio=c.fixed_k_ratio, master_feature=c.master_feature, shannon=int(c.shannon),
+                band=c.bandwidth_total / env.W, noise=10.0 ** (c.noise_dbm / 10.0), mp_lo=c.master_power[0],
+                mp_hi=c.master_power[1], wp_lo=c.worker_power[0], wp_hi=c.worker_power[1], d_lo=c.distance[0],
+                d_hi=c.distance[1], ple=c.path_loss_exp)
     pm = env.preset_master if env.preset else None
     pp = env.preset_prs if env.preset else None
     pd = env.preset_disable if env.preset else None
     es = EnvState(*[t.data_ptr() if t is not None else None for t in (
         env.gid, env.profiles, env.counter, env.task_ctr, env.R, env.C, env.master_pr, env.worker_pr, env.avail,
-        env.n_disable, env.arrive, env.lw, env.obs, env.share, env.ava, env.preset_idx, pm, pp, pd)])
+        env.n_disable, env.arrive, env.lw, env.obs, env.share, env.ava, env.preset_idx, pm, pp, pd, env.rate,
+        env.up_rate)])
     return ec, es
 
 

@@ -52,7 +52,8 @@ class DCMLRunner:
         self.save_interval, self.log_interval = a.save_interval, a.log_interval
         self.use_eval, self.eval_interval = a.use_eval, a.eval_interval
         self.train_stride, self.eval_stride = getattr(a, "train_stride", 1), getattr(a, "eval_stride", 2)
-        self.dcml = config.get("dcml_cfg") or DCMLConfig(n_workers=getattr(a, "n_workers", 100))
+        self.dcml = config.get("dcml_cfg") or DCMLConfig(n_workers=getattr(a, "n_workers", 100),
+                                                         shannon=bool(getattr(a, "shannon", False)))
         rank = self.comm.rank
         E = self.n_rollout_threads
         self.envs = config.get("envs") or DeviceDCMLEnv(E, self.dcml, self.device, seed=a.seed,

@@ -29,6 +29,7 @@ P_DISABLE = 5       # per-worker random key for the disabled subset
 P_DOWNLOAD = 6      # per-worker download retries
 P_UPLOAD = 7        # per-worker upload retries, sub = slot iteration
 P_DONE = 8          # per-env done draw
+P_SHANNON = 9       # Shannon link draws (distance, worker power; sub 0xFFFF = master power)
 P_POLICY = 16       # policy sampling streams (decode kernel)
 
 

@@ -96,3 +96,29 @@ def test_fixed_heuristic_distribution_matches_reference(tmp_path):
     assert ks_2samp(rp, op).pvalue > 1e-3, (np.mean(rp), np.mean(op))
     assert abs(np.mean(rd) - np.mean(od)) / np.mean(rd) < 0.05
     assert abs(np.mean(rp) - np.mean(op)) / np.mean(rp) < 0.05
+
+
+def test_shannon_links():
+    """shannon_enable: per-link Shannon rates (Shannon.py:14-21), share = [R, C, up/1e7, down/1e7], master Pr 0."""
+    cfg = DCMLConfig(n_workers=8, shannon=True)
+    env = DeviceDCMLEnv(16, cfg, seed=5)
+    obs, share, ava = env.reset()
+    assert share.shape == (16, 9, 2 + 16)
+    assert torch.all(env.master_pr == 0)
+    B = cfg.bandwidth_total / 8
+    noise = 10 ** (cfg.noise_dbm / 10)
+    # rates lie inside the bounds implied by the uniform ranges (distance 10..100, powers 50..60 / 10..20)
+    lo = B * np.log2(1 + 50 * 100.0 ** -4 / noise)
+    hi = B * np.log2(1 + 60 * 10.0 ** -4 / noise)
+    assert float(env.rate.min()) >= lo * 0.999 and float(env.rate.max()) <= hi * 1.001
+    assert torch.all(env.up_rate < env.rate)       # worker power < master power on the same distance
+    assert torch.allclose(share[:, 0, 2:10], (env.up_rate / 1e7).float())
+    act = torch.ones(16, 9)
+    act[:, -1] = 0.5
+    _, _, rew, done, delay, pay, _ = env.step(act)
+    assert torch.isfinite(rew).all() and (delay > 0).all()
+    # faster links than the fixed 150 MiB/s rate → shorter transfer legs than the non-Shannon env on the same task
+    ref = DeviceDCMLEnv(16, DCMLConfig(n_workers=8), seed=5)
+    ref.reset()
+    _, _, _, _, d_ref, _, _ = ref.step(act)
+    assert float(delay.mean()) <= float(d_ref.mean()) + 1e-6

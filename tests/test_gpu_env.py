@@ -8,10 +8,12 @@ from mat_dcml_amd.envs.dcml.vec_env import DeviceDCMLEnv
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("W,fixed,preset", [(32, False, False), (100, False, False), (100, True, False),
-                                            (100, False, True), (4, False, False), (128, False, False)])
-def test_env_kernel_matches_torch(gpu, W, fixed, preset):
-    cfg = DCMLConfig(n_workers=W)
+@pytest.mark.parametrize("W,fixed,preset,shannon", [(32, False, False, False), (100, False, False, False),
+                                                    (100, True, False, False), (100, False, True, False),
+                                                    (4, False, False, False), (128, False, False, False),
+                                                    (32, False, False, True)])
+def test_env_kernel_matches_torch(gpu, W, fixed, preset, shannon):
+    cfg = DCMLConfig(n_workers=W, shannon=shannon)
     E = 64
     hip = DeviceDCMLEnv(E, cfg, device=gpu, seed=7, fixed=fixed, preset=preset, backend="hip")
     ref = DeviceDCMLEnv(E, cfg, device=gpu, seed=7, fixed=fixed, preset=preset, backend="torch")
@@ -19,7 +21,7 @@ def test_env_kernel_matches_torch(gpu, W, fixed, preset):
     o1 = hip.reset()
     o2 = ref.reset()
     for a, b in zip(o1, o2):
-        assert torch.allclose(a, b, atol=1e-6), (a - b).abs().max()
+        assert torch.allclose(a, b, atol=1e-6, rtol=1e-6), (a - b).abs().max()
     g = torch.Generator(device=gpu).manual_seed(0)
     bad = 0
     for step in range(6):
