@@ -84,7 +84,14 @@ class TransformerPolicy:
             g["lr"] = lr
 
     def _fused(self):
-        return (self.kernels != "torch" and self.device.type == "cuda" and mat_fused.supports(self.transformer))
+        return (self.kernels != "torch" and self.device.type == "cuda" and self._is_mat()
+                and mat_fused.supports(self.transformer))
+
+    def _is_mat(self):
+        return isinstance(self.transformer, MultiAgentTransformer)
+
+    def _autocast(self):
+        return torch.autocast("cuda", dtype=self.amp_dtype, enabled=self.amp_dtype is not None)
 
     @torch.no_grad()
     def get_actions(self, cent_obs, obs, available_actions=None, deterministic=False, stride=1, rand=None):
@@ -92,6 +99,10 @@ class TransformerPolicy:
         m = self.transformer
         if self._fused():
             return mat_fused.get_actions(m, obs, available_actions, deterministic, stride, rand)
+        if not self._is_mat():   # variants (models/variants.py): model-level API
+            with self._autocast():
+                a, lp, v = m.get_actions(cent_obs, obs, available_actions, deterministic, stride, rand)
+            return v.float(), a, lp
         with torch.autocast("cuda", dtype=self.amp_dtype, enabled=self.amp_dtype is not None):
             v, rep = m.encoder(cent_obs, obs)
             a, lp = act_mod.autoregressive_act(m, rep, obs, available_actions, deterministic, stride, rand)
@@ -102,6 +113,9 @@ class TransformerPolicy:
         m = self.transformer
         if self._fused():
             return mat_fused.get_values(m, obs)
+        if not self._is_mat():
+            with self._autocast():
+                return m.get_values(cent_obs, obs, available_actions).float()
         with torch.autocast("cuda", dtype=self.amp_dtype, enabled=self.amp_dtype is not None):
             v, _ = m.encoder(cent_obs, obs)
         return v.float()
@@ -111,6 +125,10 @@ class TransformerPolicy:
         m = self.transformer
         if self._fused():
             values, logp, ent = mat_fused.evaluate_actions(m, obs, actions, available_actions)
+        elif not self._is_mat():
+            with self._autocast():
+                logp, values, ent = m(cent_obs, obs, actions, available_actions)
+            values = values.float()
         else:
             with torch.autocast("cuda", dtype=self.amp_dtype, enabled=self.amp_dtype is not None):
                 v, rep = m.encoder(cent_obs, obs)
