@@ -208,6 +208,9 @@ class DCMLRunner:
                                    self.trainer, episode)
 
     # ---------------------------------------------------------------------------------------- eval
+    def decide(self, obs, share, ava, stride):
+        return self.policy.get_actions(None, obs, ava, deterministic=True, stride=stride)[1]
+
     @torch.no_grad()
     def eval(self, total_num_steps=0, stride=None, n_steps=None):
         stride = self.eval_stride if stride is None else stride
@@ -224,7 +227,7 @@ class DCMLRunner:
             if self.device.type == "cuda":
                 torch.cuda.synchronize()
             t0 = time.time()
-            _, actions, _ = self.policy.get_actions(None, obs, ava, deterministic=True, stride=stride)
+            actions = self.decide(obs, share, ava, stride)
             if self.device.type == "cuda":
                 torch.cuda.synchronize()
             times.append(time.time() - t0)
