@@ -116,6 +116,17 @@ _DCML_FLAGS = [
     ("add_center_xy", "true", F, ""),
 ]
 
+# SMAC entry extras (mat_src/mat/scripts/train/train_smac.py:65-78)
+_SMAC_FLAGS = [
+    ("map_name", str, "27m_vs_30m", "SMAC map"), ("eval_map_name", str, None, "SMAC eval map"),
+    ("run_dir", str, "", ""), ("add_move_state", "true", F, ""), ("add_local_obs", "true", F, ""),
+    ("add_distance_state", "true", F, ""), ("add_enemy_action_state", "true", F, ""), ("add_agent_id", "true", F, ""),
+    ("add_visible_state", "true", F, ""), ("add_xy_state", "true", F, ""), ("use_state_agent", "false", T, ""),
+    ("use_mustalive", "false", T, ""), ("add_center_xy", "false", T, ""), ("random_agent_order", "true", F, ""),
+    ("smac_backend", str, "synthetic", "synthetic (on-device SMAC-shaped env) | sc2 (StarCraft II via process pool)"),
+    ("n_env_workers", int, None, "worker processes of the CPU env pool (sc2 backend)"),
+]
+
 # framework (new)
 _FRAMEWORK_FLAGS = [
     ("n_workers", int, 100, "DCML worker count W (agents = W + 1); 4 / 32 / 100 / 128 in the BASELINE configs"),

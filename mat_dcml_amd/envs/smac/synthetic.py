@@ -1,0 +1,210 @@
+"""SMAC-shaped synthetic battle env, vectorised on device (E envs × n_agents) — the cross-env stress config.
+
+StarCraft II is not installable here, so BASELINE config #5 (MAT on SMAC 27m_vs_30m) runs on this stand-in
+("synthetic SMAC-shaped device env"): exactly the reference's tensor contract —
+``obs (E, A, 1288)``, per-agent ``state (E, A, 1458)``, ``available_actions (E, A, 36)``, per-agent dones with
+dead agents inactive, episode limit 180, reward scaled by ``max_reward / 20`` and only positive
+(``StarCraft2_Env.py:90-97,281-283,622-623``), ``won`` / ``battles_won`` / ``battles_game`` /
+``bad_transition`` infos, auto-reset of finished episodes — with cheap kinematics instead of SC2 combat:
+
+* allies move N/S/E/W (actions 2-5) or attack enemy j (action 6+j) within shooting range; dead allies may only
+  take no-op (action 0), exactly the SMAC availability rule;
+* each enemy walks to its nearest living ally and shoots it when in range;
+* damage dealt, +10 per kill and +200 for the win form the (positive) reward.
+
+It reproduces shapes, masking, episode structure and the compute of the MAT/PPO stack on SMAC, NOT SC2 dynamics:
+learning-curve parity for SMAC needs a host with StarCraft II (``envs/smac/adapter.py``).
+"""
+from __future__ import annotations
+
+import torch
+
+from .maps import N_NO_ATTACK, SMACSpec, get_map
+
+MAP_SIZE, SIGHT, SHOOT = 32.0, 9.0, 6.0
+MOVE, ENEMY_MOVE = 1.0, 0.6
+ALLY_DMG, ENEMY_DMG = 0.15, 0.06
+DIRS = ((0.0, 1.0), (0.0, -1.0), (1.0, 0.0), (-1.0, 0.0))
+
+
+class SyntheticSMACEnv:
+    def __init__(self, n_envs: int, map_name: str = "27m_vs_30m", device="cpu", seed: int = 1,
+                 reward_scale_rate: float = 20.0, state_per_agent: bool = True):
+        self.spec: SMACSpec = get_map(map_name)
+        s = self.spec
+        self.E, self.A, self.N = int(n_envs), s.n_agents, s.n_enemies
+        self.n_actions = s.n_actions
+        self.device = torch.device(device)
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(int(seed))
+        self.reward_scale = s.max_reward / reward_scale_rate
+        self.state_per_agent = state_per_agent
+        E, A, N, dev = self.E, self.A, self.N, self.device
+        self.apos = torch.zeros(E, A, 2, device=dev)
+        self.ahp = torch.zeros(E, A, device=dev)
+        self.epos = torch.zeros(E, N, 2, device=dev)
+        self.ehp = torch.zeros(E, N, device=dev)
+        self.t = torch.zeros(E, dtype=torch.long, device=dev)
+        self.last = torch.zeros(E, A, dtype=torch.long, device=dev)
+        self.battles_won = torch.zeros(E, device=dev)
+        self.battles_game = torch.zeros(E, device=dev)
+        idx = torch.arange(A, device=dev)
+        self.others = torch.stack([torch.cat([idx[:i], idx[i + 1:]]) for i in range(A)]) if A > 1 else \
+            torch.zeros(1, 0, dtype=torch.long, device=dev)
+        self.agent_id = torch.eye(A, device=dev)
+
+    # ------------------------------------------------------------------------------------- spaces
+    @property
+    def n_agents(self):
+        return self.A
+
+    @property
+    def observation_space(self):
+        return [[self.spec.obs_dim]] * self.A
+
+    @property
+    def share_observation_space(self):
+        return [[self.spec.state_dim]] * self.A
+
+    @property
+    def action_space(self):
+        return [Discrete(self.n_actions)] * self.A
+
+    # ------------------------------------------------------------------------------------- core
+    def _rand(self, *shape):
+        return torch.rand(*shape, device=self.device, generator=self.gen)
+
+    def _reset_where(self, m):
+        E, A, N = self.E, self.A, self.N
+        ap = torch.stack([8.0 + 3.0 * self._rand(E, A), 16.0 + 6.0 * (self._rand(E, A) - 0.5)], -1)
+        ep = torch.stack([22.0 + 3.0 * self._rand(E, N), 16.0 + 6.0 * (self._rand(E, N) - 0.5)], -1)
+        mm = m.view(E, 1)
+        self.apos = torch.where(mm.unsqueeze(-1), ap, self.apos)
+        self.epos = torch.where(mm.unsqueeze(-1), ep, self.epos)
+        self.ahp = torch.where(mm, torch.ones_like(self.ahp), self.ahp)
+        self.ehp = torch.where(mm, torch.ones_like(self.ehp), self.ehp)
+        self.t = torch.where(m, torch.zeros_like(self.t), self.t)
+        self.last = torch.where(mm, torch.zeros_like(self.last), self.last)
+
+    def reset(self):
+        self._reset_where(torch.ones(self.E, dtype=torch.bool, device=self.device))
+        return self._observe()
+
+    def step(self, actions: torch.Tensor):
+        """actions (E, A[, 1]) ints.  Returns obs, state, reward (E, A, 1), dones (E, A), info dict of (E,)
+        tensors, available actions."""
+        E, A, N = self.E, self.A, self.N
+        a = actions.reshape(E, A).long()
+        alive = self.ahp > 0
+        a = torch.where(alive, a, torch.zeros_like(a))
+        # moves
+        dirs = torch.tensor(DIRS, device=self.device)
+        mv = (a >= 2) & (a < 6)
+        step = dirs[(a - 2).clamp(0, 3)] * MOVE * mv.unsqueeze(-1)
+        self.apos = (self.apos + step).clamp(0.0, MAP_SIZE)
+        # ally attacks
+        d_ae = torch.cdist(self.apos, self.epos)                                   # (E, A, N)
+        tgt = (a - N_NO_ATTACK).clamp(0, N - 1)
+        att = (a >= N_NO_ATTACK) & alive
+        in_rng = torch.gather(d_ae, 2, tgt.unsqueeze(-1)).squeeze(-1) <= SHOOT
+        e_alive = self.ehp > 0
+        hit = att & in_rng & torch.gather(e_alive, 1, tgt)
+        dmg = torch.zeros(E, N, device=self.device).scatter_add_(1, tgt, hit.float() * ALLY_DMG)
+        old_ehp = self.ehp
+        self.ehp = (self.ehp - dmg).clamp(min=0.0)
+        dealt = (old_ehp - self.ehp).sum(1)
+        kills = ((old_ehp > 0) & (self.ehp <= 0)).float().sum(1)
+        # enemy behaviour: nearest living ally, shoot if in range else approach
+        d_ea = d_ae.transpose(1, 2).masked_fill(~alive.unsqueeze(1), float("inf"))   # (E, N, A)
+        dist, near = d_ea.min(-1)
+        e_alive = self.ehp > 0
+        shoot = e_alive & (dist <= SHOOT)
+        walk = e_alive & (dist > SHOOT) & torch.isfinite(dist)
+        tp = torch.gather(self.apos, 1, near.unsqueeze(-1).expand(E, N, 2))
+        vec = tp - self.epos
+        vec = vec / vec.norm(dim=-1, keepdim=True).clamp(min=1e-6)
+        self.epos = self.epos + vec * ENEMY_MOVE * walk.unsqueeze(-1)
+        admg = torch.zeros(E, A, device=self.device).scatter_add_(1, near, shoot.float() * ENEMY_DMG)
+        self.ahp = (self.ahp - admg).clamp(min=0.0)
+        self.last = a
+        self.t += 1
+        won = (self.ehp <= 0).all(1)
+        lost = (self.ahp <= 0).all(1) & ~won
+        timeout = (self.t >= self.spec.limit) & ~won & ~lost
+        done = won | lost | timeout
+        reward = (dealt + 10.0 * kills + 200.0 * won.float()) / self.reward_scale
+        self.battles_game += done.float()
+        self.battles_won += won.float()
+        dones = (self.ahp <= 0) | done.view(E, 1)
+        info = {"won": won, "lost": lost, "bad_transition": timeout, "battles_won": self.battles_won.clone(),
+                "battles_game": self.battles_game.clone(), "dead_allies": (self.ahp <= 0).float().sum(1),
+                "dead_enemies": (self.ehp <= 0).float().sum(1)}
+        self._reset_where(done)      # unconditional: no host sync on done.any()
+        obs, state, ava = self._observe()
+        return obs, state, reward.view(E, 1, 1).expand(E, A, 1), dones, info, ava
+
+    # ------------------------------------------------------------------------------------- features
+    def _observe(self):
+        s, E, A, N = self.spec, self.E, self.A, self.N
+        u, nA = s.unit_type_bits, self.n_actions
+        dev = self.device
+        alive = (self.ahp > 0).float()
+        e_alive = (self.ehp > 0).float()
+        last1h = torch.nn.functional.one_hot(self.last, nA).float()               # (E, A, nA)
+        tb_a = torch.zeros(E, A, u, device=dev)
+        if u:
+            tb_a[..., 0] = 1
+        # moves available: inside the map after the step
+        nxt = self.apos.unsqueeze(2) + torch.tensor(DIRS, device=dev) * MOVE        # (E, A, 4, 2)
+        move = (((nxt >= 0) & (nxt <= MAP_SIZE)).all(-1).float()) * alive.unsqueeze(-1)
+        # enemies
+        rel_e = self.epos.unsqueeze(1) - self.apos.unsqueeze(2)                      # (E, A, N, 2)
+        d_e = rel_e.norm(dim=-1)
+        vis_e = (d_e <= SIGHT).float() * e_alive.unsqueeze(1) * alive.unsqueeze(-1)
+        attackable = (d_e <= SHOOT).float() * vis_e
+        ef = torch.stack([attackable, d_e / SIGHT, rel_e[..., 0] / SIGHT, rel_e[..., 1] / SIGHT,
+                          self.ehp.unsqueeze(1).expand(E, A, N)], -1) * vis_e.unsqueeze(-1)
+        if u:
+            ef = torch.cat([ef, torch.zeros(E, A, N, u, device=dev)], -1)
+        # allies (others)
+        oth = self.others
+        rel_a = self.apos[:, oth] - self.apos.unsqueeze(2)                           # (E, A, A-1, 2)
+        d_a = rel_a.norm(dim=-1)
+        vis_a = (d_a <= SIGHT).float() * alive[:, oth] * alive.unsqueeze(-1)
+        af = torch.cat([torch.stack([vis_a, d_a / SIGHT, rel_a[..., 0] / SIGHT, rel_a[..., 1] / SIGHT,
+                                     self.ahp[:, oth]], -1), tb_a[:, oth], last1h[:, oth]], -1) * vis_a.unsqueeze(-1)
+        own = torch.cat([torch.stack([self.ahp, self.apos[..., 0] / MAP_SIZE, self.apos[..., 1] / MAP_SIZE,
+                                      torch.zeros_like(self.ahp), alive], -1), tb_a, last1h], -1)
+        ids = self.agent_id.expand(E, A, A)
+        obs = torch.cat([move, ef.reshape(E, A, -1), af.reshape(E, A, -1), own, ids], -1)
+        # per-agent state: absolute positions added to every entity
+        esf = torch.cat([torch.stack([attackable, d_e / SIGHT, rel_e[..., 0] / SIGHT, rel_e[..., 1] / SIGHT,
+                                      self.ehp.unsqueeze(1).expand(E, A, N),
+                                      self.epos[..., 0].unsqueeze(1).expand(E, A, N) / MAP_SIZE,
+                                      self.epos[..., 1].unsqueeze(1).expand(E, A, N) / MAP_SIZE,
+                                      e_alive.unsqueeze(1).expand(E, A, N)], -1),
+                         torch.zeros(E, A, N, u, device=dev)], -1)
+        asf = torch.cat([torch.stack([vis_a, d_a / SIGHT, rel_a[..., 0] / SIGHT, rel_a[..., 1] / SIGHT,
+                                      self.ahp[:, oth], self.apos[:, oth][..., 0] / MAP_SIZE,
+                                      self.apos[:, oth][..., 1] / MAP_SIZE, alive[:, oth]], -1),
+                         tb_a[:, oth], last1h[:, oth]], -1)
+        c = self.apos - MAP_SIZE / 2
+        osf = torch.cat([torch.stack([self.ahp, self.apos[..., 0] / MAP_SIZE, self.apos[..., 1] / MAP_SIZE, alive,
+                                      c[..., 0] / MAP_SIZE, c[..., 1] / MAP_SIZE, torch.zeros_like(alive)], -1),
+                         tb_a, last1h], -1)
+        state = torch.cat([move, esf.reshape(E, A, -1), asf.reshape(E, A, -1), osf, ids], -1)
+        # availability (StarCraft2_Env.get_avail_agent_actions): dead → no-op only
+        ava = torch.zeros(E, A, self.n_actions, device=dev)
+        ava[..., 1] = alive
+        ava[..., 2:6] = move
+        ava[..., N_NO_ATTACK:] = attackable
+        ava[..., 0] = 1.0 - alive
+        return obs, state, ava
+
+
+class Discrete:
+    """Minimal ``gym.spaces.Discrete`` stand-in (gym is not a dependency); policies dispatch on the class name."""
+
+    def __init__(self, n):
+        self.n = n
+        self.shape = ()
