@@ -59,6 +59,30 @@ class MATTrainer:
             if self._use_valuenorm else None
         self.generator = None
         self.params = [p for p in policy.transformer.parameters() if p.requires_grad]
+        self.fused = self._setup_fused(args)
+
+    def _setup_fused(self, args):
+        """Fused minibatch step on GPU: fused fwd kernels → fused PPO loss/grad kernel → fused bwd kernels →
+        fused clip+Adam over the flat parameter buffer (no autograd graph, ~15 launches per minibatch)."""
+        pol = self.policy
+        flat = self.comm._flat if self.comm is not None else None
+        if flat is None or getattr(pol, "n_objective", 1) != 1 or not pol._fused():
+            return False
+        from ..ops import mat_train, ppo_fused
+        m = pol.transformer
+        if not mat_train.supported(m):
+            return False
+        fp = ppo_fused.flat_params_of(m)
+        if fp is None or fp.numel() != flat.buf.numel():
+            return False
+        for p in self.params:   # grads and params must share one layout
+            if p.grad is None or (p.grad.data_ptr() - flat.buf.data_ptr()) != (p.data_ptr() - fp.data_ptr()):
+                return False
+        self.loss_fused = ppo_fused.PPOLossFused(self, self.device)
+        pol.optimizer = ppo_fused.FlatAdam(fp, flat.buf, lr=pol.optimizer.param_groups[0]["lr"], eps=args.opti_eps,
+                                           weight_decay=args.weight_decay,
+                                           max_grad_norm=args.max_grad_norm if self._use_max_grad_norm else None)
+        return True
 
     # ------------------------------------------------------------------------------------------------
     def cal_value_loss(self, values, value_preds_batch, return_batch, active_masks_batch):
@@ -114,6 +138,25 @@ class MATTrainer:
         mat_fused.bump_version(pol.transformer)
         return value_loss.detach(), grad_norm.detach(), policy_loss.detach(), entropy.detach(), imp.detach().mean()
 
+    def ppo_update_fused(self, mb):
+        from ..ops import mat_train
+        pol = self.policy
+        m = pol.transformer
+        enc, dec, _ = mat_train._state(m, mb["obs"].device)
+        v, rep = enc.forward(mb["obs"], save=True)
+        logp, ent = dec.forward(rep, mb["actions"], mb["ava"], save=True)
+        self.comm._flat.buf.zero_()
+        dv, dlp, dent = self.loss_fused.run(v, logp, ent, mb, self.comm)
+        drep = dec.backward(dlp, dent)
+        enc.backward(drep, dv)
+        dec.ctx = None
+        enc.ctx = None
+        if self.comm.world_size > 1:
+            self.comm.all_reduce_grads_(self.params)
+        pol.optimizer.step()
+        mat_fused.bump_version(m)
+        return pol.optimizer.grad_norm
+
     # ------------------------------------------------------------------------------------------------
     def _advantages(self, buffer):
         adv = buffer.advantages
@@ -127,6 +170,8 @@ class MATTrainer:
         pol = self.policy
         keys = ["value_loss", "policy_loss", "dist_entropy", "actor_grad_norm", "critic_grad_norm", "ratio"]
         acc = torch.zeros(len(keys), device=self.device)
+        if self.fused:
+            self.loss_fused.out.zero_()
         T, E = buffer.T, buffer.E
         obs_f = buffer.flat("obs")
         act_f = buffer.flat("actions")
@@ -144,8 +189,14 @@ class MATTrainer:
             for idx in buffer.minibatch_indices(self.num_mini_batch, self.generator):
                 mb = {"obs": obs_f[idx], "actions": act_f[idx], "ava": ava_f[idx], "old_logp": lp_f[idx],
                       "value_preds": vp_f[idx], "returns": ret_f[idx], "active": am_f[idx], "adv": adv_f[idx]}
+                if self.fused:
+                    acc[3:5] += self.ppo_update_fused(mb)
+                    continue
                 vl, gn, pl, ent, ratio = self.ppo_update(mb)
                 acc += torch.stack([vl, pl, ent, gn, gn, ratio]).float()
+        if self.fused:   # loss scalars accumulated on device by the loss kernel: [policy, value, entropy, ratio]
+            o = self.loss_fused.out
+            acc[0], acc[1], acc[2], acc[5] = o[1], o[0], o[2], o[3]
         acc /= self.ppo_epoch * self.num_mini_batch
         return dict(zip(keys, acc))
 

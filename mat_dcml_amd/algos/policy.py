@@ -72,6 +72,9 @@ class TransformerPolicy:
                                              num_agents, args, self.device, self.action_type, semi_index)
         if getattr(args, "env_name", "") == "hands":
             self.transformer.zero_std()
+        # all parameters in one flat fp32 buffer (fused Adam / flat grads / one all-reduce)
+        from ..ops.ppo_fused import flatten_params
+        flatten_params(self.transformer)
         self.optimizer = torch.optim.Adam(self.transformer.parameters(), lr=self.lr, eps=self.opti_eps,
                                           weight_decay=self.weight_decay)
         self.kernels = getattr(args, "kernels", "auto")

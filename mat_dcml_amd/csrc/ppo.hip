@@ -1,0 +1,248 @@
+// Fused MAT-PPO loss (forward value + analytic gradients) and fused flat clip+Adam for gfx950.
+//
+// Loss = policy clip loss - entropy_coef * entropy + value_loss_coef * value loss, exactly as
+// mat_trainer.py:54-156 (reference): importance weight exp(logp - old), clipped surrogate min, active-masked or
+// plain means, ValueNorm-normalised returns (update with the minibatch first, beta = 0.99999, debiased, var
+// clamped at 1e-2), clipped value prediction, Huber(delta) or MSE, max(orig, clipped).  Instead of ~80 autograd
+// kernels the trainer runs:
+//   ppo_reduce    — per-minibatch sums (returns, returns^2 per objective, active count), block partials + atomics
+//   ppo_vn_update — ValueNorm running-moment update from those sums (one wave)
+//   ppo_grad      — per-token loss terms and d(loss)/d(logp, entropy, value); loss scalars accumulated by atomics
+// and feeds the gradients straight into the fused decoder/encoder backward kernels.
+//   adam_norm / adam_step — global grad-norm (clip_grad_norm_ semantics: scale = min(1, max/(norm+1e-6)))
+//   and one Adam update over the flat fp32 parameter / gradient / moment buffers (torch.optim.Adam maths,
+//   L2 weight decay added to the gradient).
+#include "common.h"
+
+using namespace mdl;
+
+struct PPOArgs {
+  int n;            // tokens in the minibatch (sequences x agents)
+  int n_obj;        // value objectives (1 or 2)
+  const float* v;   // (n, n_obj)
+  const float* logp;      // (n)
+  const float* ent;       // (n)
+  const float* old_logp;  // (n)
+  const float* adv;       // (n)  (already normalised)
+  const float* vpred;     // (n, n_obj) old value predictions
+  const float* ret;       // (n, n_obj) returns
+  const float* active;    // (n)
+  float* dv; float* dlogp; float* dent;
+  float* stats;     // [0..n_obj) sum ret, [n_obj..2n_obj) sum ret^2, [2n_obj] count, [2n_obj+1] sum active
+                    // (DP all-reduces the first 2n_obj+1: ValueNorm sees the global batch, losses stay local means)
+  float* out;       // accumulators: policy loss, value loss, entropy, ratio (added to, never cleared here)
+  float* vn;        // ValueNorm: running_mean[n_obj], running_mean_sq[n_obj], debiasing_term
+  float clip, coef_v, coef_e, huber_delta, beta, eps, omb;   // omb = 1 - beta computed in double on the host
+  int use_huber, use_clip_v, use_vam, use_pam, use_vn, update_vn;
+};
+
+#define MAXOBJ 2
+
+__global__ __launch_bounds__(256) void ppo_reduce_kernel(PPOArgs a) {
+  __shared__ float sm[4][2 * MAXOBJ + 2];
+  float acc[2 * MAXOBJ + 2];
+  const int K = 2 * a.n_obj + 2;
+#pragma unroll
+  for (int k = 0; k < 2 * MAXOBJ + 2; ++k) acc[k] = 0.f;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
+    for (int o = 0; o < a.n_obj; ++o) {
+      const float r = a.ret[(size_t)i * a.n_obj + o];
+      acc[o] += r;
+      acc[a.n_obj + o] += r * r;
+    }
+    acc[2 * a.n_obj] += 1.f;
+    acc[2 * a.n_obj + 1] += a.active[i];
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int k = 0; k < K; ++k) {
+    const float s = wave_sum(acc[k]);
+    if (lane == 0) sm[wid][k] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < K) {
+    float s = 0.f;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += sm[w][threadIdx.x];
+    atomicAdd(a.stats + threadIdx.x, s);
+  }
+}
+
+__global__ void ppo_vn_update_kernel(PPOArgs a) {
+  // reference ValueNorm.update (per_element_update False): w = beta for every minibatch
+  const int o = threadIdx.x;
+  const float cnt = a.stats[2 * a.n_obj];
+  const float w = a.beta, omw = a.omb;   // 1 - 0.99999 rounded in fp32 is 0.13% off: take it from the host
+  if (o < a.n_obj) {
+    const float m = a.stats[o] / cnt, sq = a.stats[a.n_obj + o] / cnt;
+    a.vn[o] = a.vn[o] * w + m * omw;
+    a.vn[a.n_obj + o] = a.vn[a.n_obj + o] * w + sq * omw;
+  }
+  __syncthreads();
+  if (o == 0) a.vn[2 * a.n_obj] = a.vn[2 * a.n_obj] * w + omw;
+}
+
+__device__ __forceinline__ float huber_grad(float e, float d) { return fabsf(e) <= d ? e : (e > 0.f ? d : -d); }
+__device__ __forceinline__ float huber(float e, float d) {
+  const float ae = fabsf(e);
+  return ae <= d ? 0.5f * e * e : d * (ae - 0.5f * d);
+}
+
+__global__ __launch_bounds__(256) void ppo_grad_kernel(PPOArgs a) {
+  __shared__ float sm[4][4];
+  const float sum_a = a.stats[2 * a.n_obj + 1], n = (float)a.n;
+  const float inv_pa = a.use_pam ? 1.f / fmaxf(sum_a, 1.f) : 1.f / n;
+  const float inv_va = (a.use_vam ? 1.f / fmaxf(sum_a, 1.f) : 1.f / n) / (float)a.n_obj;
+  float mean[MAXOBJ], istd[MAXOBJ];
+  {
+    const float d = fmaxf(a.vn[2 * a.n_obj], a.eps);
+    for (int o = 0; o < a.n_obj; ++o) {
+      const float m = a.vn[o] / d;
+      const float var = fmaxf(a.vn[a.n_obj + o] / d - m * m, 1e-2f);
+      mean[o] = a.use_vn ? m : 0.f;
+      istd[o] = a.use_vn ? rsqrtf(var) : 1.f;
+    }
+  }
+  float pl = 0.f, vl = 0.f, el = 0.f, rl = 0.f;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
+    const float act = a.active[i];
+    // policy: -min(r A, clip(r) A)
+    const float imp = __expf(a.logp[i] - a.old_logp[i]);
+    const float ad = a.adv[i];
+    const float s1 = imp * ad;
+    const float ic = fminf(fmaxf(imp, 1.f - a.clip), 1.f + a.clip);
+    const float s2 = ic * ad;
+    const float wp = a.use_pam ? act * inv_pa : inv_pa;
+    float dm;
+    if (s1 <= s2) dm = imp * ad;
+    else dm = (imp >= 1.f - a.clip && imp <= 1.f + a.clip) ? imp * ad : 0.f;  // clamp passes grad inclusively
+    pl -= fminf(s1, s2) * wp;
+    a.dlogp[i] = -wp * dm;
+    // entropy bonus
+    a.dent[i] = -a.coef_e * wp;
+    el += a.ent[i] * wp;
+    rl += imp;
+    // value
+    const float wv = a.use_vam ? act * inv_va : inv_va;
+    for (int o = 0; o < a.n_obj; ++o) {
+      const size_t j = (size_t)i * a.n_obj + o;
+      const float v = a.v[j], vp = a.vpred[j];
+      const float dvc = v - vp;
+      const float vc = vp + fminf(fmaxf(dvc, -a.clip), a.clip);
+      const float tgt = (a.ret[j] - mean[o]) * istd[o];
+      const float eo = tgt - v, ec = tgt - vc;
+      const float lo = a.use_huber ? huber(eo, a.huber_delta) : 0.5f * eo * eo;
+      const float lc = a.use_huber ? huber(ec, a.huber_delta) : 0.5f * ec * ec;
+      const float go = -(a.use_huber ? huber_grad(eo, a.huber_delta) : eo);
+      const float gc = -(a.use_huber ? huber_grad(ec, a.huber_delta) : ec) * ((dvc >= -a.clip && dvc <= a.clip) ? 1.f : 0.f);
+      float l, g;
+      if (a.use_clip_v) {
+        if (lo >= lc) { l = lo; g = go; } else { l = lc; g = gc; }
+      } else { l = lo; g = go; }
+      vl += l * wv;
+      a.dv[j] = a.coef_v * wv * g;
+    }
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float r4[4] = {pl, vl, el, rl / n};
+  for (int k = 0; k < 4; ++k) {
+    const float s = wave_sum(r4[k]);
+    if (lane == 0) sm[wid][k] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    float s = 0.f;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += sm[w][threadIdx.x];
+    atomicAdd(a.out + threadIdx.x, s);
+  }
+}
+
+static int ppo_grid(int n) {
+  int g = (n + 255) / 256;
+  return g > 1024 ? 1024 : (g < 1 ? 1 : g);
+}
+
+MDL_API int mdl_ppo_loss(const PPOArgs* a, hipStream_t st) {
+  if (a->n_obj < 1 || a->n_obj > MAXOBJ) return -1;
+  hipMemsetAsync(a->stats, 0, sizeof(float) * (2 * a->n_obj + 2), st);
+  hipLaunchKernelGGL(ppo_reduce_kernel, dim3(ppo_grid(a->n)), dim3(256), 0, st, *a);
+  MDL_CHECK_LAUNCH();
+  if (a->update_vn) {
+    hipLaunchKernelGGL(ppo_vn_update_kernel, dim3(1), dim3(64), 0, st, *a);
+    MDL_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(ppo_grad_kernel, dim3(ppo_grid(a->n)), dim3(256), 0, st, *a);
+  MDL_CHECK_LAUNCH();
+  return 0;
+}
+
+// the reduce half alone (DP: all-reduce the sums between reduce and update)
+MDL_API int mdl_ppo_reduce(const PPOArgs* a, hipStream_t st) {
+  hipMemsetAsync(a->stats, 0, sizeof(float) * (2 * a->n_obj + 2), st);
+  hipLaunchKernelGGL(ppo_reduce_kernel, dim3(ppo_grid(a->n)), dim3(256), 0, st, *a);
+  MDL_CHECK_LAUNCH();
+  return 0;
+}
+
+MDL_API int mdl_ppo_finish(const PPOArgs* a, hipStream_t st) {
+  if (a->update_vn) {
+    hipLaunchKernelGGL(ppo_vn_update_kernel, dim3(1), dim3(64), 0, st, *a);
+    MDL_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(ppo_grad_kernel, dim3(ppo_grid(a->n)), dim3(256), 0, st, *a);
+  MDL_CHECK_LAUNCH();
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------- flat Adam
+struct AdamArgs {
+  int n;
+  float* p; const float* g; float* m; float* v;
+  float* sumsq;       // [0] = sum of squared grads (filled by adam_norm), [1] = grad norm written for logging
+  float lr, beta1, beta2, eps, wd, bc1, bc2, max_norm;
+  int clip;
+};
+
+__global__ __launch_bounds__(256) void adam_norm_kernel(AdamArgs a) {
+  __shared__ float sm[4];
+  float s = 0.f;
+  const int n4 = a.n >> 2;
+  const float4* g4 = reinterpret_cast<const float4*>(a.g);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+    const float4 x = g4[i];
+    s += x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
+  }
+  for (int i = (n4 << 2) + blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x)
+    s += a.g[i] * a.g[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(a.sumsq, sm[0] + sm[1] + sm[2] + sm[3]);
+}
+
+__global__ __launch_bounds__(256) void adam_step_kernel(AdamArgs a) {
+  const float norm = sqrtf(a.sumsq[0]);
+  const float scale = a.clip ? fminf(1.f, a.max_norm / (norm + 1e-6f)) : 1.f;
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.sumsq[1] = norm;
+  const float ib1 = 1.f / a.bc1, ib2 = 1.f / a.bc2;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
+    float g = a.g[i] * scale;
+    float p = a.p[i];
+    if (a.wd != 0.f) g += a.wd * p;
+    const float m = a.m[i] * a.beta1 + (1.f - a.beta1) * g;
+    const float v = a.v[i] * a.beta2 + (1.f - a.beta2) * g * g;
+    a.m[i] = m;
+    a.v[i] = v;
+    p -= a.lr * (m * ib1) / (sqrtf(v * ib2) + a.eps);
+    a.p[i] = p;
+  }
+}
+
+MDL_API int mdl_adam(const AdamArgs* a, hipStream_t st) {
+  int g = (a->n + 255) / 256;
+  if (g > 1024) g = 1024;
+  hipMemsetAsync(a->sumsq, 0, sizeof(float), st);
+  hipLaunchKernelGGL(adam_norm_kernel, dim3(g), dim3(256), 0, st, *a);
+  MDL_CHECK_LAUNCH();
+  hipLaunchKernelGGL(adam_step_kernel, dim3(g), dim3(256), 0, st, *a);
+  MDL_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,181 @@
+"""Fused PPO loss/gradients and flat clip+Adam (``csrc/ppo.hip``) + flat parameter storage.
+
+* ``flatten_params(module)``: every parameter becomes a view of ONE contiguous fp32 buffer (same order as
+  ``FlatGrads`` in ``parallel/comm.py``), so the optimizer is a single elementwise kernel over 151k floats
+  and the gradient all-reduce / norm / clip see one buffer.
+* ``FlatAdam``: ``torch.optim.Adam`` semantics (bias-corrected moments, eps outside the sqrt, L2 weight decay)
+  fused with ``clip_grad_norm_`` (scale = min(1, max_norm / (‖g‖ + 1e-6))) — 1 memset + 2 kernels instead of the
+  ~25 launches of foreach-Adam + clip.  ``param_groups`` / ``state_dict`` keep the optimizer-facing surface
+  (``lr_decay``, checkpoints).
+* ``ppo_loss``: the MAT-PPO objective's value and analytic gradients w.r.t. (values, log-probs, entropies) in
+  3 kernels, including the ValueNorm update (reference ``mat_trainer.py:54-156``); its outputs feed the fused
+  decoder / encoder backward kernels directly (``ops/mat_train.py``).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import kernels
+from .kernels import P, _stream, check, lib, sig
+
+vp = ctypes.c_void_p
+
+
+class PPOArgs(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int), ("n_obj", ctypes.c_int)] + \
+               [(k, vp) for k in ("v", "logp", "ent", "old_logp", "adv", "vpred", "ret", "active", "dv", "dlogp",
+                                  "dent", "stats", "out", "vn")] + \
+               [(k, ctypes.c_float) for k in ("clip", "coef_v", "coef_e", "huber_delta", "beta", "eps", "omb")] + \
+               [(k, ctypes.c_int) for k in ("use_huber", "use_clip_v", "use_vam", "use_pam", "use_vn", "update_vn")]
+
+
+class AdamArgs(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int)] + [(k, vp) for k in ("p", "g", "m", "v", "sumsq")] + \
+               [(k, ctypes.c_float) for k in ("lr", "beta1", "beta2", "eps", "wd", "bc1", "bc2", "max_norm")] + \
+               [("clip", ctypes.c_int)]
+
+
+sig("mdl_ppo_loss", ctypes.POINTER(PPOArgs), vp)
+sig("mdl_ppo_reduce", ctypes.POINTER(PPOArgs), vp)
+sig("mdl_ppo_finish", ctypes.POINTER(PPOArgs), vp)
+sig("mdl_adam", ctypes.POINTER(AdamArgs), vp)
+
+
+def flatten_params(module: torch.nn.Module) -> torch.Tensor:
+    params = [p for p in module.parameters() if p.requires_grad]
+    n = sum(p.numel() for p in params)
+    dev = params[0].device
+    flat = torch.empty(n, dtype=torch.float32, device=dev)
+    off = 0
+    for p in params:
+        k = p.numel()
+        flat[off:off + k].copy_(p.data.reshape(-1).float())
+        p.data = flat[off:off + k].view_as(p)
+        off += k
+    module._mdl_flat_params = flat
+    return flat
+
+
+def flat_params_of(module):
+    flat = getattr(module, "_mdl_flat_params", None)
+    if flat is None:
+        return None
+    params = [p for p in module.parameters() if p.requires_grad]
+    off = 0
+    for p in params:   # views still in place (load_state_dict copies into them)
+        if p.data_ptr() != flat[off:].data_ptr():
+            return None
+        off += p.numel()
+    return flat
+
+
+class FlatAdam:
+    def __init__(self, flat_params: torch.Tensor, flat_grads: torch.Tensor, lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
+                 weight_decay=0.0, max_grad_norm=None):
+        self.p, self.g = flat_params, flat_grads
+        self.m = torch.zeros_like(flat_params)
+        self.v = torch.zeros_like(flat_params)
+        self.scratch = torch.zeros(2, dtype=torch.float32, device=flat_params.device)   # sumsq, norm
+        self.param_groups = [{"lr": lr, "betas": betas, "eps": eps, "weight_decay": weight_decay}]
+        self.max_grad_norm = max_grad_norm
+        self.t = 0
+
+    @property
+    def grad_norm(self):
+        return self.scratch[1]
+
+    def zero_grad(self, set_to_none=False):
+        self.g.zero_()
+
+    def step(self):
+        g = self.param_groups[0]
+        self.t += 1
+        b1, b2 = g["betas"]
+        a = AdamArgs(n=self.p.numel(), p=P(self.p), g=P(self.g), m=P(self.m), v=P(self.v), sumsq=P(self.scratch),
+                     lr=g["lr"], beta1=b1, beta2=b2, eps=g["eps"], wd=g["weight_decay"], bc1=1 - b1 ** self.t,
+                     bc2=1 - b2 ** self.t, max_norm=float(self.max_grad_norm or 0.0),
+                     clip=int(self.max_grad_norm is not None))
+        check(lib().mdl_adam(ctypes.byref(a), _stream()), "adam")
+
+    def state_dict(self):
+        return {"m": self.m, "v": self.v, "t": self.t, "param_groups": self.param_groups}
+
+    def load_state_dict(self, sd):
+        if "m" not in sd:   # a torch.optim.Adam state (per-parameter exp_avg / exp_avg_sq)
+            st = sd.get("state", {})
+            if st:
+                self.m.copy_(torch.cat([st[i]["exp_avg"].reshape(-1) for i in sorted(st)]))
+                self.v.copy_(torch.cat([st[i]["exp_avg_sq"].reshape(-1) for i in sorted(st)]))
+                self.t = int(float(st[min(st)]["step"]))
+            self.param_groups[0]["lr"] = sd["param_groups"][0]["lr"]
+            return
+        self.m.copy_(sd["m"])
+        self.v.copy_(sd["v"])
+        self.t = int(sd["t"])
+        self.param_groups[0].update({k: v for k, v in sd["param_groups"][0].items() if k != "params"})
+
+
+class PPOLossFused:
+    """Holds the per-trainer device scratch; ``run`` launches the fused loss for one minibatch."""
+
+    def __init__(self, trainer, device):
+        self.tr = trainer
+        self.stats = torch.zeros(8, dtype=torch.float32, device=device)
+        self.out = torch.zeros(4, dtype=torch.float32, device=device)
+        self._vn = None
+        self._g = None
+
+    def _vn_buffer(self, n_obj, device):
+        """ValueNorm moments as views of one flat buffer the kernels update in place (bound once)."""
+        vnm = self.tr.value_normalizer
+        if vnm is None:
+            if self._vn is None:
+                self._vn = torch.zeros(2 * n_obj + 1, dtype=torch.float32, device=device)
+            return self._vn
+        flat = getattr(vnm, "_mdl_flat", None)
+        if flat is None or vnm.running_mean.data_ptr() != flat.data_ptr():
+            flat = torch.cat([vnm.running_mean.reshape(-1), vnm.running_mean_sq.reshape(-1),
+                              vnm.debiasing_term.reshape(-1)]).float().contiguous()
+            shp_m, shp_d = vnm.running_mean.shape, vnm.debiasing_term.shape
+            vnm.running_mean = flat[:n_obj].view(shp_m)
+            vnm.running_mean_sq = flat[n_obj:2 * n_obj].view(shp_m)
+            vnm.debiasing_term = flat[2 * n_obj].view(shp_d)
+            vnm._mdl_flat = flat
+        return flat
+
+    def run(self, values, logp, ent, mb, comm=None):
+        """values (N, n_obj), logp / ent (N, 1) fp32 contiguous → (dv, dlogp, dent).  Losses accumulate into
+        ``self.out`` = [policy, value, entropy, ratio] (caller zeroes it per log window)."""
+        tr = self.tr
+        n_obj = values.shape[-1]
+        N = logp.numel()
+        dev = values.device
+        if self._g is None or self._g[0].shape != values.shape or self._g[1].numel() != N:
+            self._g = (torch.empty_like(values), torch.empty_like(logp), torch.empty_like(ent))
+        dv, dlp, dent = self._g
+        vnm = tr.value_normalizer
+        vn = self._vn_buffer(n_obj, dev)
+        ts = [t.reshape(-1).contiguous() if t.is_contiguous() else t.contiguous() for t in
+              (mb["old_logp"], mb["adv"], mb["value_preds"], mb["returns"], mb["active"])]
+        a = PPOArgs(n=N, n_obj=n_obj, v=P(values), logp=P(logp), ent=P(ent), old_logp=P(ts[0]), adv=P(ts[1]),
+                    vpred=P(ts[2]), ret=P(ts[3]), active=P(ts[4]), dv=P(dv), dlogp=P(dlp), dent=P(dent),
+                    stats=P(self.stats), out=P(self.out), vn=P(vn), clip=tr.clip_param, coef_v=tr.value_loss_coef,
+                    coef_e=tr.entropy_coef, huber_delta=tr.huber_delta, beta=vnm.beta if vnm is not None else 1.0,
+                    eps=vnm.epsilon if vnm is not None else 1e-5,
+                    omb=(1.0 - vnm.beta) if vnm is not None else 0.0, use_huber=int(tr._use_huber_loss),
+                    use_clip_v=int(tr._use_clipped_value_loss), use_vam=int(tr._use_value_active_masks),
+                    use_pam=int(tr._use_policy_active_masks), use_vn=int(vnm is not None),
+                    update_vn=int(vnm is not None))
+        if comm is not None and comm.world_size > 1 and vnm is not None:
+            check(lib().mdl_ppo_reduce(ctypes.byref(a), _stream()), "ppo_reduce")
+            comm.all_reduce_sum_(self.stats[: 2 * n_obj + 1])
+            check(lib().mdl_ppo_finish(ctypes.byref(a), _stream()), "ppo_finish")
+        else:
+            check(lib().mdl_ppo_loss(ctypes.byref(a), _stream()), "ppo_loss")
+        return dv, dlp, dent
+
+
+def available():
+    return kernels.available()
