@@ -75,7 +75,11 @@ def main(args):
     else:
         from mat_dcml_amd.runner.baseline_runner import BaselineRunner
         runner = BaselineRunner(config)
+    if all_args.resume:
+        runner.resume()
     runner.run()
+    if runner.heartbeat is not None:
+        runner.heartbeat.stop()
     if comm.is_main:
         runner.writter.export_scalars_to_json(os.path.join(runner.log_dir, "summary.json"))
         runner.writter.close()

@@ -59,6 +59,8 @@ class MATTrainer:
             if self._use_valuenorm else None
         self.generator = None
         self.params = [p for p in policy.transformer.parameters() if p.requires_grad]
+        self.poison = False          # fault injection: non-finite gradients this iteration
+        self.skipped = torch.zeros((), device=self.device)
         self.fused = self._setup_fused(args)
 
     def _setup_fused(self, args):
@@ -124,6 +126,9 @@ class MATTrainer:
         else:
             pol.optimizer.zero_grad(set_to_none=False)
         loss.backward()
+        if self.poison:
+            for p in self.params:
+                p.grad.fill_(float("nan"))
         if self.comm is not None and self.comm.world_size > 1:
             self.comm.all_reduce_grads_(self.params)
         if flat is not None:
@@ -134,7 +139,10 @@ class MATTrainer:
             grad_norm = nn.utils.clip_grad_norm_(self.params, self.max_grad_norm, foreach=True)
         else:
             grad_norm = torch.norm(torch.stack([p.grad.norm() for p in self.params if p.grad is not None]))
-        pol.optimizer.step()
+        if bool(torch.isfinite(grad_norm)):     # non-finite guard (torch path: one host sync per step)
+            pol.optimizer.step()
+        else:
+            self.skipped += 1
         mat_fused.bump_version(pol.transformer)
         return value_loss.detach(), grad_norm.detach(), policy_loss.detach(), entropy.detach(), imp.detach().mean()
 
@@ -151,6 +159,8 @@ class MATTrainer:
         enc.backward(drep, dv)
         dec.ctx = None
         enc.ctx = None
+        if self.poison:
+            self.comm._flat.buf[:1].fill_(float("nan"))   # the fused Adam kernel skips non-finite steps
         if self.comm.world_size > 1:
             self.comm.all_reduce_grads_(self.params)
         pol.optimizer.step()

@@ -196,7 +196,7 @@ MDL_API int mdl_ppo_finish(const PPOArgs* a, hipStream_t st) {
 struct AdamArgs {
   int n;
   float* p; const float* g; float* m; float* v;
-  float* sumsq;       // [0] = sum of squared grads (filled by adam_norm), [1] = grad norm written for logging
+  float* sumsq;       // [0] sum of squared grads (adam_norm), [1] grad norm (logging), [2] skipped steps
   float lr, beta1, beta2, eps, wd, bc1, bc2, max_norm;
   int clip;
 };
@@ -220,8 +220,12 @@ __global__ __launch_bounds__(256) void adam_norm_kernel(AdamArgs a) {
 
 __global__ __launch_bounds__(256) void adam_step_kernel(AdamArgs a) {
   const float norm = sqrtf(a.sumsq[0]);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    a.sumsq[1] = norm;
+    if (!isfinite(norm)) a.sumsq[2] += 1.f;   // skipped-step counter
+  }
+  if (!isfinite(norm)) return;   // non-finite guard: skip the whole step (params and moments untouched)
   const float scale = a.clip ? fminf(1.f, a.max_norm / (norm + 1e-6f)) : 1.f;
-  if (blockIdx.x == 0 && threadIdx.x == 0) a.sumsq[1] = norm;
   const float ib1 = 1.f / a.bc1, ib2 = 1.f / a.bc2;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
     float g = a.g[i] * scale;

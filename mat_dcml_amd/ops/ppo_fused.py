@@ -77,7 +77,7 @@ class FlatAdam:
         self.p, self.g = flat_params, flat_grads
         self.m = torch.zeros_like(flat_params)
         self.v = torch.zeros_like(flat_params)
-        self.scratch = torch.zeros(2, dtype=torch.float32, device=flat_params.device)   # sumsq, norm
+        self.scratch = torch.zeros(3, dtype=torch.float32, device=flat_params.device)   # sumsq, norm, skipped
         self.param_groups = [{"lr": lr, "betas": betas, "eps": eps, "weight_decay": weight_decay}]
         self.max_grad_norm = max_grad_norm
         self.t = 0
@@ -85,6 +85,10 @@ class FlatAdam:
     @property
     def grad_norm(self):
         return self.scratch[1]
+
+    @property
+    def skipped_steps(self):
+        return self.scratch[2]
 
     def zero_grad(self, set_to_none=False):
         self.g.zero_()

@@ -31,11 +31,16 @@ from ..envs.dcml.config import DCMLConfig
 from ..envs.dcml.spaces import dcml_action_spaces
 from ..envs.dcml.vec_env import DeviceDCMLEnv
 from ..parallel.comm import Comm
+from ..parallel.resilience import FaultInjector, Heartbeat
 from ..utils.logger import ScalarWriter
 from ..utils.timers import PhaseTimers
 
 
 class DCMLRunner:
+    _resumed = False
+    faults = FaultInjector(None)
+    heartbeat = None
+
     def __init__(self, config):
         a = config["all_args"]
         self.all_args = a
@@ -55,6 +60,11 @@ class DCMLRunner:
         self.dcml = config.get("dcml_cfg") or DCMLConfig(n_workers=getattr(a, "n_workers", 100),
                                                          shannon=bool(getattr(a, "shannon", False)))
         rank = self.comm.rank
+        self.faults = FaultInjector(getattr(a, "fault_inject", None), rank)
+        if self.faults.disable_frac is not None:
+            self.dcml.disable_frac = self.faults.disable_frac
+        self.heartbeat = Heartbeat(self.comm, getattr(a, "heartbeat_s", 0.0) or 0.0)
+        self._resumed = False
         E = self.n_rollout_threads
         self.envs = config.get("envs") or DeviceDCMLEnv(E, self.dcml, self.device, seed=a.seed,
                                                         env_id_offset=rank * E,
@@ -93,7 +103,10 @@ class DCMLRunner:
 
     # ---------------------------------------------------------------------------------------- rollout
     def warmup(self):
-        obs, share, ava = self.envs.reset()
+        if self._resumed:   # env restored from its checkpointed counters: continue from its current task
+            obs, share, ava = self.envs.obs, self.envs.share_view(), self.envs.ava
+        else:
+            obs, share, ava = self.envs.reset()
         self.buffer.obs[0].copy_(obs)
         self.buffer.share_obs[0].copy_(share[:, 0])
         self.buffer.available_actions[0].copy_(ava)
@@ -162,6 +175,8 @@ class DCMLRunner:
         for episode in range(self.start_episode, episodes):
             if self.use_linear_lr_decay:
                 self.policy.lr_decay(episode, episodes)
+            self.faults.maybe_kill(episode)
+            self.trainer.poison = self.faults.poison_grads(episode)
             infos = self.train_iteration()
             total = (episode + 1) * self.episode_length * self.n_rollout_threads * self.comm.world_size
             if episode % self.save_interval == 0 or episode == episodes - 1:
@@ -200,12 +215,33 @@ class DCMLRunner:
 
     def save(self, episode):
         self.comm.barrier()
-        if self.comm.is_main and self.save_dir:
+        if not self.save_dir:
+            return
+        if getattr(self.all_args, "save_trainer_state", True) and hasattr(self.envs, "task_ctr"):   # per-rank env counters
+            from ..utils.checkpoint import save_env_state
+            save_env_state(self.save_dir, episode, self.comm.rank, self.envs)
+        if self.comm.is_main:
             self.policy.save(self.save_dir, episode)
             if getattr(self.all_args, "save_trainer_state", True):
                 from ..utils.checkpoint import save_trainer_state
                 save_trainer_state(os.path.join(self.save_dir, f"trainer_state_{episode}.pt"), self.policy,
                                    self.trainer, episode)
+        self.comm.barrier()
+
+    def resume(self, models_dir=None):
+        """Restore the latest complete checkpoint (weights + Adam + ValueNorm + episode + env counters)."""
+        from ..utils.checkpoint import latest_checkpoint, load_env_state, load_trainer_state
+        models_dir = models_dir or self.save_dir
+        ep = latest_checkpoint(models_dir) if models_dir else None
+        if ep is None:
+            return None
+        self.policy.restore(os.path.join(models_dir, f"transformer_{ep}.pt"))
+        load_trainer_state(os.path.join(models_dir, f"trainer_state_{ep}.pt"), self.policy, self.trainer)
+        self._resumed = load_env_state(models_dir, ep, self.comm.rank, self.envs)
+        self.start_episode = ep + 1
+        if self.comm.is_main:
+            print(f"[resume] restored episode {ep} from {models_dir}")
+        return ep
 
     # ---------------------------------------------------------------------------------------- eval
     def decide(self, obs, share, ava, stride):

@@ -35,12 +35,46 @@ def load_transformer(model, path):
 
 
 def save_trainer_state(path, policy, trainer, episode, extra=None):
-    state = {"episode": int(episode), "optimizer": policy.optimizer.state_dict()}
+    state = {"episode": int(episode), "optimizer": policy.optimizer.state_dict(),
+             "lr": policy.optimizer.param_groups[0]["lr"]}
     if trainer.value_normalizer is not None:
         state["value_normalizer"] = trainer.value_normalizer.state_dict()
     if extra:
         state.update(extra)
     _atomic_save(state, path)
+
+
+def latest_checkpoint(models_dir):
+    """Highest episode with both ``transformer_{ep}.pt`` and ``trainer_state_{ep}.pt`` present."""
+    import re
+    if not models_dir or not os.path.isdir(models_dir):
+        return None
+    eps = []
+    for f in os.listdir(models_dir):
+        m = re.fullmatch(r"trainer_state_(\d+)\.pt", f)
+        if m and os.path.exists(os.path.join(models_dir, f"transformer_{m.group(1)}.pt")):
+            eps.append(int(m.group(1)))
+    return max(eps) if eps else None
+
+
+def save_env_state(models_dir, episode, rank, env):
+    """Per-rank env counters.  Philox streams are counter-based, so (task counter, preset index) regenerate the
+    current task exactly on restore."""
+    os.makedirs(str(models_dir), exist_ok=True)
+    st = {"task_ctr": env.task_ctr.cpu(), "preset_idx": env.preset_idx.cpu()}
+    _atomic_save(st, os.path.join(str(models_dir), f"env_state_{episode}_rank{rank}.pt"))
+
+
+def load_env_state(models_dir, episode, rank, env):
+    path = os.path.join(str(models_dir), f"env_state_{episode}_rank{rank}.pt")
+    if not os.path.exists(path):
+        return False
+    st = torch.load(path, map_location="cpu", weights_only=True)
+    dev = env.counter.device
+    env.counter.copy_(st["task_ctr"].to(dev))
+    env.preset_idx.copy_((st["preset_idx"] - 1).clamp(min=0).to(dev))
+    env._reset(torch.ones(env.E, dtype=torch.bool, device=dev))
+    return True
 
 
 def load_trainer_state(path, policy, trainer):
