@@ -29,7 +29,7 @@ DEFAULT_ARGV = ["--n_rollout_threads", "8", "--num_env_steps", "1000000", "--sav
                 "--lr", "5e-5", "--critic_lr", "5e-5", "--ppo_epoch", "15", "--num_mini_batch", "4",
                 "--gamma", "0.99", "--use_valuenorm", "--use_popart", "--entropy_coef", "0.01"]
 
-SUPPORTED = ("mat", "mat_dec", "mat_encoder", "mat_decoder", "mat_gru", "momat", "happo", "rmappo", "ppo",
+SUPPORTED = ("mat", "mat_dec", "mat_encoder", "mat_decoder", "mat_gru", "momat", "dmomat", "happo", "rmappo", "ppo",
              "ippo", "hatrpo", "random")
 
 
@@ -54,6 +54,9 @@ def main(args):
         raise NotImplementedError(all_args.algorithm_name)
     if all_args.algorithm_name == "rmappo":
         all_args.use_recurrent_policy = True
+    if all_args.algorithm_name in ("momat", "dmomat"):   # multi-objective MAT: (task completion time, payment)
+        all_args.n_objective = max(2, all_args.n_objective)
+        all_args.use_advantage_norm = all_args.use_advantage_norm or all_args.algorithm_name == "dmomat"
     if all_args.algorithm_name == "mat_dec":
         all_args.dec_actor = True
         all_args.share_actor = True
@@ -70,7 +73,7 @@ def main(args):
     np.random.seed(all_args.seed)
     all_args.use_centralized_V = True
     config = {"all_args": all_args, "device": device, "run_dir": run_dir, "comm": comm}
-    if all_args.algorithm_name in ("mat", "mat_dec", "mat_encoder", "mat_decoder", "mat_gru"):
+    if all_args.algorithm_name in ("mat", "mat_dec", "mat_encoder", "mat_decoder", "mat_gru", "momat", "dmomat"):
         runner = Runner(config)
     else:
         from mat_dcml_amd.runner.baseline_runner import BaselineRunner

@@ -18,10 +18,12 @@ import torch
 
 class RolloutBuffer:
     def __init__(self, T, E, A, obs_dim, share_dim, act_dim, act_out=1, logp_dim=1, gamma=0.99, gae_lambda=0.95,
-                 use_valuenorm=True, n_objective=1, device="cpu", store_share=True):
+                 use_valuenorm=True, n_objective=1, device="cpu", store_share=True, use_advantage_norm=False):
         self.T, self.E, self.A = T, E, A
         self.gamma, self.gae_lambda = gamma, gae_lambda
         self.use_valuenorm = use_valuenorm
+        self.use_advantage_norm = use_advantage_norm   # DMO buffer: GAE in ValueNorm-normalised space
+        self.n_objective = n_objective
         dev = torch.device(device)
         f32 = torch.float32
         self.obs = torch.zeros(T + 1, E, A, obs_dim, dtype=f32, device=dev)
@@ -64,7 +66,21 @@ class RolloutBuffer:
 
     @torch.no_grad()
     def compute_returns(self, next_value, value_normalizer=None):
+        """GAE per objective column.  ``use_advantage_norm`` = the DMO buffer (``dmo_shared_buffer.py:233-280``):
+        delta = normalize(r) + γ·v' − v on normalised predictions, returns = denormalize(gae + v) once the
+        normaliser has statistics (the raw objectives before that)."""
         self.value_preds[-1].copy_(next_value.view_as(self.value_preds[-1]))
+        vn = value_normalizer if self.use_valuenorm else None
+        if self.use_advantage_norm and vn is not None:
+            updated = bool(vn.debiasing_term.reshape(-1)[0] > 0)
+            r = vn.normalize(self.rewards)
+            g = torch.zeros_like(self.rewards[0])
+            for t in reversed(range(self.T)):
+                delta = r[t] + self.gamma * self.value_preds[t + 1] * self.masks[t + 1] - self.value_preds[t]
+                g = delta + self.gamma * self.gae_lambda * self.masks[t + 1] * g
+                self.advantages[t] = g
+                self.returns[t] = vn.denormalize(g + self.value_preds[t]) if updated else self.rewards[t]
+            return
         from ..ops import rl_ops
         rl_ops.gae(self.rewards, self.value_preds, self.masks, self.gamma, self.gae_lambda,
                    value_normalizer if self.use_valuenorm else None, self.advantages, self.returns)

@@ -61,7 +61,7 @@ class TransformerPolicy:
             self.act_prob_dim = self.act_dim
         self.num_agents = num_agents
         self.n_objective = getattr(args, "n_objective", 1)
-        if self.algorithm_name in ("mat", "mat_dec", "momat"):
+        if self.algorithm_name in ("mat", "mat_dec", "momat", "dmomat"):
             self.transformer = MultiAgentTransformer(
                 self.share_obs_dim, self.obs_dim, self.act_dim, num_agents, n_block=args.n_block, n_embd=args.n_embd,
                 n_head=args.n_head, encode_state=args.encode_state, device=self.device, action_type=self.action_type,

@@ -87,6 +87,7 @@ class DCMLRunner:
         self.buffer = RolloutBuffer(a.episode_length, E, self.num_agents, self.dcml.obs_dim, self.dcml.share_dim,
                                     self.dcml.action_dim, gamma=a.gamma, gae_lambda=a.gae_lambda,
                                     use_valuenorm=a.use_valuenorm or a.use_popart, n_objective=a.n_objective,
+                                    use_advantage_norm=bool(getattr(a, "use_advantage_norm", False)),
                                     device=self.device)
         self.log_dir = os.path.join(str(self.run_dir), "logs") if self.run_dir else None
         self.save_dir = os.path.join(str(self.run_dir), "models") if self.run_dir else None
@@ -128,7 +129,7 @@ class DCMLRunner:
                 obs, share, reward, done, delay, pay, ava = self.envs.step(actions)
             with self.timers("insert"):
                 self._track(reward, done, delay, pay)
-                self.insert(obs, share, reward, done, ava, values, actions, logp)
+                self.insert(obs, share, reward, done, ava, values, actions, logp, delay, pay)
 
     def _track(self, reward, done, delay, pay):
         self._ep_reward += reward
@@ -142,11 +143,14 @@ class DCMLRunner:
         self._ep_delay *= keep
         self._ep_pay *= keep
 
-    def insert(self, obs, share, reward, done, ava, values, actions, logp):
+    def insert(self, obs, share, reward, done, ava, values, actions, logp, delay=None, pay=None):
         E, A = self.buffer.E, self.buffer.A
         masks = (~done).float().view(E, 1, 1).expand(E, A, 1)
-        self.buffer.insert(share, obs, actions, logp, values, reward.view(E, 1, 1).expand(E, A, 1), masks,
-                           None, ava)
+        if self.buffer.n_objective == 2:   # multi-objective MAT: objectives (-completion time, -payment)
+            rew = torch.stack([-delay, -pay], -1).view(E, 1, 2).expand(E, A, 2)
+        else:
+            rew = reward.view(E, 1, 1).expand(E, A, 1)
+        self.buffer.insert(share, obs, actions, logp, values, rew, masks, None, ava)
 
     def compute(self):
         pass  # next-value + GAE are recomputed inside every PPO epoch (mat_trainer.py:178-192)
@@ -191,10 +195,13 @@ class DCMLRunner:
     def log(self, episode, episodes, total, start, infos):
         stats = self._done_stats.clone()
         self.comm.all_reduce_sum_(stats)
-        avg_step_reward = self.buffer.rewards.mean().reshape(1).double()
+        avg_step_reward = self.buffer.rewards.mean((0, 1, 2)).double()    # per objective
         self.comm.all_reduce_mean_(avg_step_reward)
         infos = {k: float(v) for k, v in infos.items()}
-        infos["average_step_rewards"] = float(avg_step_reward)
+        infos["average_step_rewards"] = float(avg_step_reward.sum())
+        if avg_step_reward.numel() > 1:   # dcml_runner.py:306-309
+            for i in range(avg_step_reward.numel()):
+                infos[f"average_step_objective_{i}"] = float(avg_step_reward[i])
         self._done_stats.zero_()
         if not self.comm.is_main:
             return
