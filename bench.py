@@ -37,7 +37,12 @@ def main():
     p.add_argument("--kernels", default="auto")
     p.add_argument("--dtype", default="bf16")
     p.add_argument("--phases", action="store_true")
+    p.add_argument("--config", default="dcml", choices=["dcml", "smac"],
+                   help="dcml: the headline 32-worker DCML config; smac: MAT on the SMAC-shaped 27m_vs_30m stress env")
+    p.add_argument("--no_eval", action="store_true", help="skip the post-timing eval latency probe")
     a = p.parse_args()
+    if a.config == "smac":
+        return bench_smac(a)
 
     from mat_dcml_amd.config import get_config, parse_args
     from mat_dcml_amd.parallel.comm import init_from_env
@@ -79,6 +84,9 @@ def main():
     n = comm.world_size
     env_steps = a.steps * a.episode_length * a.envs * n
     value = env_steps / dt
+    eval_info = None
+    if not a.no_eval and comm.is_main:   # "eval task time": batch-1 deterministic decision latency, stride 10
+        eval_info = eval_probe(runner, dev)
     if comm.is_main:
         if a.phases:
             print(runner.timers.summary(), file=sys.stderr)
@@ -94,7 +102,62 @@ def main():
                        "parallelism": f"dp{n}", "envs_per_gpu": a.envs, "episode_length": a.episode_length,
                        "ppo_epoch": 15, "num_mini_batch": 4, "kernels": a.kernels,
                        "device": torch.cuda.get_device_name(dev) if dev.type == "cuda" else "cpu"},
+            "eval": eval_info,
         }), flush=True)
+    comm.destroy()
+
+
+def eval_probe(runner, dev, n=30):
+    """Per-decision latency of the deterministic batch-decision path (stride 10, batch 1) and the mean task
+    completion time / payment over a short preset replay (DCML_MAT_ALT_Benchmark.py protocol, 1 point)."""
+    from mat_dcml_amd.runner.benchmark import run_sweep
+    res = run_sweep(runner.policy, runner.dcml, dev, sweep="AW", n_points=1, steps=100, shards=10, stride=10,
+                    latency_b1=n, verbose=False)
+    return {"decision_ms_b1_stride10": round(res["decision_ms_b1"], 4),
+            "decision_ms_batched": round(res["decision_ms_batched"], 4), "ct_aw_all": round(res["ct"][0], 4),
+            "payment_aw_all": round(res["payment"][0], 4), "weights": "random-init"}
+
+
+def bench_smac(a):
+    """BASELINE config #5 (cross-env stress): MAT on the SMAC-shaped 27m_vs_30m env, 32 envs per GPU,
+    episode_length 100, ppo_epoch 15, 1 minibatch, clip 0.05 (train_smac.sh)."""
+    from mat_dcml_amd.config import _SMAC_FLAGS, get_config, parse_args
+    from mat_dcml_amd.parallel.comm import init_from_env
+    from mat_dcml_amd.runner.smac_runner import SMACRunner
+    comm = init_from_env(prefer_gpu=True)
+    envs = a.envs if a.envs != 256 else 32
+    T = a.episode_length if a.episode_length != 50 else 100
+    argv = ["--env_name", "StarCraft2", "--algorithm_name", "mat", "--map_name", "27m_vs_30m", "--n_rollout_threads",
+            str(envs), "--episode_length", str(T), "--lr", "5e-4", "--ppo_epoch", "15", "--num_mini_batch", "1",
+            "--clip_param", "0.05", "--use_value_active_masks", "--kernels", a.kernels, "--dtype", a.dtype]
+    args = parse_args(argv, get_config(), extra=_SMAC_FLAGS, warn=False)
+    runner = SMACRunner({"all_args": args, "device": comm.device, "run_dir": None, "comm": comm})
+    runner.warmup()
+    dev = comm.device
+    for _ in range(a.warmup):
+        runner.train_iteration()
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        runner.train_iteration()
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    comm.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    comm.all_reduce_max_(t)
+    dt, n = float(t), comm.world_size
+    value = a.steps * T * envs * n / dt
+    if comm.is_main:
+        print(json.dumps({"metric": "env-steps/sec (whole node) MAT on SMAC 27m_vs_30m (synthetic SMAC-shaped env)",
+                          "value": round(value, 2), "unit": "env-steps/s", "n_gpus": n, "steps": a.steps,
+                          "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
+                          "data": "synthetic (SMAC-shaped on-device env: 27 agents x 1288 obs, 36 actions)",
+                          "config": {"model": "MAT (2+2 blocks, d=64, 2 heads) on SMAC 27m_vs_30m", "global_batch":
+                                     envs * n, "seq_len": 27, "parallelism": f"dp{n}", "episode_length": T}}),
+              flush=True)
     comm.destroy()
 
 

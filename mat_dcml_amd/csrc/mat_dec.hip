@@ -141,10 +141,7 @@ __device__ __forceinline__ void attn_cross_bwd(const Mat* m, const LNp& ln, RT* 
   __syncthreads();
   // recompute k, v (from x1) and q (from rep)
   g2lds_rows(c.XB, sv_x1, c.tok0, c.NR, c.NT * 16, c.tid);
-  for (int it = c.tid; it < c.nseq * 2 * c.L; it += 256) {
-    const int s = it / (2 * c.L), rem = it - s * 2 * c.L, h = rem / c.L, i = rem - h * c.L;
-    c.LSE[it] = sv_lse[(size_t)(c.tok0 + s * c.L + i) * 2 + h];
-  }
+  load_lse(sv_lse, c);
 #pragma unroll
   for (int k = 0; k < MAXRT; ++k) {
     const int rt = c.wave + 4 * k;

@@ -109,145 +109,255 @@ __device__ __forceinline__ void st_head_f(bf16_t* buf, int row, int h, const flo
 
 constexpr float ATT_SCALE = 0.17677669529663687f;  // 1/sqrt(32)
 
-// ------------------------------------------------------------------------------------------ attention (VALU)
-// items (s, h, i): online softmax over the keys of sequence s; O may alias Q (each item reads only its own q row)
-__device__ __forceinline__ void attn_fwd(const bf16_t* Q, const bf16_t* K, const bf16_t* V, bf16_t* O, bool causal, float* lse_g,
-                         const Ctx& c) {
-  const int L = c.L, n_items = c.nseq * 2 * L;
-  for (int it = c.tid; it < n_items; it += 256) {
-    const int s = it / (2 * L), rem = it - s * 2 * L, h = rem / L, i = rem - h * L;
-    const int row = s * L + i;
-    uint32_t q[16];
-    ld_head_u(Q, row, h, q);
-    float m = -1e30f, l = 0.f, acc[32];
+#ifdef MDL_ATTN_VALU
+#include "attn_valu.h"
+#else
+// ------------------------------------------------------------------------------------------ attention (MFMA)
+// Sequence-block-diagonal attention over the workgroup's packed rows (rows of sequence s = [sL, sL+L)), on
+// v_mfma_f32_16x16x32_bf16 with the head dimension (32) as one K step.  Work items = (16-row tile, head), one per
+// wave at a time; keys / queries are visited in 32-row chunks aligned to 32 (always inside the NRP-row buffers)
+// and masked to the item's sequences (+ causal).
+//
+// Layout trick: the score tile is computed TRANSPOSED (Sᵀ = K·Qᵀ, A operand = K rows in the permuted order
+// pi_t(m) = 8(m>>2) + 4t + (m&3) for the two 16-key halves t of a chunk).  The C layout then leaves lane (g, c)
+// holding S[query c][key kb + 8g + j] for j = 4t + r — exactly the A-operand layout of the following P·V MFMA,
+// whose B operand (V, K along the token axis) comes from ds_read_b64_tr_b16 transposed reads (ld_frag_T).
+// No LDS round trip for P / dS.  LSE / delta live in LDS as [head][row] (NRP rows per head).
+__device__ __forceinline__ int pi_row(int t, int m) { return 8 * (m >> 2) + 4 * t + (m & 3); }
+
+__device__ __forceinline__ bf16x8 pack8(const float* x) {
+  bf16x8 f;
 #pragma unroll
-    for (int d = 0; d < 32; ++d) acc[d] = 0.f;
-    const int jn = causal ? i + 1 : L;
-    for (int j = 0; j < jn; ++j) {
-      const int kr = s * L + j;
-      uint32_t k[16];
-      ld_head_u(K, kr, h, k);
-      float d = 0.f;
+  for (int j = 0; j < 8; ++j) f[j] = (short)f2bf(x[j]);
+  return f;
+}
+
+// x ≈ hi + lo with both halves bf16 (≈16 mantissa bits): dS has rows summing to zero and feeds bias gradients,
+// where a single bf16 rounding of dS leaves a visible bias; two MFMAs (hi, lo) keep it at fp32-like accuracy.
+__device__ __forceinline__ void pack8_split(const float* x, bf16x8& hi, bf16x8& lo) {
 #pragma unroll
-      for (int t = 0; t < 16; ++t) d = dot2(q[t], k[t], d);
-      d *= ATT_SCALE;
-      if (d > m + 8.f) {  // lazy rescale: exp(d - m) stays <= e^8 between rescales
-        const float cf = __expf(m - d);
-        l *= cf;
-#pragma unroll
-        for (int e = 0; e < 32; ++e) acc[e] *= cf;
-        m = d;
-      }
-      const float pj = __expf(d - m);
-      l += pj;
-      uint32_t v[16];
-      ld_head_u(V, kr, h, v);
-#pragma unroll
-      for (int t = 0; t < 16; ++t) {
-        acc[2 * t] += pj * lo_bf(v[t]);
-        acc[2 * t + 1] += pj * hi_bf(v[t]);
-      }
-    }
-    const float inv = 1.f / l;
-#pragma unroll
-    for (int d = 0; d < 32; ++d) acc[d] *= inv;
-    st_head_f(O, row, h, acc);
-    if (lse_g) lse_g[(size_t)(c.tok0 + row) * 2 + h] = m + __logf(l);
+  for (int j = 0; j < 8; ++j) {
+    const uint16_t h = f2bf(x[j]);
+    hi[j] = (short)h;
+    lo[j] = (short)f2bf(x[j] - bf2f(h));
   }
 }
 
-// backward pass 1 (by query row): recompute P from the saved log-sum-exp, delta_i = dO_i·O_i, dq_i
+// scores of one 32-key chunk, transposed: out[j] = S[q][kb + 8g + j] (q = this lane's query column)
+__device__ __forceinline__ void score_chunk_T(const bf16_t* K, int kb, int h, bf16x8 qB, float* out, int lane) {
+  const int g = lane >> 4, c16 = lane & 15;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const bf16x8 a = lda_tm(K, kb + pi_row(t, c16), 4 * h + g);
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    const f32x4 r = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qB, z, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[4 * t + i] = r[i];
+  }
+}
+
+struct SeqSpan { int lo, hi; };   // [lo, hi) rows of the sequences a 16-row tile touches, 32-aligned chunk bounds
+
+__device__ __forceinline__ SeqSpan tile_span(int t16, const Ctx& c, bool causal_hi) {
+  const int r0 = t16 * 16, r1 = min(r0 + 15, c.NR - 1);
+  const int lo = (r0 / c.L) * c.L;
+  const int hi = causal_hi ? r1 + 1 : min((r1 / c.L + 1) * c.L, c.NR);
+  return SeqSpan{lo & ~31, (hi + 31) & ~31};
+}
+
+// forward: O (may alias Q) = softmax(scale Q Kᵀ) V per head; lse_g (global [tok][2]) written if non-null
+__device__ __forceinline__ void attn_fwd(const bf16_t* Q, const bf16_t* K, const bf16_t* V, bf16_t* O, bool causal, float* lse_g,
+                                         const Ctx& c) {
+  const int lane = c.lane, g = lane >> 4, c16 = lane & 15;
+  for (int item = c.wave; item < 2 * c.NT; item += 4) {
+    const int qt = item >> 1, h = item & 1;
+    const int q = qt * 16 + c16;
+    const bool qv = q < c.NR;
+    const int qs = (q / c.L) * c.L, qe = causal ? q + 1 : min(qs + c.L, c.NR);
+    const SeqSpan sp = tile_span(qt, c, causal);
+    const bf16x8 qB = lda_tm(Q, q, 4 * h + g);
+    // pass 1: per-lane online max / sum over its 8 keys per chunk, then merge the 4 lane groups
+    float m = -INFINITY, l = 0.f;
+    for (int kb = sp.lo; kb < sp.hi; kb += 32) {
+      float sc[8];
+      score_chunk_T(K, kb, h, qB, sc, lane);
+      float cm = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = kb + 8 * g + j;
+        sc[j] = (qv && k >= qs && k < qe) ? sc[j] * ATT_SCALE : -INFINITY;
+        cm = fmaxf(cm, sc[j]);
+      }
+      const float nm = fmaxf(m, cm);
+      if (nm > -INFINITY) {
+        float add = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) add += __expf(sc[j] - nm);
+        l = l * __expf(m - nm) + add;
+        m = nm;
+      }
+    }
+#pragma unroll
+    for (int x = 16; x <= 32; x <<= 1) {
+      const float om = __shfl_xor(m, x, 64), ol = __shfl_xor(l, x, 64);
+      const float nm = fmaxf(m, om);
+      l = (nm > -INFINITY) ? l * __expf(m - nm) + ol * __expf(om - nm) : 0.f;
+      m = nm;
+    }
+    const float lse = l > 0.f ? m + __logf(l) : 0.f;
+    // pass 2: P = exp(S - lse) (already normalised) → O = P V on MFMA
+    f32x4 o[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    for (int kb = sp.lo; kb < sp.hi; kb += 32) {
+      float sc[8];
+      score_chunk_T(K, kb, h, qB, sc, lane);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = kb + 8 * g + j;
+        sc[j] = (qv && k >= qs && k < qe) ? __expf(sc[j] * ATT_SCALE - lse) : 0.f;
+      }
+      bf16x8 pah, pal;
+      pack8_split(sc, pah, pal);
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const bf16x8 vf = ld_frag_T(V, kb, 32 * h + 16 * dt, lane);
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pah, vf, o[dt], 0, 0, 0);
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pal, vf, o[dt], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = qt * 16 + 4 * g + r;
+        O[tmo(row, 32 * h + 16 * dt + c16)] = f2bf(row < c.NR ? o[dt][r] : 0.f);
+      }
+    if (lse_g && g == 0 && qv) lse_g[(size_t)(c.tok0 + q) * 2 + h] = lse;
+  }
+}
+
+// backward pass 1 (by query tile): delta_q = sum_k P dP, dS = P (dP - delta), dQ = scale dS K  (→ DQ)
 __device__ __forceinline__ void attn_bwd_q(const bf16_t* Q, const bf16_t* K, const bf16_t* V, const bf16_t* DA, bf16_t* DQ,
-                           bool causal, const Ctx& c) {
+                                           bool causal, const Ctx& c) {
 #ifdef MDL_ABLATE_ATTN
   return;
 #endif
-  const int L = c.L, n_items = c.nseq * 2 * L;
-  for (int it = c.tid; it < n_items; it += 256) {
-    const int s = it / (2 * L), rem = it - s * 2 * L, h = rem / L, i = rem - h * L;
-    const int row = s * L + i;
-    uint32_t q[16], da[16];
-    ld_head_u(Q, row, h, q);
-    ld_head_u(DA, row, h, da);
-    const float lse = c.LSE[it];
-    const int jn = causal ? i + 1 : L;
-    float o[32];
-#pragma unroll
-    for (int d = 0; d < 32; ++d) o[d] = 0.f;
-    for (int j = 0; j < jn; ++j) {
-      const int kr = s * L + j;
-      uint32_t k[16], v[16];
-      ld_head_u(K, kr, h, k);
-      float d = 0.f;
-#pragma unroll
-      for (int t = 0; t < 16; ++t) d = dot2(q[t], k[t], d);
-      const float p = __expf(d * ATT_SCALE - lse);
-      ld_head_u(V, kr, h, v);
-#pragma unroll
-      for (int t = 0; t < 16; ++t) { o[2 * t] += p * lo_bf(v[t]); o[2 * t + 1] += p * hi_bf(v[t]); }
-    }
+  const int lane = c.lane, g = lane >> 4, c16 = lane & 15;
+  for (int item = c.wave; item < 2 * c.NT; item += 4) {
+    const int qt = item >> 1, h = item & 1;
+    const int q = qt * 16 + c16;
+    const bool qv = q < c.NR;
+    const int qs = (q / c.L) * c.L, qe = causal ? q + 1 : min(qs + c.L, c.NR);
+    const SeqSpan sp = tile_span(qt, c, causal);
+    const bf16x8 qB = lda_tm(Q, q, 4 * h + g), dB = lda_tm(DA, q, 4 * h + g);
+    const float lse = c.LSE[h * c.NRP + q];
     float delta = 0.f;
+    for (int kb = sp.lo; kb < sp.hi; kb += 32) {
+      float sc[8], dp[8];
+      score_chunk_T(K, kb, h, qB, sc, lane);
+      score_chunk_T(V, kb, h, dB, dp, lane);
 #pragma unroll
-    for (int t = 0; t < 16; ++t) delta += lo_bf(da[t]) * o[2 * t] + hi_bf(da[t]) * o[2 * t + 1];
-    c.DEL[it] = delta;
-    float dq[32];
+      for (int j = 0; j < 8; ++j) {
+        const int k = kb + 8 * g + j;
+        if (qv && k >= qs && k < qe) delta += __expf(sc[j] * ATT_SCALE - lse) * dp[j];
+      }
+    }
+    delta += __shfl_xor(delta, 16, 64);
+    delta += __shfl_xor(delta, 32, 64);
+    f32x4 dq[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    for (int kb = sp.lo; kb < sp.hi; kb += 32) {
+      float sc[8], dp[8];
+      score_chunk_T(K, kb, h, qB, sc, lane);
+      score_chunk_T(V, kb, h, dB, dp, lane);
 #pragma unroll
-    for (int d = 0; d < 32; ++d) dq[d] = 0.f;
-    for (int j = 0; j < jn; ++j) {
-      const int kr = s * L + j;
-      uint32_t k[16], v[16];
-      ld_head_u(K, kr, h, k);
-      ld_head_u(V, kr, h, v);
-      float d = 0.f, dp = 0.f;
+      for (int j = 0; j < 8; ++j) {
+        const int k = kb + 8 * g + j;
+        sc[j] = (qv && k >= qs && k < qe) ? __expf(sc[j] * ATT_SCALE - lse) * (dp[j] - delta) : 0.f;
+      }
+      bf16x8 dah, dal;
+      pack8_split(sc, dah, dal);
 #pragma unroll
-      for (int t = 0; t < 16; ++t) { d = dot2(q[t], k[t], d); dp = dot2(da[t], v[t], dp); }
-      const float p = __expf(d * ATT_SCALE - lse);
-      const float ds = p * (dp - delta);
-#pragma unroll
-      for (int t = 0; t < 16; ++t) { dq[2 * t] += ds * lo_bf(k[t]); dq[2 * t + 1] += ds * hi_bf(k[t]); }
+      for (int dt = 0; dt < 2; ++dt) {
+        const bf16x8 kf = ld_frag_T(K, kb, 32 * h + 16 * dt, lane);
+        dq[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dah, kf, dq[dt], 0, 0, 0);
+        dq[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dal, kf, dq[dt], 0, 0, 0);
+      }
     }
 #pragma unroll
-    for (int d = 0; d < 32; ++d) dq[d] *= ATT_SCALE;
-    st_head_f(DQ, row, h, dq);
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = qt * 16 + 4 * g + r;
+        DQ[tmo(row, 32 * h + 16 * dt + c16)] = f2bf(row < c.NR ? dq[dt][r] * ATT_SCALE : 0.f);
+      }
+    if (g == 0) c.DEL[h * c.NRP + q] = qv ? delta : 0.f;
   }
 }
 
-// backward pass 2 (by key row): dk_j, dv_j, written in place over K / V
+// backward pass 2 (by key tile): dV = Pᵀ dO, dK = scale dSᵀ Q, written in place over K / V (head columns)
 __device__ __forceinline__ void attn_bwd_kv(const bf16_t* Q, bf16_t* K, bf16_t* V, const bf16_t* DA, bool causal, const Ctx& c) {
 #ifdef MDL_ABLATE_ATTN
   return;
 #endif
-  const int L = c.L, n_items = c.nseq * 2 * L;
-  for (int it = c.tid; it < n_items; it += 256) {
-    const int s = it / (2 * L), rem = it - s * 2 * L, h = rem / L, j = rem - h * L;
-    const int row = s * L + j;
-    uint32_t k[16], v[16];
-    ld_head_u(K, row, h, k);
-    ld_head_u(V, row, h, v);
-    float dk[32], dv[32];
+  const int lane = c.lane, g = lane >> 4, c16 = lane & 15;
+  for (int item = c.wave; item < 2 * c.NT; item += 4) {
+    const int kt = item >> 1, h = item & 1;
+    const int k = kt * 16 + c16;
+    const bool kv = k < c.NR;
+    const int ks = (k / c.L) * c.L, ke = min(ks + c.L, c.NR);
+    const int qlo = causal ? k : ks;   // queries that see key k
+    SeqSpan sp = tile_span(kt, c, false);
+    if (causal) sp.lo = (kt * 16) & ~31;
+    const bf16x8 kB = lda_tm(K, k, 4 * h + g), vB = lda_tm(V, k, 4 * h + g);
+    f32x4 dk[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, dv[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    for (int qb = sp.lo; qb < sp.hi; qb += 32) {
+      float sc[8], dp[8];
+      score_chunk_T(Q, qb, h, kB, sc, lane);    // sc[j] = S[query qb + 8g + j][key k]
+      score_chunk_T(DA, qb, h, vB, dp, lane);   // dp[j] = dP[query][key k]
+      const float4* lp = (const float4*)(c.LSE + h * c.NRP + qb + 8 * g);
+      const float4* dl = (const float4*)(c.DEL + h * c.NRP + qb + 8 * g);
+      const float4 l0 = lp[0], l1 = lp[1], d0 = dl[0], d1 = dl[1];
+      const float lsev[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+      const float delv[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+      float p[8], ds[8];
 #pragma unroll
-    for (int d = 0; d < 32; ++d) { dk[d] = 0.f; dv[d] = 0.f; }
-    const int base = (s * 2 + h) * L;
-    for (int i = causal ? j : 0; i < L; ++i) {
-      const int qr = s * L + i;
-      uint32_t q[16], da[16];
-      ld_head_u(Q, qr, h, q);
-      ld_head_u(DA, qr, h, da);
-      float d = 0.f, dp = 0.f;
+      for (int j = 0; j < 8; ++j) {
+        const int qq = qb + 8 * g + j;
+        const bool ok = kv && qq >= qlo && qq < ke;
+        p[j] = ok ? __expf(sc[j] * ATT_SCALE - lsev[j]) : 0.f;
+        ds[j] = ok ? p[j] * (dp[j] - delv[j]) : 0.f;
+      }
+      bf16x8 pah, pal, dsh, dsl;
+      pack8_split(p, pah, pal);
+      pack8_split(ds, dsh, dsl);
 #pragma unroll
-      for (int t = 0; t < 16; ++t) { d = dot2(q[t], k[t], d); dp = dot2(da[t], v[t], dp); }
-      const float p = __expf(d * ATT_SCALE - c.LSE[base + i]);
-      const float ds = p * (dp - c.DEL[base + i]);
-#pragma unroll
-      for (int t = 0; t < 16; ++t) {
-        dk[2 * t] += ds * lo_bf(q[t]); dk[2 * t + 1] += ds * hi_bf(q[t]);
-        dv[2 * t] += p * lo_bf(da[t]); dv[2 * t + 1] += p * hi_bf(da[t]);
+      for (int dt = 0; dt < 2; ++dt) {
+        const bf16x8 of = ld_frag_T(DA, qb, 32 * h + 16 * dt, lane);
+        dv[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pah, of, dv[dt], 0, 0, 0);
+        dv[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pal, of, dv[dt], 0, 0, 0);
+        const bf16x8 qf = ld_frag_T(Q, qb, 32 * h + 16 * dt, lane);
+        dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dsh, qf, dk[dt], 0, 0, 0);
+        dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dsl, qf, dk[dt], 0, 0, 0);
       }
     }
 #pragma unroll
-    for (int d = 0; d < 32; ++d) dk[d] *= ATT_SCALE;
-    st_head_f(K, row, h, dk);
-    st_head_f(V, row, h, dv);
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = kt * 16 + 4 * g + r;
+        const bool ok = row < c.NR;
+        K[tmo(row, 32 * h + 16 * dt + c16)] = f2bf(ok ? dk[dt][r] * ATT_SCALE : 0.f);
+        V[tmo(row, 32 * h + 16 * dt + c16)] = f2bf(ok ? dv[dt][r] : 0.f);
+      }
+  }
+}
+
+#endif  // MDL_ATTN_VALU
+
+// saved per-row log-sum-exp ([tok][2] global) -> LDS [head][NRP]
+__device__ __forceinline__ void load_lse(const float* sv_lse, const Ctx& c) {
+  for (int i = c.tid; i < 2 * c.NRP; i += 256) {
+    const int h = i / c.NRP, row = i - h * c.NRP;
+    c.LSE[i] = row < c.NR ? sv_lse[(size_t)(c.tok0 + row) * 2 + h] : 0.f;
   }
 }
 
@@ -530,10 +640,7 @@ __device__ __forceinline__ void attn_self_bwd(const Mat* m, const LNp& ln, RT* d
   __syncthreads();
   // recompute q, k, v from the saved input (whole tile, cooperative copy)
   g2lds_rows(c.XB, sv_xin, c.tok0, c.NR, c.NT * 16, c.tid);
-  for (int it = c.tid; it < c.nseq * 2 * c.L; it += 256) {
-    const int s = it / (2 * c.L), rem = it - s * 2 * c.L, h = rem / c.L, i = rem - h * c.L;
-    c.LSE[it] = sv_lse[(size_t)(c.tok0 + s * c.L + i) * 2 + h];
-  }
+  load_lse(sv_lse, c);
   __syncthreads();
   {
     bf16_t* outs[3] = {c.QB, c.KB, c.VB};
@@ -603,14 +710,15 @@ __device__ __forceinline__ Ctx make_ctx(const PT& p, char* smem) {
   bf16_t* base = (bf16_t*)smem;
   c.QB = base; c.KB = base + bs; c.VB = base + 2 * bs; c.DA = base + 3 * bs; c.DQ = base + 4 * bs; c.XB = base + 5 * bs;
   c.LSE = (float*)(base + 6 * bs);
-  c.DEL = c.LSE + p.SQ * 2 * p.L;
+  c.DEL = c.LSE + 2 * p.NRP;
   return c;
 }
 
 }  // namespace
 
 __host__ __device__ inline size_t mat_train_lds_bytes(int NRP, int SQ, int L) {
-  return (size_t)NRP * 64 * 2 * 6 + (size_t)SQ * 2 * L * 4 * 2;
+  const size_t aux = (size_t)NRP * 2 * 4 * 2;   // LSE / delta [2][NRP] f32 (also the decoder's embedding-grad scratch)
+  return (size_t)NRP * 64 * 2 * 6 + (aux < 9 * 64 * 4 ? 9 * 64 * 4 : aux);
 }
 
 

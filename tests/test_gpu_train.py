@@ -118,4 +118,5 @@ def test_full_mat_fused_grads(gpu, L, B):
             lim = max(6e-2, 2.5 * rel(refb[n], r)) if n != "decoder.log_std" else max(0.1, 10 * rel(refb[n], r))
         if e > lim:
             bad.append((n, round(e, 4), round(rel(refb[n], r), 4)))
+        print(f"{n:45s} err {e:.4f} yardstick {rel(refb[n], r):.4f} |ref| {r.norm().item():.4e}")
     assert not bad, bad
