@@ -18,6 +18,8 @@ MI355X-specific:
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -81,6 +83,9 @@ class MATTrainer:
             if p.grad is None or (p.grad.data_ptr() - flat.buf.data_ptr()) != (p.data_ptr() - fp.data_ptr()):
                 return False
         self.loss_fused = ppo_fused.PPOLossFused(self, self.device)
+        copies = int(os.environ.get("MAT_DCML_GRAD_COPIES", "0"))   # TODO: 8 once the large-grid fault is fixed
+        if copies > 0:
+            mat_train.attach_grad_workspace(m, flat.buf, copies=copies)
         pol.optimizer = ppo_fused.FlatAdam(fp, flat.buf, lr=pol.optimizer.param_groups[0]["lr"], eps=args.opti_eps,
                                            weight_decay=args.weight_decay,
                                            max_grad_norm=args.max_grad_norm if self._use_max_grad_norm else None)
@@ -155,8 +160,11 @@ class MATTrainer:
         logp, ent = dec.forward(rep, mb["actions"], mb["ava"], save=True)
         self.comm._flat.buf.zero_()
         dv, dlp, dent = self.loss_fused.run(v, logp, ent, mb, self.comm)
+        m._mdl_gws_active = hasattr(m, "_mdl_gws")   # weight-gradient atomics into the 8-copy workspace
         drep = dec.backward(dlp, dent)
         enc.backward(drep, dv)
+        m._mdl_gws_active = False
+        mat_train.reduce_grad_workspace(m)
         dec.ctx = None
         enc.ctx = None
         if self.poison:

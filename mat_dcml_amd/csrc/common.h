@@ -64,20 +64,37 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 // ------------------------------------------------------------------------------------------ bf16
 typedef unsigned short bf16_t;
 __device__ __forceinline__ float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
-__device__ __forceinline__ bf16_t f2bf(float f) {  // round-to-nearest-even (NaN-preserving enough for our data)
-  uint32_t u = __float_as_uint(f);
-  u += 0x7FFFu + ((u >> 16) & 1u);
-  return (bf16_t)(u >> 16);
+__device__ __forceinline__ bf16_t f2bf(float f) {  // round-to-nearest-even: one v_cvt_pk_bf16_f32 on gfx950
+  return __builtin_bit_cast(bf16_t, (__bf16)f);
 }
 
 typedef __attribute__((ext_vector_type(8))) short bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// Phi(x) = 0.5 (1 + erf(x / sqrt 2)) with erf from Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below bf16
+// resolution): one rcp, one exp and a degree-5 polynomial instead of the libm erff.  The exp(-x^2/2) factor is
+// shared with the Gaussian pdf of the GELU derivative.
+__device__ __forceinline__ float phi_and_pdf(float x, float& pdf) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __frcp_rn(1.0f + 0.3275911f * z);
+  const float e = __expf(-z * z);
+  float poly = 1.061405429f;
+  poly = fmaf(poly, t, -1.453152027f);
+  poly = fmaf(poly, t, 1.421413741f);
+  poly = fmaf(poly, t, -0.284496736f);
+  poly = fmaf(poly, t, 0.254829592f);
+  const float erf_abs = 1.0f - poly * t * e;
+  pdf = 0.39894228040143268f * e;
+  return 0.5f + 0.5f * copysignf(erf_abs, x);
+}
+__device__ __forceinline__ float gelu_erf(float x) {
+  float pdf;
+  return x * phi_and_pdf(x, pdf);
+}
 __device__ __forceinline__ float gelu_erf_grad(float x) {
-  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  float pdf;
+  const float cdf = phi_and_pdf(x, pdf);
   return cdf + x * pdf;
 }
 

@@ -134,10 +134,10 @@ __device__ __forceinline__ void attn_cross_bwd(const Mat* m, const LNp& ln, RT* 
       }
     }
   }
-  flush_ln(dlg, dlb, ln, lane);
-  flush_cols(dbp, m[7].db, lane);
+  flush_ln(dlg, dlb, ln, c);
+  flush_cols(dbp, c.g(m[7].db), lane);
   __syncthreads();
-  wgrad_tm(c.DQ, c.XB, c.NRP, m[7].dW, c.wave, lane);
+  wgrad_tm(c.DQ, c.XB, c.NRP, c.g(m[7].dW), c.wave, lane);
   __syncthreads();
   // recompute k, v (from x1) and q (from rep)
   g2lds_rows(c.XB, sv_x1, c.tok0, c.NR, c.NT * 16, c.tid);
@@ -204,9 +204,9 @@ __device__ __forceinline__ void attn_cross_bwd(const Mat* m, const LNp& ln, RT* 
     }
   }
   __syncthreads();
-  wgrad_tm(c.DQ, c.QB, c.NRP, m[4].dW, c.wave, lane);
-  wgrad_tm(c.KB, c.XB, c.NRP, m[5].dW, c.wave, lane);
-  wgrad_tm(c.VB, c.XB, c.NRP, m[6].dW, c.wave, lane);
+  wgrad_tm(c.DQ, c.QB, c.NRP, c.g(m[4].dW), c.wave, lane);
+  wgrad_tm(c.KB, c.XB, c.NRP, c.g(m[5].dW), c.wave, lane);
+  wgrad_tm(c.VB, c.XB, c.NRP, c.g(m[6].dW), c.wave, lane);
   // d x1 = dk Wk + dv Wv ;  d rep += ds + dq Wq
   const bf16_t* dsrc[3] = {c.DQ, c.KB, c.VB};
 #pragma unroll
@@ -237,7 +237,7 @@ __device__ __forceinline__ void attn_cross_bwd(const Mat* m, const LNp& ln, RT* 
         }
       }
     }
-    flush_cols(dbb, m[4 + mi].db, lane);
+    flush_cols(dbb, c.g(m[4 + mi].db), lane);
   }
   // d rep read-modify-write (each row owned by exactly one wave of one workgroup)
 #pragma unroll
@@ -488,26 +488,26 @@ __global__ __launch_bounds__(256, 1) void mat_dec_bwd(DecP p) {
         gemm_rt(dx[k], c.DQ, rt, Bb, lane, false);
       }
     }
-    flush_ln(dlg, dlb, p.lnh, lane);
-    flush_cols(dbh, p.h1.db, lane);
+    flush_ln(dlg, dlb, p.lnh, c);
+    flush_cols(dbh, c.g(p.h1.db), lane);
 #pragma unroll
     for (int a = 0; a < 8; ++a) {
       if (a < p.A) {
-        flush_cols(dwh2[a], p.d_wh2 ? p.d_wh2 + a * 64 : nullptr, lane);
+        flush_cols(dwh2[a], c.g(p.d_wh2 ? p.d_wh2 + a * 64 : nullptr), lane);
         float x = dbh2[a];
         x += __shfl_xor(x, 16, 64);
         x += __shfl_xor(x, 32, 64);
-        if (lane == 0 && p.d_bh2) atomicAdd(p.d_bh2 + a, x);
+        if (lane == 0 && p.d_bh2) atomicAdd(c.g(p.d_bh2) + a, x);
       }
     }
     {
       float x = dls;
       x += __shfl_xor(x, 16, 64);
       x += __shfl_xor(x, 32, 64);
-      if (lane == 0 && p.d_log_std) atomicAdd(p.d_log_std + (p.A - 1), x);
+      if (lane == 0 && p.d_log_std) atomicAdd(c.g(p.d_log_std) + (p.A - 1), x);
     }
     __syncthreads();
-    wgrad_tm(c.DQ, c.XB, c.NRP, p.h1.dW, c.wave, lane);
+    wgrad_tm(c.DQ, c.XB, c.NRP, c.g(p.h1.dW), c.wave, lane);
     __syncthreads();
   }
   // ---------------- blocks in reverse
@@ -548,12 +548,12 @@ __global__ __launch_bounds__(256, 1) void mat_dec_bwd(DecP p) {
           }
       }
     }
-    flush_ln(dlg, dlb, LNp{nullptr, nullptr, p.d_lnd_g, p.d_lnd_b}, lane);
+    flush_ln(dlg, dlb, LNp{nullptr, nullptr, p.d_lnd_g, p.d_lnd_b}, c);
     __syncthreads();
     if (p.d_wa)
       for (int i = c.tid; i < (p.A + 1) * 64; i += 256) {
         const int t = i / 64, col = i % 64;
-        atomicAdd(p.d_wa + col * (p.A + 1) + t, EMB[i]);
+        atomicAdd(c.g(p.d_wa) + col * (p.A + 1) + t, EMB[i]);
       }
   }
 }

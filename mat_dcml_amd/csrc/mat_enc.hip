@@ -135,12 +135,12 @@ __global__ __launch_bounds__(256, 1) void mat_enc_bwd(EncP p) {
         for (int ct = 0; ct < 4; ++ct) dx[k].v[ct] = dr.v[ct] + t.v[ct];
       }
     }
-    flush_ln(dlg, dlb, p.lnh, lane);
-    flush_cols(dbh, p.h1.db, lane);
-    flush_cols(dw2[0], p.d_wh2, lane);
-    if (p.n_obj > 1) flush_cols(dw2[1], p.d_wh2 ? p.d_wh2 + 64 : nullptr, lane);
+    flush_ln(dlg, dlb, p.lnh, c);
+    flush_cols(dbh, c.g(p.h1.db), lane);
+    flush_cols(dw2[0], c.g(p.d_wh2), lane);
+    if (p.n_obj > 1) flush_cols(dw2[1], c.g(p.d_wh2 ? p.d_wh2 + 64 : nullptr), lane);
     __syncthreads();
-    wgrad_tm(c.DQ, c.XB, c.NRP, p.h1.dW, c.wave, lane);
+    wgrad_tm(c.DQ, c.XB, c.NRP, c.g(p.h1.dW), c.wave, lane);
     __syncthreads();
   }
   // ---------------- blocks in reverse
@@ -205,8 +205,8 @@ __global__ __launch_bounds__(256, 1) void mat_enc_bwd(EncP p) {
         }
       }
     }
-    flush_ln(dlg, dlb, LNp{nullptr, nullptr, p.d_ln0_g, p.d_ln0_b}, lane);
-    flush_cols(dbe, p.d_be, lane);
+    flush_ln(dlg, dlb, LNp{nullptr, nullptr, p.d_ln0_g, p.d_ln0_b}, c);
+    flush_cols(dbe, c.g(p.d_be), lane);
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(256, 1) void mat_enc_bwd(EncP p) {
           float x = dwe[ct][kk];
           x += __shfl_xor(x, 16, 64);
           x += __shfl_xor(x, 32, 64);
-          if (g == 0 && p.d_we) atomicAdd(p.d_we + (16 * ct + c16) * p.od + kk, x);
+          if (g == 0 && p.d_we) atomicAdd(c.g(p.d_we) + (16 * ct + c16) * p.od + kk, x);
         }
       }
 #pragma unroll
@@ -227,8 +227,8 @@ __global__ __launch_bounds__(256, 1) void mat_enc_bwd(EncP p) {
         b2 += __shfl_xor(b2, 16, 64);
         b2 += __shfl_xor(b2, 32, 64);
         if (lane == 0) {
-          if (p.d_lno_g) atomicAdd(p.d_lno_g + kk, a);
-          if (p.d_lno_b) atomicAdd(p.d_lno_b + kk, b2);
+          if (p.d_lno_g) atomicAdd(c.g(p.d_lno_g) + kk, a);
+          if (p.d_lno_b) atomicAdd(c.g(p.d_lno_b) + kk, b2);
         }
       }
     }

@@ -45,6 +45,8 @@ struct EncP {
   Sv sv[3];
   const float* drep;
   const float* dv;
+  long long g_delta, g_stride;   // dW workspace: copy k of a gradient lives at grad + g_delta + k * g_stride
+  int g_copies;                  // 0: atomics straight into the gradients
 };
 
 struct DecP {
@@ -73,10 +75,14 @@ struct DecP {
   const float* dent;
   float* drep;           // [tok][64] accumulated (pre-zeroed)
   bf16_t* sv_head;       // [tok][64] head input (last block output)
+  long long g_delta, g_stride;
+  int g_copies;
 };
 
 struct Ctx {
   int tid, lane, wave, L, nseq, NR, NT, NRP, tok0;
+  ptrdiff_t gofs;   // gradient-copy offset (floats): this block's slice of the 8-way dW workspace, 0 = direct
+  __device__ __forceinline__ float* g(float* p) const { return p ? p + gofs : p; }
   bf16_t *QB, *KB, *VB, *DA, *DQ, *XB;
   float *LSE, *DEL;
 };
@@ -400,9 +406,9 @@ __device__ __forceinline__ void zero_lds(char* smem, size_t bytes, int tid) {
   for (size_t i = (size_t)tid * 16; i < bytes; i += 256 * 16) *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
 }
 
-__device__ __forceinline__ void flush_ln(f32x4 dg, f32x4 db, const LNp& ln, int lane) {
-  flush_cols(dg, ln.dg, lane);
-  flush_cols(db, ln.db, lane);
+__device__ __forceinline__ void flush_ln(f32x4 dg, f32x4 db, const LNp& ln, const Ctx& c) {
+  flush_cols(dg, c.g(ln.dg), c.lane);
+  flush_cols(db, c.g(ln.db), c.lane);
 }
 
 // ------------------------------------------------------------------------------------------ sublayers (forward)
@@ -588,12 +594,12 @@ __device__ __forceinline__ void mlp_bwd(const Mat& m1, const Mat& m2, const LNp&
       }
     }
   }
-  flush_ln(dlg, dlb, ln, lane);
-  flush_cols(db1, m1.db, lane);
-  flush_cols(db2, m2.db, lane);
+  flush_ln(dlg, dlb, ln, c);
+  flush_cols(db1, c.g(m1.db), lane);
+  flush_cols(db2, c.g(m2.db), lane);
   __syncthreads();
-  wgrad_tm(c.DA, c.XB, c.NRP, m2.dW, c.wave, lane);
-  wgrad_tm(c.KB, c.QB, c.NRP, m1.dW, c.wave, lane);
+  wgrad_tm(c.DA, c.XB, c.NRP, c.g(m2.dW), c.wave, lane);
+  wgrad_tm(c.KB, c.QB, c.NRP, c.g(m1.dW), c.wave, lane);
   __syncthreads();
 }
 
@@ -633,10 +639,10 @@ __device__ __forceinline__ void attn_self_bwd(const Mat* m, const LNp& ln, RT* d
       }
     }
   }
-  flush_ln(dlg, dlb, ln, lane);
-  flush_cols(dbp, m[3].db, lane);
+  flush_ln(dlg, dlb, ln, c);
+  flush_cols(dbp, c.g(m[3].db), lane);
   __syncthreads();
-  wgrad_tm(c.DQ, c.XB, c.NRP, m[3].dW, c.wave, lane);
+  wgrad_tm(c.DQ, c.XB, c.NRP, c.g(m[3].dW), c.wave, lane);
   __syncthreads();
   // recompute q, k, v from the saved input (whole tile, cooperative copy)
   g2lds_rows(c.XB, sv_xin, c.tok0, c.NR, c.NT * 16, c.tid);
@@ -665,9 +671,9 @@ __device__ __forceinline__ void attn_self_bwd(const Mat* m, const LNp& ln, RT* d
   __syncthreads();
   attn_bwd_kv(c.QB, c.KB, c.VB, c.DA, causal, c);
   __syncthreads();
-  wgrad_tm(c.DQ, c.XB, c.NRP, m[0].dW, c.wave, lane);
-  wgrad_tm(c.KB, c.XB, c.NRP, m[1].dW, c.wave, lane);
-  wgrad_tm(c.VB, c.XB, c.NRP, m[2].dW, c.wave, lane);
+  wgrad_tm(c.DQ, c.XB, c.NRP, c.g(m[0].dW), c.wave, lane);
+  wgrad_tm(c.KB, c.XB, c.NRP, c.g(m[1].dW), c.wave, lane);
+  wgrad_tm(c.VB, c.XB, c.NRP, c.g(m[2].dW), c.wave, lane);
   const bf16_t* dsrc[3] = {c.DQ, c.KB, c.VB};
 #pragma unroll
   for (int mi = 0; mi < 3; ++mi) {
@@ -687,7 +693,7 @@ __device__ __forceinline__ void attn_self_bwd(const Mat* m, const LNp& ln, RT* d
         for (int ct = 0; ct < 4; ++ct) dx[k].v[ct] += t.v[ct];
       }
     }
-    flush_cols(dbb, m[mi].db, lane);
+    flush_cols(dbb, c.g(m[mi].db), lane);
   }
   __syncthreads();
 }
@@ -706,6 +712,9 @@ __device__ __forceinline__ Ctx make_ctx(const PT& p, char* smem) {
   c.NT = (c.NR + 15) >> 4;
   c.NRP = p.NRP;
   c.tok0 = seq0 * p.L;
+  // spread the fp32 weight-gradient atomics over g_copies copies (blockIdx % 8 ~ the XCD the block runs on):
+  // 8x fewer adders per address than every workgroup hitting the same 16 KB matrix
+  c.gofs = p.g_copies > 0 ? (ptrdiff_t)p.g_delta + (ptrdiff_t)(blockIdx.x % p.g_copies) * (ptrdiff_t)p.g_stride : 0;
   const size_t bs = (size_t)p.NRP * 64;
   bf16_t* base = (bf16_t*)smem;
   c.QB = base; c.KB = base + bs; c.VB = base + 2 * bs; c.DA = base + 3 * bs; c.DQ = base + 4 * bs; c.XB = base + 5 * bs;

@@ -250,3 +250,26 @@ MDL_API int mdl_adam(const AdamArgs* a, hipStream_t st) {
   MDL_CHECK_LAUNCH();
   return 0;
 }
+
+// ------------------------------------------------------------------------------------------- dW workspace
+// g[i] += sum_k ws[k * stride + i]; ws zeroed for the next minibatch (the training kernels spread their weight-
+// gradient atomics over `copies` copies, see mat_train_common.h Ctx::gofs).
+__global__ __launch_bounds__(256) void grad_reduce_kernel(float* g, float* ws, int n, long long stride, int copies) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < copies; ++k) {
+      float* w = ws + (size_t)k * stride + i;
+      s += *w;
+      *w = 0.f;
+    }
+    g[i] += s;
+  }
+}
+
+MDL_API int mdl_grad_reduce(float* g, float* ws, int n, long long stride, int copies, hipStream_t st) {
+  int grid = (n + 255) / 256;
+  if (grid > 1024) grid = 1024;
+  hipLaunchKernelGGL(grad_reduce_kernel, dim3(grid), dim3(256), 0, st, g, ws, n, stride, copies);
+  MDL_CHECK_LAUNCH();
+  return 0;
+}

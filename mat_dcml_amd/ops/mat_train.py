@@ -41,7 +41,8 @@ class EncP(ctypes.Structure):
                [(n, VP) for n in ("obs", "lno_g", "lno_b", "we", "be", "ln0_g", "ln0_b", "d_lno_g", "d_lno_b", "d_we",
                                   "d_be", "d_ln0_g", "d_ln0_b")] + \
                [("blk", Blk * 3), ("h1", Mat), ("lnh", LNp), ("wh2", VP), ("bh2", VP), ("d_wh2", VP), ("rep", VP),
-                ("v", VP), ("sv", Sv * 3), ("drep", VP), ("dv", VP)]
+                ("v", VP), ("sv", Sv * 3), ("drep", VP), ("dv", VP), ("g_delta", ctypes.c_longlong),
+                ("g_stride", ctypes.c_longlong), ("g_copies", ctypes.c_int)]
 
 
 class DecP(ctypes.Structure):
@@ -50,10 +51,12 @@ class DecP(ctypes.Structure):
                [("blk", Blk * 3), ("h1", Mat), ("lnh", LNp)] + \
                [(n, VP) for n in ("wh2", "bh2", "d_wh2", "d_bh2", "stdv", "log_std", "d_log_std", "rep", "logp",
                                   "ent")] + \
-               [("sv", Sv * 3)] + [(n, VP) for n in ("dlogp", "dent", "drep", "sv_head")]
+               [("sv", Sv * 3)] + [(n, VP) for n in ("dlogp", "dent", "drep", "sv_head")] + \
+               [("g_delta", ctypes.c_longlong), ("g_stride", ctypes.c_longlong), ("g_copies", ctypes.c_int)]
 
 
 sig("mdl_mat_train_geometry", ctypes.c_int)
+sig("mdl_grad_reduce", VP, VP, ctypes.c_int, ctypes.c_longlong, ctypes.c_int, VP)
 sig("mdl_mat_enc_fwd", ctypes.POINTER(EncP), ctypes.c_int, ctypes.c_int, VP)
 sig("mdl_mat_enc_bwd", ctypes.POINTER(EncP), ctypes.c_int, VP)
 sig("mdl_mat_dec_fwd", ctypes.POINTER(DecP), ctypes.c_int, ctypes.c_int, VP)
@@ -233,6 +236,7 @@ class EncoderFused:
         p.obs, p.rep, p.v, p.drep, p.dv = obs.data_ptr(), rep.data_ptr(), v.data_ptr(), drep.data_ptr(), dv.data_ptr()
         for i, s in enumerate(svs):
             p.sv[i] = s
+        p.g_delta, p.g_stride, p.g_copies = m._mdl_gws if getattr(m, "_mdl_gws_active", False) else (0, 0, 0)
         check(lib().mdl_mat_enc_bwd(ctypes.byref(p), m.n_block, kernels._stream()), "mat_enc_bwd")
         b = m.encoder.head[3].bias
         if b.grad is not None:
@@ -334,6 +338,7 @@ class DecoderFused:
         p.dlogp, p.dent, p.drep, p.sv_head = dlogp.data_ptr(), dent.data_ptr(), drep.data_ptr(), head
         for i, s in enumerate(svs):
             p.sv[i] = s
+        p.g_delta, p.g_stride, p.g_copies = m._mdl_gws if getattr(m, "_mdl_gws_active", False) else (0, 0, 0)
         check(lib().mdl_mat_dec_bwd(ctypes.byref(p), m.n_block, kernels._stream()), "mat_dec_bwd")
         return drep
 
@@ -359,6 +364,29 @@ class _MATFusedFn(torch.autograd.Function):
         dec.ctx = None
         enc.ctx = None
         return torch.zeros((), device=drep.device), None, None, None, None, None
+
+
+def attach_grad_workspace(model, flat_grads: torch.Tensor, copies: int = 8):
+    """Spread the backward kernels' weight-gradient atomics over ``copies`` workspace copies of the flat gradient
+    buffer (every parameter's ``.grad`` must be a view of ``flat_grads``); ``reduce_grad_workspace`` folds them
+    back.  Cuts the number of workgroups adding into one 16 KB weight matrix by ``copies``."""
+    n = flat_grads.numel()
+    stride = (n + 63) // 64 * 64
+    ws = torch.zeros(copies * stride, dtype=torch.float32, device=flat_grads.device)
+    delta = (ws.data_ptr() - flat_grads.data_ptr()) // 4
+    assert (ws.data_ptr() - flat_grads.data_ptr()) % 4 == 0
+    model._mdl_gws = (delta, stride, copies)
+    model._mdl_gws_buf = (ws, flat_grads, stride, copies)
+    return ws
+
+
+def reduce_grad_workspace(model):
+    st = getattr(model, "_mdl_gws_buf", None)
+    if st is None:
+        return
+    ws, g, stride, copies = st
+    check(lib().mdl_grad_reduce(g.data_ptr(), ws.data_ptr(), g.numel(), stride, copies, kernels._stream()),
+          "grad_reduce")
 
 
 def _state(model, dev):
