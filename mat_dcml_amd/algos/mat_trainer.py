@@ -83,7 +83,7 @@ class MATTrainer:
             if p.grad is None or (p.grad.data_ptr() - flat.buf.data_ptr()) != (p.data_ptr() - fp.data_ptr()):
                 return False
         self.loss_fused = ppo_fused.PPOLossFused(self, self.device)
-        copies = int(os.environ.get("MAT_DCML_GRAD_COPIES", "0"))   # TODO: 8 once the large-grid fault is fixed
+        copies = int(os.environ.get("MAT_DCML_GRAD_COPIES", "8"))
         if copies > 0:
             mat_train.attach_grad_workspace(m, flat.buf, copies=copies)
         pol.optimizer = ppo_fused.FlatAdam(fp, flat.buf, lr=pol.optimizer.param_groups[0]["lr"], eps=args.opti_eps,

@@ -284,9 +284,8 @@ __device__ __forceinline__ float mask_logit(const DecP& p, int tok, int a, float
 
 // ============================================================================================== decoder forward
 template <int NB, bool SAVE>
-__global__ __launch_bounds__(256, 1) void mat_dec_fwd(DecP p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const Ctx c = make_ctx(p, smem);
+__device__ __forceinline__ void mat_dec_fwd_tile(const DecP& p, char* smem, int seq0, int nseq) {
+  const Ctx c = make_ctx(p, smem, seq0, nseq);
   if (c.nseq <= 0) return;
   zero_lds(smem, mat_train_lds_bytes(p.NRP, p.SQ, p.L), c.tid);
   __syncthreads();
@@ -375,11 +374,16 @@ __global__ __launch_bounds__(256, 1) void mat_dec_fwd(DecP p) {
   }
 }
 
+template <int NB, bool SAVE>
+__global__ __launch_bounds__(256, 1) void mat_dec_fwd(DecP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  FOR_TILES(p, (mat_dec_fwd_tile<NB, SAVE>(p, smem, s0, ns)));
+}
+
 // ============================================================================================== decoder backward
 template <int NB>
-__global__ __launch_bounds__(256, 1) void mat_dec_bwd(DecP p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const Ctx c = make_ctx(p, smem);
+__device__ __forceinline__ void mat_dec_bwd_tile(const DecP& p, char* smem, int seq0, int nseq) {
+  const Ctx c = make_ctx(p, smem, seq0, nseq);
   if (c.nseq <= 0) return;
   zero_lds(smem, mat_train_lds_bytes(p.NRP, p.SQ, p.L), c.tid);
   __syncthreads();
@@ -556,6 +560,12 @@ __global__ __launch_bounds__(256, 1) void mat_dec_bwd(DecP p) {
         atomicAdd(c.g(p.d_wa) + col * (p.A + 1) + t, EMB[i]);
       }
   }
+}
+
+template <int NB>
+__global__ __launch_bounds__(256, 1) void mat_dec_bwd(DecP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  FOR_TILES(p, (mat_dec_bwd_tile<NB>(p, smem, s0, ns)));
 }
 
 

@@ -3,9 +3,8 @@
 
 // ============================================================================================== encoder forward
 template <int NB, bool SAVE>
-__global__ __launch_bounds__(256, 1) void mat_enc_fwd(EncP p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const Ctx c = make_ctx(p, smem);
+__device__ __forceinline__ void mat_enc_fwd_tile(const EncP& p, char* smem, int seq0, int nseq) {
+  const Ctx c = make_ctx(p, smem, seq0, nseq);
   if (c.nseq <= 0) return;
   zero_lds(smem, mat_train_lds_bytes(p.NRP, p.SQ, p.L), c.tid);
   __syncthreads();
@@ -68,11 +67,16 @@ __global__ __launch_bounds__(256, 1) void mat_enc_fwd(EncP p) {
   }
 }
 
+template <int NB, bool SAVE>
+__global__ __launch_bounds__(256, 1) void mat_enc_fwd(EncP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  FOR_TILES(p, (mat_enc_fwd_tile<NB, SAVE>(p, smem, s0, ns)));
+}
+
 // ============================================================================================== encoder backward
 template <int NB>
-__global__ __launch_bounds__(256, 1) void mat_enc_bwd(EncP p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const Ctx c = make_ctx(p, smem);
+__device__ __forceinline__ void mat_enc_bwd_tile(const EncP& p, char* smem, int seq0, int nseq) {
+  const Ctx c = make_ctx(p, smem, seq0, nseq);
   if (c.nseq <= 0) return;
   zero_lds(smem, mat_train_lds_bytes(p.NRP, p.SQ, p.L), c.tid);
   __syncthreads();
@@ -233,6 +237,12 @@ __global__ __launch_bounds__(256, 1) void mat_enc_bwd(EncP p) {
       }
     }
   }
+}
+
+template <int NB>
+__global__ __launch_bounds__(256, 1) void mat_enc_bwd(EncP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  FOR_TILES(p, (mat_enc_bwd_tile<NB>(p, smem, s0, ns)));
 }
 
 

@@ -17,6 +17,7 @@
 // reads and are flushed with one fp32 atomic per element per workgroup.
 #pragma once
 #include "tile.h"
+#include <cstdlib>
 
 using namespace mdl;
 
@@ -700,14 +701,14 @@ __device__ __forceinline__ void attn_self_bwd(const Mat* m, const LNp& ln, RT* d
 
 // ------------------------------------------------------------------------------------------ context
 template <typename PT>
-__device__ __forceinline__ Ctx make_ctx(const PT& p, char* smem) {
+__device__ __forceinline__ Ctx make_ctx(const PT& p, char* smem, int seq0, int nseq) {
   Ctx c;
   c.tid = threadIdx.x;
+  asm volatile("" : "+v"(c.tid));   // opaque per tile: lane-derived addresses are not hoisted out of the tile loop
   c.lane = c.tid & 63;
-  c.wave = c.tid >> 6;
+  c.wave = __builtin_amdgcn_readfirstlane(c.tid >> 6);
   c.L = p.L;
-  const int seq0 = blockIdx.x * p.SQ;
-  c.nseq = min(p.SQ, p.Bs - seq0);
+  c.nseq = nseq;
   c.NR = c.nseq * p.L;
   c.NT = (c.NR + 15) >> 4;
   c.NRP = p.NRP;
@@ -731,13 +732,41 @@ __host__ __device__ inline size_t mat_train_lds_bytes(int NRP, int SQ, int L) {
 }
 
 
+// Persistent, balanced tiling: workgroup w owns the contiguous sequence range [Bs*w/G, Bs*(w+1)/G) and walks it in
+// near-equal chunks of <= SQ sequences.  With G = #CUs the makespan is ceil(Bs/G) sequences per CU instead of
+// ceil(Bs/SQ/G) full tiles (640 tiles of 5 on 256 CUs = 3 rounds of 5 -> 13 sequences per CU).
+#define FOR_TILES(p, CALL)                                                                         \
+  {                                                                                                \
+    const long long G_ = gridDim.x, w_ = blockIdx.x;                                               \
+    const int lo_ = (int)((long long)(p).Bs * w_ / G_), hi_ = (int)((long long)(p).Bs * (w_ + 1) / G_); \
+    const int n_ = hi_ - lo_, nch_ = (n_ + (p).SQ - 1) / (p).SQ;                                   \
+    for (int ch_ = 0; ch_ < nch_; ++ch_) {                                                         \
+      const int s0 = lo_ + (int)((long long)n_ * ch_ / nch_);                                      \
+      const int ns = lo_ + (int)((long long)n_ * (ch_ + 1) / nch_) - s0;                           \
+      if (ch_) __syncthreads();                                                                    \
+      CALL;                                                                                        \
+    }                                                                                              \
+  }
+
+static int n_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    const char* e = getenv("MAT_DCML_PERSISTENT");
+    if (e && e[0] == '0') n = 1 << 30;   // one tile per workgroup (non-persistent grid)
+  }
+  return n;
+}
+
 template <typename K, typename PT>
 static int launch(K kern, const PT* p, hipStream_t st) {
   const size_t lds = mat_train_lds_bytes(p->NRP, p->SQ, p->L);
   if (lds > 160 * 1024) return -2;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return (int)e;
-  const int grid = (p->Bs + p->SQ - 1) / p->SQ;
+  const int tiles = (p->Bs + p->SQ - 1) / p->SQ;
+  const int grid = tiles < n_cus() ? tiles : n_cus();
   hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, *p);
   MDL_CHECK_LAUNCH();
   return 0;

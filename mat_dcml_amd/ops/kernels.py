@@ -72,7 +72,14 @@ def _declare(L):
 
 
 def sig(name, *args):
+    """Register an entry point's argument types.  Applied at load time, and immediately when the library is
+    already loaded (modules that declare signatures may be imported after the first launch — without this, raw
+    Python-int pointers would be passed as 32-bit C ints)."""
     _SIGS[name] = list(args)
+    if _lib is not None:
+        fn = getattr(_lib, name)
+        fn.argtypes = list(args)
+        fn.restype = ctypes.c_int
 
 
 def check(rc, name):

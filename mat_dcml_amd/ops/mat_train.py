@@ -237,6 +237,8 @@ class EncoderFused:
         for i, s in enumerate(svs):
             p.sv[i] = s
         p.g_delta, p.g_stride, p.g_copies = m._mdl_gws if getattr(m, "_mdl_gws_active", False) else (0, 0, 0)
+        if p.g_copies:
+            check_grad_ptrs(p, m._mdl_gws_buf[1])
         check(lib().mdl_mat_enc_bwd(ctypes.byref(p), m.n_block, kernels._stream()), "mat_enc_bwd")
         b = m.encoder.head[3].bias
         if b.grad is not None:
@@ -339,6 +341,8 @@ class DecoderFused:
         for i, s in enumerate(svs):
             p.sv[i] = s
         p.g_delta, p.g_stride, p.g_copies = m._mdl_gws if getattr(m, "_mdl_gws_active", False) else (0, 0, 0)
+        if p.g_copies:
+            check_grad_ptrs(p, m._mdl_gws_buf[1])
         check(lib().mdl_mat_dec_bwd(ctypes.byref(p), m.n_block, kernels._stream()), "mat_dec_bwd")
         return drep
 
@@ -378,6 +382,30 @@ def attach_grad_workspace(model, flat_grads: torch.Tensor, copies: int = 8):
     model._mdl_gws = (delta, stride, copies)
     model._mdl_gws_buf = (ws, flat_grads, stride, copies)
     return ws
+
+
+def _grad_ptr_fields(st, prefix=""):
+    """All gradient pointers of an EncP / DecP ctypes struct (d_* / dW / db / dg / db fields), recursively."""
+    out = []
+    for name, typ in st._fields_:
+        v = getattr(st, name)
+        if isinstance(v, ctypes.Array):
+            for i, e in enumerate(v):
+                if isinstance(e, ctypes.Structure):
+                    out += _grad_ptr_fields(e, f"{prefix}{name}[{i}].")
+        elif isinstance(v, ctypes.Structure):
+            out += _grad_ptr_fields(v, f"{prefix}{name}.")
+        elif (name.startswith("d_") or name in ("dW", "db", "dg")) and v:
+            out.append((prefix + name, v))
+    return out
+
+
+def check_grad_ptrs(p, flat):
+    """Host-side guard for the gradient workspace: every gradient pointer must lie inside ``flat``."""
+    lo, hi = flat.data_ptr(), flat.data_ptr() + flat.numel() * 4
+    bad = [(n, v) for n, v in _grad_ptr_fields(p) if not (lo <= v < hi)]
+    if bad:
+        raise RuntimeError(f"gradient pointers outside the flat gradient buffer: {bad[:6]} (flat {lo:#x}..{hi:#x})")
 
 
 def reduce_grad_workspace(model):
