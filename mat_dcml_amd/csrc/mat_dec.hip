@@ -107,13 +107,13 @@ __device__ __forceinline__ void attn_cross_bwd(const Mat* m, const LNp& ln, RT* 
     BFr Bpf, Bpb;
     loadB(Bpf, m[7].fw, lane);
     loadB(Bpb, m[7].bw, lane);
+    g2tiles(c.XB, sv_a, nullptr, nullptr, c);
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
       const int rt = c.wave + 4 * k;
       if (rt < c.NT) {
         const f32x4 vm = row_mask(rt, c.NR, lane);
         RT r_;
-        g2tile(c.XB, sv_a, rt, c);
         ld_g_f(rep, c.tok0, rt, c.NR, r_, lane);
         wave_lds_sync();
         RT s, xh, y, ds;

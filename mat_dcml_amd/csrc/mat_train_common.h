@@ -388,6 +388,39 @@ __device__ __forceinline__ void g2tile(bf16_t* buf, const bf16_t* src, int rt, c
   }
 }
 
+// all of this wave's row tiles of one or two saved activations -> LDS, every global load issued before the first
+// LDS store (one latency instead of one per tile); rows beyond NR are zero-filled.
+__device__ __forceinline__ void g2tiles(bf16_t* buf0, const bf16_t* src0, bf16_t* buf1, const bf16_t* src1,
+                                        const Ctx& c) {
+  uint4 v0[MAXRT][2], v1[MAXRT][2];
+#pragma unroll
+  for (int k = 0; k < MAXRT; ++k) {
+    const int rt = c.wave + 4 * k;
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii) {
+      const int i = c.lane + 64 * ii, row = rt * 16 + (i >> 3), lc = i & 7;
+      const bool ok = rt < c.NT && row < c.NR;
+      const size_t off = (size_t)(c.tok0 + row) * 64 + lc * 8;
+      v0[k][ii] = ok ? *(const uint4*)(src0 + off) : make_uint4(0, 0, 0, 0);
+      v1[k][ii] = (ok && src1) ? *(const uint4*)(src1 + off) : make_uint4(0, 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < MAXRT; ++k) {
+    const int rt = c.wave + 4 * k;
+    if (rt < c.NT) {
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii) {
+        const int i = c.lane + 64 * ii, row = rt * 16 + (i >> 3), lc = i & 7;
+        const int o = (row << 6) + ((lc ^ ((row >> 1) & 7)) << 3);
+        *(uint4*)(buf0 + o) = v0[k][ii];
+        if (src1) *(uint4*)(buf1 + o) = v1[k][ii];
+      }
+    }
+  }
+  wave_lds_sync();
+}
+
 // load a saved bf16 activation tile as an RT via LDS staging (vector global loads; buf rows of tile rt are
 // overwritten and keep the activation, usable as a GEMM / weight-gradient operand afterwards)
 __device__ __forceinline__ void ld_saved(bf16_t* buf, const bf16_t* src, int rt, RT& t, const Ctx& c) {
@@ -556,14 +589,15 @@ __device__ __forceinline__ void mlp_bwd(const Mat& m1, const Mat& m2, const LNp&
     loadB(B2f, m2.fw, lane);
     loadB(B2b, m2.bw, lane);
     loadB(B1b, m1.bw, lane);
+    g2tiles(c.QB, sv_x, c.XB, sv_h, c);     // QB rows = X of dW1, XB = pre-GELU h
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
       const int rt = c.wave + 4 * k;
       if (rt < c.NT) {
         const f32x4 vm = row_mask(rt, c.NR, lane);
         RT x, h, gl;
-        ld_saved(c.QB, sv_x, rt, x, c);     // QB rows = X of dW1
-        ld_saved(c.XB, sv_h, rt, h, c);
+        ld_tm(c.QB, rt, x, lane);
+        ld_tm(c.XB, rt, h, lane);
         gl = h;
         gelu_rt(gl);
         st_tm_m(c.XB, rt, gl, vm, lane);   // X of dW2
@@ -614,14 +648,14 @@ __device__ __forceinline__ void attn_self_bwd(const Mat* m, const LNp& ln, RT* d
     BFr Bpf, Bpb;
     loadB(Bpf, m[3].fw, lane);
     loadB(Bpb, m[3].bw, lane);
+    g2tiles(c.XB, sv_a, c.DA, sv_xin, c);  // XB = attention output (X of dWp), DA = block input
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
       const int rt = c.wave + 4 * k;
       if (rt < c.NT) {
         const f32x4 vm = row_mask(rt, c.NR, lane);
         RT a, xin;
-        g2tile(c.XB, sv_a, rt, c);          // X of dWp
-        ld_saved(c.DA, sv_xin, rt, xin, c);
+        ld_tm(c.DA, rt, xin, lane);
         RT s, xh, y, ds;
         gemm_rt(s, c.XB, rt, Bpf, lane, false);
         add_bias(s, m[3].b, lane);
