@@ -72,7 +72,7 @@ def test_encoder_backward(gpu, L, B):
     assert not bad, bad
 
 
-@pytest.mark.parametrize("L,B", [(33, 40), (5, 77), (101, 6)])
+@pytest.mark.parametrize("L,B", [(33, 40), (5, 77), (101, 6), (129, 3)])
 def test_full_mat_fused_grads(gpu, L, B):
     """Teacher-forced log-prob / entropy / value and ALL parameter gradients of a PPO-like loss."""
     from mat_dcml_amd.models import act as act_mod
