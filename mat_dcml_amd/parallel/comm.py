@@ -125,15 +125,17 @@ def init_from_env(prefer_gpu=True, timeout_s=600) -> Comm:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_gpu = prefer_gpu and torch.cuda.is_available()
-    device = torch.device(f"cuda:{local}") if use_gpu else torch.device("cpu")
+    # one process per GPU; ranks beyond the visible GPU count share devices round-robin (test rehearsal on a
+    # 1-GPU box together with MAT_DCML_DIST_BACKEND=gloo — RCCL wants one device per rank)
+    device = torch.device(f"cuda:{local % max(1, torch.cuda.device_count())}") if use_gpu else torch.device("cpu")
     if use_gpu:
         torch.cuda.set_device(device)
     group = None
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = "nccl" if use_gpu else "gloo"
+        backend = os.environ.get("MAT_DCML_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
-        if use_gpu:
+        if use_gpu and backend == "nccl":
             kw["device_id"] = device
         dist.init_process_group(**kw)
     return Comm(rank, world, local, device, group)

@@ -16,13 +16,15 @@ def _free_port():
     return p
 
 
-def _run(rank, world, port, fn, q):
+def _run(rank, world, port, fn, q, gpu=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
+    if gpu:   # ranks share the box's GPU(s); gloo carries the collectives (RCCL wants one GPU per rank)
+        os.environ["MAT_DCML_DIST_BACKEND"] = "gloo"
     torch.set_num_threads(1)
     try:
         from mat_dcml_amd.parallel.comm import init_from_env
-        comm = init_from_env(prefer_gpu=False)
+        comm = init_from_env(prefer_gpu=gpu)
         q.put((rank, fn(comm)))
         comm.destroy()
     except Exception as e:  # pragma: no cover - surfaced by the assert below
@@ -30,11 +32,11 @@ def _run(rank, world, port, fn, q):
         q.put((rank, "ERR " + traceback.format_exc()))
 
 
-def spawn(fn, world=2):
+def spawn(fn, world=2, gpu=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_run, args=(r, world, port, fn, q)) for r in range(world)]
+    procs = [ctx.Process(target=_run, args=(r, world, port, fn, q, gpu)) for r in range(world)]
     for p in procs:
         p.start()
     out = dict(q.get(timeout=300) for _ in range(world))
@@ -114,3 +116,27 @@ def test_dp_runner_keeps_ranks_in_sync():
     assert out[0][0] == out[1][0] and out[0][1] == out[1][1]  # identical parameters after the update
     assert out[0][2] != out[1][2]                              # but different env partitions
     assert out[0][3] == out[1][3]                              # identical ValueNorm statistics
+
+
+def _runner_case_w32(comm):
+    from mat_dcml_amd.config import get_config, parse_args
+    from mat_dcml_amd.runner.dcml_runner import DCMLRunner
+    args = parse_args(["--n_workers", "32", "--n_rollout_threads", "16", "--episode_length", "8", "--ppo_epoch", "2",
+                       "--num_mini_batch", "2", "--use_valuenorm", "--env_name", "DCML"], get_config(), warn=False)
+    r = DCMLRunner({"all_args": args, "device": comm.device, "run_dir": None, "comm": comm})
+    r.warmup()
+    for _ in range(2):
+        r.train_iteration()
+    flat = torch.cat([p.detach().reshape(-1) for p in r.policy.transformer.parameters()]).double().cpu()
+    return float(flat.sum()), float(flat.pow(2).sum()), bool(r.trainer.fused), \
+        [float(t) for t in r.trainer.value_normalizer.running_mean_var()]
+
+
+@pytest.mark.gpu
+def test_dp_fused_gpu_path_keeps_ranks_in_sync(gpu):
+    """2 ranks on the GPU box through the fused HIP trainer (flat grads, 8-copy dW workspace, fused loss with the
+    ValueNorm sums all-reduced between its kernels, fused Adam): parameters identical across ranks."""
+    out = spawn(_runner_case_w32, world=2, gpu=True)
+    assert out[0][2] and out[1][2]
+    assert out[0][0] == out[1][0] and out[0][1] == out[1][1]
+    assert out[0][3] == out[1][3]
