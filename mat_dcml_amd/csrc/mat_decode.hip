@@ -126,22 +126,35 @@ __device__ __forceinline__ void store_xf(float* X, int lane, const float xf[16])
 }
 
 
-// Causal attention of the pass's tile rows over cached rows 0..i of their env.  8 lanes per (tile row, head):
-// lanes stride over key rows for the scores, then each lane produces 4 of the head's 32 output dims.
-__device__ __forceinline__ void attention_phase(const bf16_t* KV, const float* Q, float* PR, bf16_t* XA,
-                                                const int* ROWI, int R, int EPW, int L, int b, int kind,
-                                                float scale, int tid) {
-  const int pair = tid >> 3, u = tid & 7;
-  const int t = pair >> 1, h = pair & 1;
-  const int i = ROWI[t];
-  const int m = t / R;
-  float* pr = PR + (t * 2 + h) * L;
-  float mx = -INFINITY;
-  if (i >= 0) {
+// Causal attention of the pass's tile rows over cached rows 0..i of their env.  32 lanes (half a wave) per
+// (tile row, head): scores with lanes striding over the keys; P·V with the 32 lanes split into 8 groups of 4 output
+// dims x 4 key groups (each lane sums ~i/4 keys, the 4 key groups are combined by two xor-shuffles).  An item's
+// lanes live in one wave, so the score -> P·V hand-off through PR needs only a wave-level LDS wait.
+template <int lpi>
+__device__ __forceinline__ void attention_phase_t(const bf16_t* KV, const float* Q, float* PR, bf16_t* XA,
+                                                  const int* ROWI, int R, int EPW, int L, int b, int kind,
+                                                  float scale, int tid) {
+  // lpi = lanes per (row, head) item: 32 when <= 4 tile rows are live (rollout), 16 / 8 for the wider stride-mode
+  // passes, so every pass uses all 256 lanes
+  const int u = tid & (lpi - 1);
+  const int dg = u & 7, kg = u >> 3, nkg = lpi >> 3;
+  for (int item = tid / lpi; item < 32; item += 256 / lpi) {
+    const int t = item >> 1, h = item & 1;
+    const int i = ROWI[t];          // uniform over the 32 lanes of the item
+    if (i < 0) {                    // unused tile row: zero A-operand row for the projection
+      if (kg == 0) {
+        bf16_t* xa = XA + t * XP + 32 * h + 4 * dg;
+        xa[0] = 0; xa[1] = 0; xa[2] = 0; xa[3] = 0;
+      }
+      continue;
+    }
+    const int m = t / R;
+    float* pr = PR + (t * 2 + h) * L;
     float q[32];
 #pragma unroll
     for (int d = 0; d < 32; ++d) q[d] = Q[t * SP + 32 * h + d];
-    for (int j = u; j <= i; j += 8) {
+    float mx = -INFINITY;
+    for (int j = u; j <= i; j += lpi) {
       const bf16_t* krow = KV + kv_off(b, kind, m, j, 0, EPW, L) - ((0 ^ (j & 7)) << 3);  // row base
       float dot = 0.f;
 #pragma unroll
@@ -155,27 +168,20 @@ __device__ __forceinline__ void attention_phase(const bf16_t* KV, const float* Q
       pr[j] = sc;
       mx = fmaxf(mx, sc);
     }
-  }
-  mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
-  mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
-  mx = fmaxf(mx, __shfl_xor(mx, 4, 64));
-  float sum = 0.f;
-  if (i >= 0) {
-    for (int j = u; j <= i; j += 8) {
+#pragma unroll
+    for (int x = 1; x < lpi; x <<= 1) mx = fmaxf(mx, __shfl_xor(mx, x, 64));
+    float sum = 0.f;
+    for (int j = u; j <= i; j += lpi) {
       const float pj = __expf(pr[j] - mx);
       pr[j] = pj;
       sum += pj;
     }
-  }
-  sum += __shfl_xor(sum, 1, 64);
-  sum += __shfl_xor(sum, 2, 64);
-  sum += __shfl_xor(sum, 4, 64);
-  __syncthreads();
-  bf16_t* xa = XA + t * XP + 32 * h + 4 * u;
-  if (i >= 0) {
+#pragma unroll
+    for (int x = 1; x < lpi; x <<= 1) sum += __shfl_xor(sum, x, 64);
+    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // PR written by this item's lanes (same wave)
     float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
-    const int lc = 4 * h + (u >> 1), off = 4 * (u & 1);
-    for (int j = 0; j <= i; ++j) {
+    const int lc = 4 * h + (dg >> 1), off = 4 * (dg & 1);
+    for (int j = kg; j <= i; j += nkg) {
       const float pj = pr[j];
       const bf16_t* vrow = KV + kv_off(b, kind + 1, m, j, 0, EPW, L) - ((0 ^ (j & 7)) << 3);
       const uint2 v4 = *(const uint2*)(vrow + ((lc ^ (j & 7)) << 3) + off);
@@ -184,11 +190,25 @@ __device__ __forceinline__ void attention_phase(const bf16_t* KV, const float* Q
       acc2 += pj * __uint_as_float(v4.y << 16);
       acc3 += pj * __uint_as_float(v4.y & 0xFFFF0000u);
     }
-    const float inv = 1.f / sum;
-    xa[0] = f2bf(acc0 * inv); xa[1] = f2bf(acc1 * inv); xa[2] = f2bf(acc2 * inv); xa[3] = f2bf(acc3 * inv);
-  } else {
-    xa[0] = 0; xa[1] = 0; xa[2] = 0; xa[3] = 0;
+#pragma unroll
+    for (int x = 8; x < lpi; x <<= 1) {
+      acc0 += __shfl_xor(acc0, x, 64); acc1 += __shfl_xor(acc1, x, 64);
+      acc2 += __shfl_xor(acc2, x, 64); acc3 += __shfl_xor(acc3, x, 64);
+    }
+    if (kg == 0) {
+      const float inv = 1.f / sum;
+      bf16_t* xa = XA + t * XP + 32 * h + 4 * dg;
+      xa[0] = f2bf(acc0 * inv); xa[1] = f2bf(acc1 * inv); xa[2] = f2bf(acc2 * inv); xa[3] = f2bf(acc3 * inv);
+    }
   }
+}
+
+__device__ __forceinline__ void attention_phase(const bf16_t* KV, const float* Q, float* PR, bf16_t* XA,
+                                                const int* ROWI, int R, int EPW, int L, int b, int kind,
+                                                float scale, int tid, int lpi) {
+  if (lpi == 32) attention_phase_t<32>(KV, Q, PR, XA, ROWI, R, EPW, L, b, kind, scale, tid);
+  else if (lpi == 16) attention_phase_t<16>(KV, Q, PR, XA, ROWI, R, EPW, L, b, kind, scale, tid);
+  else attention_phase_t<8>(KV, Q, PR, XA, ROWI, R, EPW, L, b, kind, scale, tid);
 }
 
 // Action head: LN(head1 output) · W_h2 + b -> logits; availability mask, sampling, log-prob (16 lanes per row).
@@ -319,6 +339,8 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) { crow_i[r] = ROWI[4 * g4 + r]; crow_m[r] = (4 * g4 + r) / R; }
       const int arow_i = ROWI[c16], arow_m = c16 / R;
+      const int live = n_env * R;                           // live tile rows this pass
+      const int lpi = live <= 4 ? 32 : (live <= 8 ? 16 : 8);
 
 #pragma unroll
       for (int b = 0; b < NB; ++b) {
@@ -350,7 +372,7 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
         }
         __syncthreads();
         // ---------------- [B] causal self-attention over cached rows 0..i
-        attention_phase(KV, Q, PR, XA, ROWI, R, EPW, L, b, 0, scale, tid);
+        attention_phase(KV, Q, PR, XA, ROWI, R, EPW, L, b, 0, scale, tid, lpi);
         __syncthreads();
         // ---------------- [C] proj1 + bias + residual x -> S
         afrag_xa(XA, lane, a);
@@ -387,7 +409,7 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
         }
         __syncthreads();
         // ---------------- [E] causal cross-attention (q = rep rows, k/v = x1 rows)
-        attention_phase(KV, Q, PR, XA, ROWI, R, EPW, L, b, 2, scale, tid);
+        attention_phase(KV, Q, PR, XA, ROWI, R, EPW, L, b, 2, scale, tid, lpi);
         __syncthreads();
         // ---------------- [F] proj2 + bias + rep_i -> S
         afrag_xa(XA, lane, a);
