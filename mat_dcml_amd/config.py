@@ -127,6 +127,14 @@ _SMAC_FLAGS = [
     ("n_env_workers", int, None, "worker processes of the CPU env pool (sc2 backend)"),
 ]
 
+# MPE (``mat_src/mat/scripts/train/train_mpe.py:53-60`` + the scenario args the scenarios read)
+_MPE_FLAGS = [
+    ("scenario_name", str, "simple_spread", "MPE scenario"), ("num_landmarks", int, 3, ""),
+    ("num_agents", int, 3, "agents (spread / reference / speaker_listener / push / adversary / crypto)"),
+    ("num_good_agents", int, 1, "good agents (tag / world_comm / attack)"),
+    ("num_adversaries", int, 3, "adversaries (tag / world_comm / attack)"),
+]
+
 # framework (new)
 _FRAMEWORK_FLAGS = [
     ("n_workers", int, 100, "DCML worker count W (agents = W + 1); 4 / 32 / 100 / 128 in the BASELINE configs"),

@@ -51,10 +51,10 @@ class SMACRunner(DCMLRunner):
         self.use_eval, self.eval_interval = a.use_eval, a.eval_interval
         self.train_stride, self.eval_stride = getattr(a, "train_stride", 1), 1
         E, rank = self.n_rollout_threads, self.comm.rank
-        self.envs = config.get("envs") or make_smac_env(a, E, self.device, a.seed, rank * E)
+        self.envs = config.get("envs") or self.make_env(a, E, a.seed, rank * E)
         self.eval_envs = config.get("eval_envs")
         if self.eval_envs is None and self.use_eval:
-            self.eval_envs = make_smac_env(a, self.n_eval_rollout_threads, self.device, a.seed + 7, rank)
+            self.eval_envs = self.make_env(a, self.n_eval_rollout_threads, a.seed + 7, rank)
         self.num_agents = self.envs.n_agents
         obs_dim = self.envs.observation_space[0][0]
         share_dim = self.envs.share_observation_space[0][0]
@@ -78,6 +78,9 @@ class SMACRunner(DCMLRunner):
         self._ep_reward = torch.zeros(E, device=self.device)
         self._done_stats = torch.zeros(4, device=self.device, dtype=torch.float64)   # n, Σreward, won, dead
         self._last_battles = torch.zeros(2, device=self.device)
+
+    def make_env(self, a, n_envs, seed, env_id_offset):
+        return make_smac_env(a, n_envs, self.device, seed, env_id_offset)
 
     def warmup(self):
         obs, state, ava = self.envs.reset()

@@ -55,6 +55,39 @@ def install_stubs():
             sys.path.insert(0, p)
 
 
+def install_gym_stub():
+    """Minimal ``gym`` for the reference MPE env (``environment.py`` / ``multi_discrete.py``): only the space
+    classes and ``gym.Env`` it subclasses.  gym itself is not installed."""
+    if "gym" in sys.modules:
+        return
+    import numpy as np
+    gym = types.ModuleType("gym")
+    spaces = types.ModuleType("gym.spaces")
+    envs = types.ModuleType("gym.envs")
+    reg = types.ModuleType("gym.envs.registration")
+
+    class Space:
+        pass
+
+    class Discrete(Space):
+        def __init__(self, n):
+            self.n = n
+
+    class Box(Space):
+        def __init__(self, low, high, shape=None, dtype=np.float32):
+            self.low, self.high, self.shape, self.dtype = low, high, shape, dtype
+
+    class Tuple(Space):
+        def __init__(self, spaces_):
+            self.spaces = spaces_
+
+    gym.Env, gym.Space = type("Env", (), {}), Space
+    spaces.Discrete, spaces.Box, spaces.Tuple = Discrete, Box, Tuple
+    reg.EnvSpec = type("EnvSpec", (), {})
+    gym.spaces, gym.envs, envs.registration = spaces, envs, reg
+    sys.modules.update({"gym": gym, "gym.spaces": spaces, "gym.envs": envs, "gym.envs.registration": reg})
+
+
 @contextlib.contextmanager
 def ref_cwd(tmp_path):
     """chdir into tmp_path with a data -> reference/data symlink."""
