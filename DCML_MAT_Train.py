@@ -22,6 +22,7 @@ import torch
 
 from mat_dcml_amd.config import get_config, parse_args
 from mat_dcml_amd.parallel.comm import init_from_env
+from mat_dcml_amd.utils.checkpoint import make_run_dir
 from mat_dcml_amd.runner.dcml_runner import DCMLRunner as Runner
 
 DEFAULT_ARGV = ["--n_rollout_threads", "8", "--num_env_steps", "1000000", "--save_interval", "50",
@@ -31,21 +32,6 @@ DEFAULT_ARGV = ["--n_rollout_threads", "8", "--num_env_steps", "1000000", "--sav
 
 SUPPORTED = ("mat", "mat_dec", "mat_encoder", "mat_decoder", "mat_gru", "momat", "dmomat", "happo", "rmappo", "ppo",
              "ippo", "hatrpo", "random")
-
-
-def make_run_dir(all_args, comm):
-    root = Path(all_args.results_dir or os.path.join(os.getcwd(), "results"))
-    run_dir = root / all_args.env_name / all_args.scenario / all_args.algorithm_name / all_args.experiment_name
-    name = None
-    if comm.is_main:
-        run_dir.mkdir(parents=True, exist_ok=True)
-        nums = [int(p.name[3:]) for p in run_dir.iterdir() if p.name.startswith("run") and p.name[3:].isdigit()]
-        name = f"run{max(nums) + 1}" if nums and not all_args.resume else (f"run{max(nums)}" if nums else "run1")
-    name = comm.all_gather_object(name)[0]
-    run_dir = run_dir / name
-    if comm.is_main:
-        run_dir.mkdir(parents=True, exist_ok=True)
-    return run_dir
 
 
 def main(args):

@@ -29,7 +29,7 @@ DIRS = ((0.0, 1.0), (0.0, -1.0), (1.0, 0.0), (-1.0, 0.0))
 
 class SyntheticSMACEnv:
     def __init__(self, n_envs: int, map_name: str = "27m_vs_30m", device="cpu", seed: int = 1,
-                 reward_scale_rate: float = 20.0, state_per_agent: bool = True):
+                 reward_scale_rate: float = 20.0, state_per_agent: bool = True, random_agent_order: bool = False):
         self.spec: SMACSpec = get_map(map_name)
         s = self.spec
         self.E, self.A, self.N = int(n_envs), s.n_agents, s.n_enemies
@@ -52,6 +52,10 @@ class SyntheticSMACEnv:
         self.others = torch.stack([torch.cat([idx[:i], idx[i + 1:]]) for i in range(A)]) if A > 1 else \
             torch.zeros(1, 0, dtype=torch.long, device=dev)
         self.agent_id = torch.eye(A, device=dev)
+        # Random_StarCraft2_Env.py:386-389: a fresh agent permutation per episode; outputs are permuted rows,
+        # incoming actions are mapped back with the inverse (agent_recovery, :483-484)
+        self.random_agent_order = bool(random_agent_order)
+        self.perm = torch.arange(A, device=dev).expand(E, A).clone()
 
     # ------------------------------------------------------------------------------------- spaces
     @property
@@ -85,16 +89,31 @@ class SyntheticSMACEnv:
         self.ehp = torch.where(mm, torch.ones_like(self.ehp), self.ehp)
         self.t = torch.where(m, torch.zeros_like(self.t), self.t)
         self.last = torch.where(mm, torch.zeros_like(self.last), self.last)
+        if self.random_agent_order:
+            p = torch.argsort(self._rand(E, A), dim=1)
+            self.perm = torch.where(mm, p, self.perm)
+
+    def _rows(self, x, perm):
+        if not self.random_agent_order:
+            return x
+        idx = perm.view(*perm.shape, *([1] * (x.dim() - 2))).expand(*perm.shape, *x.shape[2:])
+        return torch.gather(x, 1, idx)
+
+    def _observe_perm(self):
+        return tuple(self._rows(x, self.perm) for x in self._observe())
 
     def reset(self):
         self._reset_where(torch.ones(self.E, dtype=torch.bool, device=self.device))
-        return self._observe()
+        return self._observe_perm()
 
     def step(self, actions: torch.Tensor):
         """actions (E, A[, 1]) ints.  Returns obs, state, reward (E, A, 1), dones (E, A), info dict of (E,)
         tensors, available actions."""
         E, A, N = self.E, self.A, self.N
         a = actions.reshape(E, A).long()
+        if self.random_agent_order:   # row j of the policy output belongs to agent perm[j]
+            a = torch.empty_like(a).scatter_(1, self.perm, a)
+        old_perm = self.perm
         alive = self.ahp > 0
         a = torch.where(alive, a, torch.zeros_like(a))
         # moves
@@ -140,8 +159,8 @@ class SyntheticSMACEnv:
                 "battles_game": self.battles_game.clone(), "dead_allies": (self.ahp <= 0).float().sum(1),
                 "dead_enemies": (self.ehp <= 0).float().sum(1)}
         self._reset_where(done)      # unconditional: no host sync on done.any()
-        obs, state, ava = self._observe()
-        return obs, state, reward.view(E, 1, 1).expand(E, A, 1), dones, info, ava
+        obs, state, ava = self._observe_perm()
+        return obs, state, reward.view(E, 1, 1).expand(E, A, 1), self._rows(dones, old_perm), info, ava
 
     # ------------------------------------------------------------------------------------- features
     def _observe(self):
@@ -175,6 +194,7 @@ class SyntheticSMACEnv:
                                      self.ahp[:, oth]], -1), tb_a[:, oth], last1h[:, oth]], -1) * vis_a.unsqueeze(-1)
         own = torch.cat([torch.stack([self.ahp, self.apos[..., 0] / MAP_SIZE, self.apos[..., 1] / MAP_SIZE,
                                       torch.zeros_like(self.ahp), alive], -1), tb_a, last1h], -1)
+        own = own * alive.unsqueeze(-1)            # a dead unit observes nothing but its id (get_obs_agent)
         ids = self.agent_id.expand(E, A, A)
         obs = torch.cat([move, ef.reshape(E, A, -1), af.reshape(E, A, -1), own, ids], -1)
         # per-agent state: absolute positions added to every entity

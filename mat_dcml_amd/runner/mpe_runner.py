@@ -22,7 +22,7 @@ from .smac_runner import SMACRunner
 
 
 class MPERunner(SMACRunner):
-    def make_env(self, a, n_envs, seed, env_id_offset):
+    def make_env(self, a, n_envs, seed, env_id_offset, maps=None):
         return MPEVecEnv(a, n_envs, device=self.device, seed=seed * 1000 + env_id_offset)
 
     def warmup(self):

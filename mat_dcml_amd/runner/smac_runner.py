@@ -28,12 +28,18 @@ from ..utils.timers import PhaseTimers
 from .dcml_runner import DCMLRunner
 
 
-def make_smac_env(args, n_envs, device, seed, env_id_offset=0):
+def make_smac_env(args, n_envs, device, seed, env_id_offset=0, maps=None):
     backend = getattr(args, "smac_backend", "synthetic")
     if backend == "sc2":
         from ..envs.smac.adapter import make_sc2_vec_env
         return make_sc2_vec_env(args, n_envs, seed, device)
-    return SyntheticSMACEnv(n_envs, args.map_name, device=device, seed=seed * 1000 + env_id_offset)
+    rao = bool(getattr(args, "random_agent_order", False))
+    if maps:   # multi-map training (train_smac_multi.py): unified layout + task embedding
+        from ..envs.smac.multi import SyntheticSMACMultiEnv
+        return SyntheticSMACMultiEnv(maps, n_envs, device=device, seed=seed * 1000 + env_id_offset,
+                                     random_agent_order=rao)
+    return SyntheticSMACEnv(n_envs, args.map_name, device=device, seed=seed * 1000 + env_id_offset,
+                            random_agent_order=rao)
 
 
 class SMACRunner(DCMLRunner):
@@ -51,10 +57,11 @@ class SMACRunner(DCMLRunner):
         self.use_eval, self.eval_interval = a.use_eval, a.eval_interval
         self.train_stride, self.eval_stride = getattr(a, "train_stride", 1), 1
         E, rank = self.n_rollout_threads, self.comm.rank
-        self.envs = config.get("envs") or self.make_env(a, E, a.seed, rank * E)
+        self.envs = config.get("envs") or self.make_env(a, E, a.seed, rank * E, getattr(a, "train_maps", None))
         self.eval_envs = config.get("eval_envs")
         if self.eval_envs is None and self.use_eval:
-            self.eval_envs = self.make_env(a, self.n_eval_rollout_threads, a.seed + 7, rank)
+            self.eval_envs = self.make_env(a, self.n_eval_rollout_threads, a.seed + 7, rank,
+                                           getattr(a, "eval_maps", None) or getattr(a, "train_maps", None))
         self.num_agents = self.envs.n_agents
         obs_dim = self.envs.observation_space[0][0]
         share_dim = self.envs.share_observation_space[0][0]
@@ -79,8 +86,8 @@ class SMACRunner(DCMLRunner):
         self._done_stats = torch.zeros(4, device=self.device, dtype=torch.float64)   # n, Σreward, won, dead
         self._last_battles = torch.zeros(2, device=self.device)
 
-    def make_env(self, a, n_envs, seed, env_id_offset):
-        return make_smac_env(a, n_envs, self.device, seed, env_id_offset)
+    def make_env(self, a, n_envs, seed, env_id_offset, maps=None):
+        return make_smac_env(a, n_envs, self.device, seed, env_id_offset, maps)
 
     def warmup(self):
         obs, state, ava = self.envs.reset()

@@ -10,6 +10,7 @@ Loads always use ``weights_only=True``.
 from __future__ import annotations
 
 import os
+from pathlib import Path
 
 import torch
 
@@ -83,3 +84,20 @@ def load_trainer_state(path, policy, trainer):
     if trainer.value_normalizer is not None and "value_normalizer" in state:
         trainer.value_normalizer.load_state_dict(state["value_normalizer"])
     return state
+
+
+def make_run_dir(all_args, comm):
+    """``results/<env>/<scenario>/<algo>/<exp>/run{n}`` (reference ``DCML_MAT_Train.py:116-147``); rank 0 picks
+    the run number, every rank gets the same path."""
+    root = Path(all_args.results_dir or os.path.join(os.getcwd(), "results"))
+    run_dir = root / all_args.env_name / all_args.scenario / all_args.algorithm_name / all_args.experiment_name
+    name = None
+    if comm.is_main:
+        run_dir.mkdir(parents=True, exist_ok=True)
+        nums = [int(p.name[3:]) for p in run_dir.iterdir() if p.name.startswith("run") and p.name[3:].isdigit()]
+        name = f"run{max(nums) + 1}" if nums and not all_args.resume else (f"run{max(nums)}" if nums else "run1")
+    name = comm.all_gather_object(name)[0]
+    run_dir = run_dir / name
+    if comm.is_main:
+        run_dir.mkdir(parents=True, exist_ok=True)
+    return run_dir

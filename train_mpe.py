@@ -14,6 +14,7 @@ import torch
 
 from mat_dcml_amd.config import _MPE_FLAGS, get_config, parse_args
 from mat_dcml_amd.parallel.comm import init_from_env
+from mat_dcml_amd.utils.checkpoint import make_run_dir
 from mat_dcml_amd.runner.mpe_runner import MPERunner
 
 # train_mpe.sh (the reference passes --use_ReLU/--gain/--critic_lr for its baselines; MAT ignores them)
@@ -25,7 +26,6 @@ DEFAULT_ARGV = ["--env_name", "MPE", "--algorithm_name", "mat", "--experiment_na
 
 
 def main(argv):
-    from DCML_MAT_Train import make_run_dir
     all_args = parse_args(argv, get_config(), extra=_MPE_FLAGS)
     all_args.scenario = all_args.scenario_name
     comm = init_from_env(prefer_gpu=all_args.cuda)

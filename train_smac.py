@@ -14,6 +14,7 @@ import torch
 
 from mat_dcml_amd.config import _SMAC_FLAGS, get_config, parse_args
 from mat_dcml_amd.parallel.comm import init_from_env
+from mat_dcml_amd.utils.checkpoint import make_run_dir
 from mat_dcml_amd.runner.smac_runner import SMACRunner
 
 DEFAULT_ARGV = ["--env_name", "StarCraft2", "--algorithm_name", "mat", "--experiment_name", "single",
@@ -23,7 +24,6 @@ DEFAULT_ARGV = ["--env_name", "StarCraft2", "--algorithm_name", "mat", "--experi
 
 
 def main(argv):
-    from DCML_MAT_Train import make_run_dir
     all_args = parse_args(argv, get_config(), extra=_SMAC_FLAGS)
     all_args.scenario = all_args.map_name
     comm = init_from_env(prefer_gpu=all_args.cuda)
