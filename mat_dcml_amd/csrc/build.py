@@ -26,7 +26,8 @@ def _sources():
 
 def _hash(path):
     h = hashlib.sha256()
-    for p in [path] + sorted(os.path.join(HERE, f) for f in os.listdir(HERE) if f.endswith(".h")):
+    deps = sorted(os.path.join(HERE, f) for f in os.listdir(HERE) if f.endswith((".h", ".hip")))
+    for p in [path] + deps:
         with open(p, "rb") as f:
             h.update(f.read())
     h.update(" ".join(FLAGS).encode())

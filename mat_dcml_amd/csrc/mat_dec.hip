@@ -375,7 +375,7 @@ __device__ __forceinline__ void mat_dec_fwd_tile(const DecP& p, char* smem, int 
 }
 
 template <int NB, bool SAVE>
-__global__ __launch_bounds__(256, 1) void mat_dec_fwd(DecP p) {
+__global__ __launch_bounds__(256, WGPC) void MDL_V(mat_dec_fwd)(DecP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   FOR_TILES(p, (mat_dec_fwd_tile<NB, SAVE>(p, smem, s0, ns)));
 }
@@ -563,24 +563,24 @@ __device__ __forceinline__ void mat_dec_bwd_tile(const DecP& p, char* smem, int 
 }
 
 template <int NB>
-__global__ __launch_bounds__(256, 1) void mat_dec_bwd(DecP p) {
+__global__ __launch_bounds__(256, WGPC) void MDL_V(mat_dec_bwd)(DecP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   FOR_TILES(p, (mat_dec_bwd_tile<NB>(p, smem, s0, ns)));
 }
 
 
-MDL_API int mdl_mat_dec_fwd(const DecP* p, int NB, int save, hipStream_t st) {
+MDL_API int MDL_V(mdl_mat_dec_fwd)(const DecP* p, int NB, int save, hipStream_t st) {
   if (p->A > 8 || p->A < 1) return -1;
-  if (NB == 1) return save ? launch(mat_dec_fwd<1, true>, p, st) : launch(mat_dec_fwd<1, false>, p, st);
-  if (NB == 2) return save ? launch(mat_dec_fwd<2, true>, p, st) : launch(mat_dec_fwd<2, false>, p, st);
-  if (NB == 3) return save ? launch(mat_dec_fwd<3, true>, p, st) : launch(mat_dec_fwd<3, false>, p, st);
+  if (NB == 1) return save ? launch(MDL_V(mat_dec_fwd)<1, true>, p, st) : launch(MDL_V(mat_dec_fwd)<1, false>, p, st);
+  if (NB == 2) return save ? launch(MDL_V(mat_dec_fwd)<2, true>, p, st) : launch(MDL_V(mat_dec_fwd)<2, false>, p, st);
+  if (NB == 3) return save ? launch(MDL_V(mat_dec_fwd)<3, true>, p, st) : launch(MDL_V(mat_dec_fwd)<3, false>, p, st);
   return -3;
 }
 
-MDL_API int mdl_mat_dec_bwd(const DecP* p, int NB, hipStream_t st) {
+MDL_API int MDL_V(mdl_mat_dec_bwd)(const DecP* p, int NB, hipStream_t st) {
   if (p->A > 8 || p->A < 1) return -1;
-  if (NB == 1) return launch(mat_dec_bwd<1>, p, st);
-  if (NB == 2) return launch(mat_dec_bwd<2>, p, st);
-  if (NB == 3) return launch(mat_dec_bwd<3>, p, st);
+  if (NB == 1) return launch(MDL_V(mat_dec_bwd)<1>, p, st);
+  if (NB == 2) return launch(MDL_V(mat_dec_bwd)<2>, p, st);
+  if (NB == 3) return launch(MDL_V(mat_dec_bwd)<3>, p, st);
   return -3;
 }

@@ -15,8 +15,9 @@ __device__ __forceinline__ void mat_enc_fwd_tile(const EncP& p, char* smem, int 
     const int rt = c.wave + 4 * k;
     if (rt < c.NT) {
       RT pre, xh;
-      EmbRow er[4];
-      embed_pre(p, rt, pre, er, c);
+      float* ES = emb_scratch(c);
+      embed_stage(p, rt, ES, c);
+      embed_pre(p, rt, pre, ES, c);
       gelu_rt(pre);
       f32x4 mu, rs;
       ln_fwd(pre, xh, xr[k], mu, rs, p.ln0_g, p.ln0_b, lane);
@@ -68,7 +69,7 @@ __device__ __forceinline__ void mat_enc_fwd_tile(const EncP& p, char* smem, int 
 }
 
 template <int NB, bool SAVE>
-__global__ __launch_bounds__(256, 1) void mat_enc_fwd(EncP p) {
+__global__ __launch_bounds__(256, WGPC) void MDL_V(mat_enc_fwd)(EncP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   FOR_TILES(p, (mat_enc_fwd_tile<NB, SAVE>(p, smem, s0, ns)));
 }
@@ -157,6 +158,8 @@ __device__ __forceinline__ void mat_enc_bwd_tile(const EncP& p, char* smem, int 
     attn_self_bwd(B.m, B.ln[0], dx, p.sv[bb].xin, p.sv[bb].a1, p.sv[bb].lse1, false, cc);
   }
   // ---------------- embedding backward: x0 = LN0(GELU(W_e · LN_obs(obs) + b_e))
+  __syncthreads();   // QB becomes the per-wave LN_obs scratch
+#ifndef MDL_ABLATE_EMB
   {
     f32x4 dlg = {0, 0, 0, 0}, dlb = {0, 0, 0, 0}, dbe = {0, 0, 0, 0};
     float dwe[4][16], dlog[16], dlob[16];
@@ -172,8 +175,9 @@ __device__ __forceinline__ void mat_enc_bwd_tile(const EncP& p, char* smem, int 
       if (rt < c.NT) {
         const f32x4 vm = row_mask(rt, c.NR, lane);
         RT pre, e, xh, y, de;
-        EmbRow er[4];
-        embed_pre(p, rt, pre, er, c);
+        const float* ES = emb_scratch(c);
+        embed_stage(p, rt, emb_scratch(c), c);
+        embed_pre(p, rt, pre, ES, c);
         e = pre;
         gelu_rt(e);
         f32x4 mu, rs;
@@ -185,12 +189,20 @@ __device__ __forceinline__ void mat_enc_bwd_tile(const EncP& p, char* smem, int 
           for (int r = 0; r < 4; ++r) de.v[ct][r] *= gelu_erf_grad(pre.v[ct][r]) * vm[r];
         colsum_acc(de, dbe, vm);
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct)
+        for (int k4 = 0; k4 < 4; ++k4) {
+          if (4 * k4 < p.od) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
+            for (int r = 0; r < 4; ++r) {
+              const f32x4 oh = *(const f32x4*)(ES + (4 * g + r) * 32 + 4 * k4);
 #pragma unroll
-            for (int kk = 0; kk < 16; ++kk) dwe[ct][kk] += de.v[ct][r] * er[r].oh[kk];
+              for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) dwe[ct][4 * k4 + j] += de.v[ct][r] * oh[j];
+            }
+          }
+        }
         // d(LN_obs output)[row][kk] = sum_col dpre * W_e[col][kk]  -> LN_obs affine-parameter grads
+#ifndef MDL_ABLATE_DOH
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
 #pragma unroll
@@ -203,10 +215,12 @@ __device__ __forceinline__ void mat_enc_bwd_tile(const EncP& p, char* smem, int 
               t += __shfl_xor(t, 2, 64);
               t += __shfl_xor(t, 4, 64);
               t += __shfl_xor(t, 8, 64);
-              if (c16 == 0) { dlog[kk] += t * er[r].ohat[kk]; dlob[kk] += t; }
+              if (c16 == 0) { dlog[kk] += t * ES[(4 * g + r) * 32 + 16 + kk]; dlob[kk] += t; }
             }
           }
         }
+#endif
+        wave_lds_sync();   // scratch reads done before the next tile's staging overwrites it
       }
     }
     flush_ln(dlg, dlb, LNp{nullptr, nullptr, p.d_ln0_g, p.d_ln0_b}, c);
@@ -237,10 +251,11 @@ __device__ __forceinline__ void mat_enc_bwd_tile(const EncP& p, char* smem, int 
       }
     }
   }
+#endif
 }
 
 template <int NB>
-__global__ __launch_bounds__(256, 1) void mat_enc_bwd(EncP p) {
+__global__ __launch_bounds__(256, WGPC) void MDL_V(mat_enc_bwd)(EncP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   FOR_TILES(p, (mat_enc_bwd_tile<NB>(p, smem, s0, ns)));
 }
@@ -248,32 +263,35 @@ __global__ __launch_bounds__(256, 1) void mat_enc_bwd(EncP p) {
 
 
 // ============================================================================================== host API
-MDL_API int mdl_mat_train_geometry(int L) {
-  // sequences per tile: rows = SQ*L <= 4*MAXRT*16 = 192, LDS-padded rows a multiple of 32; returns SQ | NRP << 16
-  int SQ = 192 / L;
+MDL_API int MDL_V(mdl_mat_train_geometry)(int L) {
+  // sequences per tile: rows = SQ*L <= 4*MAXRT*16, LDS-padded rows a multiple of 32; returns SQ | NRP << 16
+  const int MAXROWS = 64 * MAXRT;
+  int SQ = MAXROWS / L;
   if (SQ < 1) return 0;
   int NRP = ((SQ * L + 31) / 32) * 32;
-  while (SQ > 1 && (NRP > 192 || mat_train_lds_bytes(NRP, SQ, L) > 160 * 1024)) {
+  if (NRP < 64) NRP = 64;   // QB doubles as the 4 x 2 KB LN_obs scratch of the embedding
+  while (SQ > 1 && (NRP > MAXROWS || mat_train_lds_bytes(NRP, SQ, L) > LDS_BUDGET)) {
     --SQ;
     NRP = ((SQ * L + 31) / 32) * 32;
+    if (NRP < 64) NRP = 64;
   }
-  if (mat_train_lds_bytes(NRP, SQ, L) > 160 * 1024 || (SQ * L + 15) / 16 > 4 * MAXRT) return 0;
+  if (mat_train_lds_bytes(NRP, SQ, L) > LDS_BUDGET || (SQ * L + 15) / 16 > 4 * MAXRT) return 0;
   return SQ | (NRP << 16);
 }
 
-MDL_API int mdl_mat_enc_fwd(const EncP* p, int NB, int save, hipStream_t st) {
+MDL_API int MDL_V(mdl_mat_enc_fwd)(const EncP* p, int NB, int save, hipStream_t st) {
   if (p->od > 16 || p->od < 1 || p->n_obj > 2) return -1;
-  if (NB == 1) return save ? launch(mat_enc_fwd<1, true>, p, st) : launch(mat_enc_fwd<1, false>, p, st);
-  if (NB == 2) return save ? launch(mat_enc_fwd<2, true>, p, st) : launch(mat_enc_fwd<2, false>, p, st);
-  if (NB == 3) return save ? launch(mat_enc_fwd<3, true>, p, st) : launch(mat_enc_fwd<3, false>, p, st);
+  if (NB == 1) return save ? launch(MDL_V(mat_enc_fwd)<1, true>, p, st) : launch(MDL_V(mat_enc_fwd)<1, false>, p, st);
+  if (NB == 2) return save ? launch(MDL_V(mat_enc_fwd)<2, true>, p, st) : launch(MDL_V(mat_enc_fwd)<2, false>, p, st);
+  if (NB == 3) return save ? launch(MDL_V(mat_enc_fwd)<3, true>, p, st) : launch(MDL_V(mat_enc_fwd)<3, false>, p, st);
   return -3;
 }
 
-MDL_API int mdl_mat_enc_bwd(const EncP* p, int NB, hipStream_t st) {
+MDL_API int MDL_V(mdl_mat_enc_bwd)(const EncP* p, int NB, hipStream_t st) {
   if (p->od > 16 || p->od < 1 || p->n_obj > 2) return -1;
-  if (NB == 1) return launch(mat_enc_bwd<1>, p, st);
-  if (NB == 2) return launch(mat_enc_bwd<2>, p, st);
-  if (NB == 3) return launch(mat_enc_bwd<3>, p, st);
+  if (NB == 1) return launch(MDL_V(mat_enc_bwd)<1>, p, st);
+  if (NB == 2) return launch(MDL_V(mat_enc_bwd)<2>, p, st);
+  if (NB == 3) return launch(MDL_V(mat_enc_bwd)<3>, p, st);
   return -3;
 }
 

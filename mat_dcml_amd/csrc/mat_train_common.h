@@ -23,7 +23,22 @@ using namespace mdl;
 
 namespace {
 
-constexpr int MAXRT = 3;  // row tiles per wave (NT <= 12)
+// Variant builds (mat_*_o2.hip) re-include the kernels with other tiling constants and a name suffix.
+#ifndef MDL_VARIANT_SUFFIX
+#define MDL_VARIANT_SUFFIX
+#endif
+#define MDL_CAT2(a, b) a##b
+#define MDL_CAT(a, b) MDL_CAT2(a, b)
+#define MDL_V(name) MDL_CAT(name, MDL_VARIANT_SUFFIX)
+#ifndef MDL_MAXRT
+#define MDL_MAXRT 3
+#endif
+#ifndef MDL_WGPC
+#define MDL_WGPC 1   // resident workgroups per CU the kernels are sized for (LDS budget, register cap, grid)
+#endif
+constexpr int MAXRT = MDL_MAXRT;  // row tiles per wave (NT <= 4 * MAXRT)
+constexpr int WGPC = MDL_WGPC;
+constexpr int LDS_BUDGET = 160 * 1024 / WGPC;
 
 struct Mat { const bf16_t* fw; const bf16_t* bw; const float* b; float* dW; float* db; };
 struct LNp { const float* g; const float* b; float* dg; float* db; };
@@ -536,45 +551,72 @@ __device__ __forceinline__ void mlp_fwd(const Mat& m1, const Mat& m2, const LNp&
 }
 
 // obs embedding (VALU; obs_dim <= 16): x0 = LN0(GELU(W_e · LN_obs(obs) + b_e))  — ma_transformer.py:133-134,151
-struct EmbRow { float oh[16]; float ohat[16]; };
+// The LN_obs rows of the wave's current tile are staged in a per-wave LDS scratch (16 rows x [oh(16) | ohat(16)]
+// f32 = 2 KB, aliasing the QB buffer, which is free before the first / after the last attention) instead of
+// registers: 4 rows x 32 floats per lane kept the encoder backward above 256 VGPRs (scratch spills).
+constexpr int ES_FLOATS = 16 * 32;
+__device__ __forceinline__ float* emb_scratch(const Ctx& c) { return (float*)c.QB + c.wave * ES_FLOATS; }
 
-__device__ __forceinline__ void obs_ln_row(const EncP& p, int tok, bool valid, EmbRow& er) {
-  const int od = p.od;
-  float o[16];
-  float mean = 0.f;
+// lanes 0..15 each normalise one row of the tile (obs_dim <= 16) into the scratch; rows >= NR are zero
+__device__ __forceinline__ void embed_stage(const EncP& p, int rt, float* ES, const Ctx& c) {
+  const int lane = c.lane, od = p.od;
+  if (lane < 16) {
+    const int row = rt * 16 + lane;
+    const bool valid = row < c.NR;
+    const size_t tok = (size_t)(c.tok0 + (valid ? row : 0));
+    float o[16];
+    float mean = 0.f;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) { o[k] = (valid && k < od) ? p.obs[(size_t)tok * od + k] : 0.f; mean += o[k]; }
-  mean /= (float)od;
-  float var = 0.f;
+    for (int k = 0; k < 16; ++k) { o[k] = (valid && k < od) ? p.obs[tok * od + k] : 0.f; mean += o[k]; }
+    mean /= (float)od;
+    float var = 0.f;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) if (k < od) { const float d = o[k] - mean; var += d * d; }
-  const float rstd = rsqrtf(var / (float)od + 1e-5f);
+    for (int k = 0; k < 16; ++k) if (k < od) { const float d = o[k] - mean; var += d * d; }
+    const float rstd = rsqrtf(var / (float)od + 1e-5f);
+    float* e = ES + lane * 32;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    er.ohat[k] = k < od ? (o[k] - mean) * rstd : 0.f;
-    er.oh[k] = k < od ? er.ohat[k] * p.lno_g[k] + p.lno_b[k] : 0.f;
+    for (int k = 0; k < 16; k += 4) {
+      f32x4 oh, hat;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int kk = k + j;
+        hat[j] = (valid && kk < od) ? (o[kk] - mean) * rstd : 0.f;
+        oh[j] = (valid && kk < od) ? hat[j] * p.lno_g[kk] + p.lno_b[kk] : 0.f;
+      }
+      *(f32x4*)(e + k) = oh;
+      *(f32x4*)(e + 16 + k) = hat;
+    }
   }
+  wave_lds_sync();
 }
 
-__device__ __forceinline__ void embed_pre(const EncP& p, int rt, RT& pre, EmbRow* er, const Ctx& c) {
+// pre = W_e · LN_obs(obs) + b_e for the tile (LN_obs rows read back from the scratch, broadcast per lane group)
+__device__ __forceinline__ void embed_pre(const EncP& p, int rt, RT& pre, const float* ES, const Ctx& c) {
   const int g = c.lane >> 4, c16 = c.lane & 15;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int row = rt * 16 + 4 * g + r;
-    obs_ln_row(p, c.tok0 + row, row < c.NR, er[r]);
-  }
+  const int nk = (p.od + 3) >> 2;
 #pragma unroll
   for (int ct = 0; ct < 4; ++ct) {
     const int col = 16 * ct + c16;
-    float w[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) w[k] = k < p.od ? p.we[col * p.od + k] : 0.f;
+    for (int r = 0; r < 4; ++r) pre.v[ct][r] = p.be[col];
+  }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float s = p.be[col];
+  for (int k4 = 0; k4 < 4; ++k4) {
+    if (k4 < nk) {
+      f32x4 x[4];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) s += w[k] * er[r].oh[k];
-      pre.v[ct][r] = s;
+      for (int r = 0; r < 4; ++r) x[r] = *(const f32x4*)(ES + (4 * g + r) * 32 + 4 * k4);
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        const int col = 16 * ct + c16;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int k = 4 * k4 + j;
+          const float w = k < p.od ? p.we[col * p.od + k] : 0.f;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) pre.v[ct][r] += w * x[r][j];
+        }
+      }
     }
   }
 }
@@ -795,12 +837,13 @@ static int n_cus() {
 
 template <typename K, typename PT>
 static int launch(K kern, const PT* p, hipStream_t st) {
+  if (p->SQ <= 0 || p->NRP <= 0 || (p->SQ * p->L + 15) / 16 > 4 * MAXRT) return -4;   // geometry not valid here
   const size_t lds = mat_train_lds_bytes(p->NRP, p->SQ, p->L);
-  if (lds > 160 * 1024) return -2;
+  if (lds > LDS_BUDGET) return -2;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return (int)e;
   const int tiles = (p->Bs + p->SQ - 1) / p->SQ;
-  const int grid = tiles < n_cus() ? tiles : n_cus();
+  const int grid = tiles < n_cus() * WGPC ? tiles : n_cus() * WGPC;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, *p);
   MDL_CHECK_LAUNCH();
   return 0;

@@ -11,6 +11,7 @@
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -55,18 +56,28 @@ class DecP(ctypes.Structure):
                [("g_delta", ctypes.c_longlong), ("g_stride", ctypes.c_longlong), ("g_copies", ctypes.c_int)]
 
 
-sig("mdl_mat_train_geometry", ctypes.c_int)
+# builds of the training kernels, by name suffix (csrc/mat_train_common.h MDL_VARIANT_SUFFIX).  Only the base build
+# (three 16-row tiles per wave, one workgroup per CU, L <= 192) ships: an occupancy-2 build (one tile per wave, two
+# workgroups per CU) measured 1.6x / 2.9x slower backward kernels (register spills, 5x more weight-gradient atomics;
+# profiles/r1_occupancy_ab.md).
+VARIANTS = ("",)
+for _v in VARIANTS:
+    sig("mdl_mat_train_geometry" + _v, ctypes.c_int)
+    sig("mdl_mat_enc_fwd" + _v, ctypes.POINTER(EncP), ctypes.c_int, ctypes.c_int, VP)
+    sig("mdl_mat_enc_bwd" + _v, ctypes.POINTER(EncP), ctypes.c_int, VP)
+    sig("mdl_mat_dec_fwd" + _v, ctypes.POINTER(DecP), ctypes.c_int, ctypes.c_int, VP)
+    sig("mdl_mat_dec_bwd" + _v, ctypes.POINTER(DecP), ctypes.c_int, VP)
 sig("mdl_grad_reduce", VP, VP, ctypes.c_int, ctypes.c_longlong, ctypes.c_int, VP)
-sig("mdl_mat_enc_fwd", ctypes.POINTER(EncP), ctypes.c_int, ctypes.c_int, VP)
-sig("mdl_mat_enc_bwd", ctypes.POINTER(EncP), ctypes.c_int, VP)
-sig("mdl_mat_dec_fwd", ctypes.POINTER(DecP), ctypes.c_int, ctypes.c_int, VP)
-sig("mdl_mat_dec_bwd", ctypes.POINTER(DecP), ctypes.c_int, VP)
 sig("mdl_pack_weights", VP, ctypes.c_int, VP)
 
 
 def geometry(L):
-    v = lib().mdl_mat_train_geometry(L)
-    return v & 0xFFFF, v >> 16
+    """(SQ sequences per tile, NRP padded rows, kernel-variant suffix) — the first variant whose tiling fits L."""
+    for sfx in VARIANTS:
+        v = getattr(lib(), "mdl_mat_train_geometry" + sfx)(L)
+        if v:
+            return v & 0xFFFF, v >> 16, sfx
+    return 0, 0, ""
 
 
 def _ptr(t):
@@ -203,7 +214,7 @@ class EncoderFused:
         self._build()
         B, L, od = obs.shape
         dev = obs.device
-        SQ, NRP = geometry(L)
+        SQ, NRP, sfx = geometry(L)
         n_tok = B * L
         obs = obs.float().contiguous()
         rep = torch.empty(B, L, 64, device=dev)
@@ -219,7 +230,7 @@ class EncoderFused:
                 saves += [t, lse]
                 p.sv[bi] = Sv(t[0].data_ptr(), t[1].data_ptr(), lse.data_ptr(), t[2].data_ptr(), None, None, None,
                               t[3].data_ptr())
-        check(lib().mdl_mat_enc_fwd(ctypes.byref(p), m.n_block, int(save), kernels._stream()), "mat_enc_fwd")
+        check(getattr(lib(), "mdl_mat_enc_fwd" + sfx)(ctypes.byref(p), m.n_block, int(save), kernels._stream()), "mat_enc_fwd")
         self.ctx = (obs, rep, v, saves, [Sv.from_buffer_copy(p.sv[i]) for i in range(m.n_block)])
         return v, rep
 
@@ -231,7 +242,7 @@ class EncoderFused:
         drep = drep.float().contiguous()
         dv = dv.float().contiguous()
         B, L, od = obs.shape
-        SQ, NRP = geometry(L)
+        SQ, NRP, sfx = geometry(L)
         p.Bs, p.L, p.od, p.SQ, p.NRP, p.n_obj = B, L, od, SQ, NRP, m.n_objective
         p.obs, p.rep, p.v, p.drep, p.dv = obs.data_ptr(), rep.data_ptr(), v.data_ptr(), drep.data_ptr(), dv.data_ptr()
         for i, s in enumerate(svs):
@@ -239,7 +250,7 @@ class EncoderFused:
         p.g_delta, p.g_stride, p.g_copies = m._mdl_gws if getattr(m, "_mdl_gws_active", False) else (0, 0, 0)
         if p.g_copies:
             check_grad_ptrs(p, m._mdl_gws_buf[1])
-        check(lib().mdl_mat_enc_bwd(ctypes.byref(p), m.n_block, kernels._stream()), "mat_enc_bwd")
+        check(getattr(lib(), "mdl_mat_enc_bwd" + sfx)(ctypes.byref(p), m.n_block, kernels._stream()), "mat_enc_bwd")
         b = m.encoder.head[3].bias
         if b.grad is not None:
             b.grad.add_(dv.reshape(-1, dv.shape[-1]).sum(0))
@@ -288,9 +299,10 @@ class DecoderFused:
         return L if m.action_type == "Discrete" else L + m.semi_index
 
     def _geom(self, B, L):
-        SQ, NRP = geometry(L)
+        SQ, NRP, sfx = geometry(L)
         p = self.p
         p.Bs, p.L, p.A, p.SQ, p.NRP, p.n_disc = B, L, self.model.action_dim, SQ, NRP, self._n_disc(L)
+        return sfx
 
     def forward(self, rep, actions, ava=None, save=True):
         m = self.model
@@ -307,7 +319,7 @@ class DecoderFused:
         ava_c = ava.float().contiguous() if ava is not None else None
         logp = torch.empty(B, L, 1, device=dev)
         ent = torch.empty(B, L, 1, device=dev)
-        self._geom(B, L)
+        sfx = self._geom(B, L)
         p = self.p
         p.act, p.ava, p.rep, p.logp, p.ent = act.data_ptr(), _ptr(ava_c), rep.data_ptr(), logp.data_ptr(), ent.data_ptr()
         saves = []
@@ -321,7 +333,7 @@ class DecoderFused:
             head = torch.empty(n_tok, 64, device=dev, dtype=torch.bfloat16)
             saves.append(head)
             p.sv_head = head.data_ptr()
-        check(lib().mdl_mat_dec_fwd(ctypes.byref(p), m.n_block, int(save), kernels._stream()), "mat_dec_fwd")
+        check(getattr(lib(), "mdl_mat_dec_fwd" + sfx)(ctypes.byref(p), m.n_block, int(save), kernels._stream()), "mat_dec_fwd")
         self.ctx = (rep, act, ava_c, logp, ent, saves, [Sv.from_buffer_copy(p.sv[i]) for i in range(m.n_block)],
                     p.sv_head)
         return logp, ent
@@ -331,7 +343,7 @@ class DecoderFused:
         rep, act, ava_c, logp, ent, saves, svs, head = self.ctx
         self._build()
         B, L = act.shape
-        self._geom(B, L)
+        sfx = self._geom(B, L)
         p = self.p
         dlogp = dlogp.reshape(-1).float().contiguous()
         dent = dent.reshape(-1).float().contiguous()
@@ -343,7 +355,7 @@ class DecoderFused:
         p.g_delta, p.g_stride, p.g_copies = m._mdl_gws if getattr(m, "_mdl_gws_active", False) else (0, 0, 0)
         if p.g_copies:
             check_grad_ptrs(p, m._mdl_gws_buf[1])
-        check(lib().mdl_mat_dec_bwd(ctypes.byref(p), m.n_block, kernels._stream()), "mat_dec_bwd")
+        check(getattr(lib(), "mdl_mat_dec_bwd" + sfx)(ctypes.byref(p), m.n_block, kernels._stream()), "mat_dec_bwd")
         return drep
 
 
