@@ -10,6 +10,7 @@ and keyed by ``model._mdl_version``, bumped by the trainer after every update).
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -47,6 +48,12 @@ def supports(model, L=None) -> bool:
         return False
     L = L or model.n_agent
     return lib().mdl_mat_decode_geometry(model.n_block, L, 1) > 0
+
+
+# envs per decode workgroup cap (kernel maximum 16).  The decode is latency bound (one dependent chain of ~20
+# barrier-separated phases per agent), so spreading envs over more CUs only shortens the attention phases:
+# 256 envs x 33 agents: 690 us at 16 envs per workgroup, 642 us at 1 (tests/bench_decode.py)
+_EPW_CAP = int(os.environ.get("MAT_DCML_DECODE_EPW", "1"))
 
 
 def bump_version(model):
@@ -105,7 +112,7 @@ def decode(model, rep, ava=None, deterministic=False, stride=1, rand=None):
     ava_c = ava.float().contiguous() if ava is not None else None
     out_a = torch.empty(B, L, device=dev)
     out_lp = torch.empty(B, L, device=dev)
-    geo = lib().mdl_mat_decode_geometry(model.n_block, L, B)
+    geo = lib().mdl_mat_decode_geometry(model.n_block, L, min(B, _EPW_CAP))
     epw, rmax = geo & 0xFF, geo >> 8
     if epw <= 0:
         raise RuntimeError(f"mat_decode: L={L} does not fit in LDS")
