@@ -44,17 +44,84 @@ enum Purpose : uint32_t {
   P_DONE = 8, P_SHANNON = 9, P_POLICY = 16
 };
 
+// ------------------------------------------------------------------------------------------ cross-lane (VALU)
+// __shfl_xor compiles to ds_bpermute_b32: an LDS-pipe round trip per step.  These use DPP (within 16-lane rows)
+// and v_permlane16/32_swap (across rows) instead: plain VALU ops, no lgkmcnt wait.  Every lane of a group ends
+// with bit-identical results (each step adds the same two operands in the same order).
+constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_ROW_MIRROR = 0x140, DPP_ROW_HALF_MIRROR = 0x141, DPP_ROW_ROR8 = 0x128;
+template <int CTRL>
+__device__ __forceinline__ float dppf(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+// v_permlane16/32_swap of a register with (an opaque copy of) itself: r[0] = the even rows / low half of x
+// everywhere, r[1] = the odd rows / high half.  (With the SAME value for both operands hipcc folds r[1] into
+// r[0], so the copy is hidden behind an empty asm.)
+__device__ __forceinline__ void swap16(float x, float& even, float& odd) {
+  unsigned a = __builtin_bit_cast(unsigned, x), b = a;
+  asm volatile("" : "+v"(b));
+  const auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+  even = __builtin_bit_cast(float, (unsigned)r[0]);
+  odd = __builtin_bit_cast(float, (unsigned)r[1]);
+}
+__device__ __forceinline__ void swap32(float x, float& lo, float& hi) {
+  unsigned a = __builtin_bit_cast(unsigned, x), b = a;
+  asm volatile("" : "+v"(b));
+  const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+  lo = __builtin_bit_cast(float, (unsigned)r[0]);
+  hi = __builtin_bit_cast(float, (unsigned)r[1]);
+}
+// value of lane ^ 16 / lane ^ 32
+__device__ __forceinline__ float xor16_partner(float x) {
+  float e, o;
+  swap16(x, e, o);
+  return ((threadIdx.x >> 4) & 1) ? e : o;
+}
+__device__ __forceinline__ float xor32_partner(float x) {
+  float lo, hi;
+  swap32(x, lo, hi);
+  return ((threadIdx.x >> 5) & 1) ? lo : hi;
+}
+// sum / max over aligned groups of N lanes, N in {2, 4, 8, 16, 32, 64}
+template <int N>
+__device__ __forceinline__ float group_sum(float x) {
+  x += dppf<DPP_XOR1>(x);
+  if (N > 2) x += dppf<DPP_XOR2>(x);
+  if (N > 4) x += dppf<DPP_ROW_HALF_MIRROR>(x);
+  if (N > 8) x += dppf<DPP_ROW_MIRROR>(x);
+  if (N > 16) {
+    float e, o;
+    swap16(x, e, o);
+    x = e + o;
+  }
+  if (N > 32) {
+    float lo, hi;
+    swap32(x, lo, hi);
+    x = lo + hi;
+  }
+  return x;
+}
+template <int N>
+__device__ __forceinline__ float group_max(float x) {
+  x = fmaxf(x, dppf<DPP_XOR1>(x));
+  if (N > 2) x = fmaxf(x, dppf<DPP_XOR2>(x));
+  if (N > 4) x = fmaxf(x, dppf<DPP_ROW_HALF_MIRROR>(x));
+  if (N > 8) x = fmaxf(x, dppf<DPP_ROW_MIRROR>(x));
+  if (N > 16) x = fmaxf(x, xor16_partner(x));
+  if (N > 32) x = fmaxf(x, xor32_partner(x));
+  return x;
+}
+// sum over the lanes sharing lane & 15 (the 4 rows of 16): lane ^ 16, lane ^ 32 partners
+__device__ __forceinline__ float cross_row_sum(float x) {
+  float a, b;
+  swap16(x, a, b);
+  x = a + b;
+  swap32(x, a, b);
+  return a + b;
+}
+
 // ------------------------------------------------------------------------------------------ wave64 reductions
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
+__device__ __forceinline__ float wave_sum(float v) { return group_sum<64>(v); }
+__device__ __forceinline__ float wave_max(float v) { return group_max<64>(v); }
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

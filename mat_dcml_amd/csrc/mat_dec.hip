@@ -499,15 +499,13 @@ __device__ __forceinline__ void mat_dec_bwd_tile(const DecP& p, char* smem, int 
       if (a < p.A) {
         flush_cols(dwh2[a], c.g(p.d_wh2 ? p.d_wh2 + a * 64 : nullptr), lane);
         float x = dbh2[a];
-        x += __shfl_xor(x, 16, 64);
-        x += __shfl_xor(x, 32, 64);
+        x = cross_row_sum(x);
         if (lane == 0 && p.d_bh2) atomicAdd(c.g(p.d_bh2) + a, x);
       }
     }
     {
       float x = dls;
-      x += __shfl_xor(x, 16, 64);
-      x += __shfl_xor(x, 32, 64);
+      x = cross_row_sum(x);
       if (lane == 0 && p.d_log_std) atomicAdd(c.g(p.d_log_std) + (p.A - 1), x);
     }
     __syncthreads();

@@ -76,14 +76,12 @@ __device__ __forceinline__ void afrag_ln(const float* S, const float* gam, const
   float s = 0.f;
 #pragma unroll
   for (int j = 0; j < 16; ++j) s += v[j];
-  s += __shfl_xor(s, 16, 64);
-  s += __shfl_xor(s, 32, 64);
+  s = cross_row_sum(s);
   const float mean = s * (1.f / 64.f);
   float q = 0.f;
 #pragma unroll
   for (int j = 0; j < 16; ++j) { const float d = v[j] - mean; q += d * d; }
-  q += __shfl_xor(q, 16, 64);
-  q += __shfl_xor(q, 32, 64);
+  q = cross_row_sum(q);
   const float rstd = rsqrtf(q * (1.f / 64.f) + 1e-5f);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -168,16 +166,14 @@ __device__ __forceinline__ void attention_phase_t(const bf16_t* KV, const float*
       pr[j] = sc;
       mx = fmaxf(mx, sc);
     }
-#pragma unroll
-    for (int x = 1; x < lpi; x <<= 1) mx = fmaxf(mx, __shfl_xor(mx, x, 64));
+    mx = group_max<lpi>(mx);
     float sum = 0.f;
     for (int j = u; j <= i; j += lpi) {
       const float pj = __expf(pr[j] - mx);
       pr[j] = pj;
       sum += pj;
     }
-#pragma unroll
-    for (int x = 1; x < lpi; x <<= 1) sum += __shfl_xor(sum, x, 64);
+    sum = group_sum<lpi>(sum);
     __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // PR written by this item's lanes (same wave)
     float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
     const int lc = 4 * h + (dg >> 1), off = 4 * (dg & 1);
@@ -190,10 +186,13 @@ __device__ __forceinline__ void attention_phase_t(const bf16_t* KV, const float*
       acc2 += pj * __uint_as_float(v4.y << 16);
       acc3 += pj * __uint_as_float(v4.y & 0xFFFF0000u);
     }
-#pragma unroll
-    for (int x = 8; x < lpi; x <<= 1) {
-      acc0 += __shfl_xor(acc0, x, 64); acc1 += __shfl_xor(acc1, x, 64);
-      acc2 += __shfl_xor(acc2, x, 64); acc3 += __shfl_xor(acc3, x, 64);
+    if (lpi > 8) {   // reduce over the key groups kg: lane ^ 8 (DPP row_ror:8), then lane ^ 16
+      acc0 += dppf<DPP_ROW_ROR8>(acc0); acc1 += dppf<DPP_ROW_ROR8>(acc1);
+      acc2 += dppf<DPP_ROW_ROR8>(acc2); acc3 += dppf<DPP_ROW_ROR8>(acc3);
+    }
+    if (lpi > 16) {
+      acc0 += xor16_partner(acc0); acc1 += xor16_partner(acc1);
+      acc2 += xor16_partner(acc2); acc3 += xor16_partner(acc3);
     }
     if (kg == 0) {
       const float inv = 1.f / sum;
@@ -221,12 +220,12 @@ __device__ __forceinline__ void head_phase(const DecParams& p, const float* H1, 
 #pragma unroll
   for (int k = 0; k < 4; ++k) v[k] = H1[t * SP + 4 * q + k];
   float sm = v[0] + v[1] + v[2] + v[3];
-  sm += __shfl_xor(sm, 1, 64); sm += __shfl_xor(sm, 2, 64); sm += __shfl_xor(sm, 4, 64); sm += __shfl_xor(sm, 8, 64);
+  sm = group_sum<16>(sm);
   const float mean = sm * (1.f / 64.f);
   float sq = 0.f;
 #pragma unroll
   for (int k = 0; k < 4; ++k) { const float d = v[k] - mean; sq += d * d; }
-  sq += __shfl_xor(sq, 1, 64); sq += __shfl_xor(sq, 2, 64); sq += __shfl_xor(sq, 4, 64); sq += __shfl_xor(sq, 8, 64);
+  sq = group_sum<16>(sq);
   const float rstd = rsqrtf(sq * (1.f / 64.f) + 1e-5f);
   float hn[4];
 #pragma unroll
@@ -234,8 +233,7 @@ __device__ __forceinline__ void head_phase(const DecParams& p, const float* H1, 
   for (int a = 0; a < AD; ++a) {
     const float* w = p.wh2 + a * 64 + 4 * q;
     float part = w[0] * hn[0] + w[1] * hn[1] + w[2] * hn[2] + w[3] * hn[3];
-    part += __shfl_xor(part, 1, 64); part += __shfl_xor(part, 2, 64);
-    part += __shfl_xor(part, 4, 64); part += __shfl_xor(part, 8, 64);
+    part = group_sum<16>(part);
     if (q == 0) LG[t * SP + a] = part + p.bh2[a];
   }
   if (q != 0 || i < 0 || i < s || i >= e) return;

@@ -211,10 +211,7 @@ __device__ __forceinline__ void mat_enc_bwd_tile(const EncP& p, char* smem, int 
               float t = 0.f;
 #pragma unroll
               for (int ct = 0; ct < 4; ++ct) t += de.v[ct][r] * p.we[(16 * ct + c16) * p.od + kk];
-              t += __shfl_xor(t, 1, 64);
-              t += __shfl_xor(t, 2, 64);
-              t += __shfl_xor(t, 4, 64);
-              t += __shfl_xor(t, 8, 64);
+              t = group_sum<16>(t);
               if (c16 == 0) { dlog[kk] += t * ES[(4 * g + r) * 32 + 16 + kk]; dlob[kk] += t; }
             }
           }
@@ -231,8 +228,7 @@ __device__ __forceinline__ void mat_enc_bwd_tile(const EncP& p, char* smem, int 
       for (int kk = 0; kk < 16; ++kk) {
         if (kk < p.od) {
           float x = dwe[ct][kk];
-          x += __shfl_xor(x, 16, 64);
-          x += __shfl_xor(x, 32, 64);
+          x = cross_row_sum(x);
           if (g == 0 && p.d_we) atomicAdd(c.g(p.d_we) + (16 * ct + c16) * p.od + kk, x);
         }
       }
@@ -240,10 +236,8 @@ __device__ __forceinline__ void mat_enc_bwd_tile(const EncP& p, char* smem, int 
     for (int kk = 0; kk < 16; ++kk) {
       if (kk < p.od) {
         float a = dlog[kk], b2 = dlob[kk];
-        a += __shfl_xor(a, 16, 64);
-        a += __shfl_xor(a, 32, 64);
-        b2 += __shfl_xor(b2, 16, 64);
-        b2 += __shfl_xor(b2, 32, 64);
+        a = cross_row_sum(a);
+        b2 = cross_row_sum(b2);
         if (lane == 0) {
           if (p.d_lno_g) atomicAdd(c.g(p.d_lno_g) + kk, a);
           if (p.d_lno_b) atomicAdd(c.g(p.d_lno_b) + kk, b2);

@@ -221,7 +221,8 @@ __device__ __forceinline__ void attn_fwd(const bf16_t* Q, const bf16_t* K, const
     }
 #pragma unroll
     for (int x = 16; x <= 32; x <<= 1) {
-      const float om = __shfl_xor(m, x, 64), ol = __shfl_xor(l, x, 64);
+      const float om = x == 16 ? xor16_partner(m) : xor32_partner(m);
+      const float ol = x == 16 ? xor16_partner(l) : xor32_partner(l);
       const float nm = fmaxf(m, om);
       l = (nm > -INFINITY) ? l * __expf(m - nm) + ol * __expf(om - nm) : 0.f;
       m = nm;
@@ -283,8 +284,7 @@ __device__ __forceinline__ void attn_bwd_q(const bf16_t* Q, const bf16_t* K, con
         if (qv && k >= qs && k < qe) delta += __expf(sc[j] * ATT_SCALE - lse) * dp[j];
       }
     }
-    delta += __shfl_xor(delta, 16, 64);
-    delta += __shfl_xor(delta, 32, 64);
+    delta = cross_row_sum(delta);
     f32x4 dq[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
     for (int kb = sp.lo; kb < sp.hi; kb += 32) {
       float sc[8], dp[8];

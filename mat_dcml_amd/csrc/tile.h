@@ -67,11 +67,7 @@ __device__ __forceinline__ f32x4 rowsum(const RT& t) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     float x = t.v[0][r] + t.v[1][r] + t.v[2][r] + t.v[3][r];
-    x += __shfl_xor(x, 1, 64);
-    x += __shfl_xor(x, 2, 64);
-    x += __shfl_xor(x, 4, 64);
-    x += __shfl_xor(x, 8, 64);
-    s[r] = x;
+    s[r] = group_sum<16>(x);
   }
   return s;
 }
@@ -143,8 +139,7 @@ __device__ __forceinline__ void flush_cols(f32x4 acc, float* dst, int lane) {
 #pragma unroll
   for (int ct = 0; ct < 4; ++ct) {
     float x = acc[ct];
-    x += __shfl_xor(x, 16, 64);
-    x += __shfl_xor(x, 32, 64);
+    x = cross_row_sum(x);
     if ((lane >> 4) == 0) atomicAdd(dst + 16 * ct + (lane & 15), x);
   }
 }
