@@ -151,6 +151,13 @@ class MATTrainer:
         mat_fused.bump_version(pol.transformer)
         return value_loss.detach(), grad_norm.detach(), policy_loss.detach(), entropy.detach(), imp.detach().mean()
 
+    def _dec_grad_range(self, m):
+        """Flat-gradient element range of the decoder parameters (None if not contiguous)."""
+        if not hasattr(self, "_dec_range"):
+            from ..ops import mat_train
+            self._dec_range = mat_train.flat_range(list(m.decoder.parameters()), self.comm._flat.buf)
+        return self._dec_range
+
     def ppo_update_fused(self, mb):
         from ..ops import mat_train
         pol = self.policy
@@ -158,19 +165,38 @@ class MATTrainer:
         enc, dec, _ = mat_train._state(m, mb["obs"].device)
         v, rep = enc.forward(mb["obs"], save=True)
         logp, ent = dec.forward(rep, mb["actions"], mb["ava"], save=True)
-        self.comm._flat.buf.zero_()
+        buf = self.comm._flat.buf
+        buf.zero_()
         dv, dlp, dent = self.loss_fused.run(v, logp, ent, mb, self.comm)
         m._mdl_gws_active = hasattr(m, "_mdl_gws")   # weight-gradient atomics into the 8-copy workspace
         drep = dec.backward(dlp, dent)
+        # data parallel: the decoder's gradient all-reduce (RCCL, on the process group's stream) runs under the
+        # encoder backward; the rest of the buffer is reduced after it
+        rng = self._dec_grad_range(m) if self.comm.world_size > 1 and not self.poison else None
+        work = None
+        if rng is not None:
+            mat_train.reduce_grad_workspace(m, *rng)
+            work = self.comm.all_reduce_sum_async(buf[rng[0]:rng[1]])
         enc.backward(drep, dv)
         m._mdl_gws_active = False
-        mat_train.reduce_grad_workspace(m)
+        if rng is None:
+            mat_train.reduce_grad_workspace(m)
+        else:
+            mat_train.reduce_grad_workspace(m, 0, rng[0])
+            mat_train.reduce_grad_workspace(m, rng[1])
         dec.ctx = None
         enc.ctx = None
         if self.poison:
-            self.comm._flat.buf[:1].fill_(float("nan"))   # the fused Adam kernel skips non-finite steps
+            buf[:1].fill_(float("nan"))   # the fused Adam kernel skips non-finite steps
         if self.comm.world_size > 1:
-            self.comm.all_reduce_grads_(self.params)
+            if work is None:
+                self.comm.all_reduce_grads_(self.params)
+            else:
+                for a, b in ((0, rng[0]), (rng[1], buf.numel())):
+                    if b > a:
+                        self.comm.all_reduce_sum_(buf[a:b])
+                work.wait()
+                buf.mul_(1.0 / self.comm.world_size)
         pol.optimizer.step()
         mat_fused.bump_version(m)
         return pol.optimizer.grad_norm

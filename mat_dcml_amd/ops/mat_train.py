@@ -420,13 +420,30 @@ def check_grad_ptrs(p, flat):
         raise RuntimeError(f"gradient pointers outside the flat gradient buffer: {bad[:6]} (flat {lo:#x}..{hi:#x})")
 
 
-def reduce_grad_workspace(model):
+def reduce_grad_workspace(model, lo=0, hi=None):
+    """Fold the workspace copies of flat-gradient elements [lo, hi) back into the flat buffer (and zero them)."""
     st = getattr(model, "_mdl_gws_buf", None)
     if st is None:
         return
     ws, g, stride, copies = st
-    check(lib().mdl_grad_reduce(g.data_ptr(), ws.data_ptr(), g.numel(), stride, copies, kernels._stream()),
-          "grad_reduce")
+    hi = g.numel() if hi is None else hi
+    if hi <= lo:
+        return
+    check(lib().mdl_grad_reduce(g.data_ptr() + 4 * lo, ws.data_ptr() + 4 * lo, hi - lo, stride, copies,
+                                kernels._stream()), "grad_reduce")
+
+
+def flat_range(params, flat):
+    """[lo, hi) element range of ``flat`` holding the gradients of ``params`` (None if not one contiguous range)."""
+    offs = sorted(((p.grad.data_ptr() - flat.data_ptr()) // 4, p.numel()) for p in params if p.grad is not None)
+    if not offs:
+        return None
+    lo = end = offs[0][0]
+    for o, n in offs:
+        if o != end:
+            return None
+        end = o + n
+    return lo, end
 
 
 def _state(model, dev):

@@ -83,6 +83,14 @@ class Comm:
         dist.all_reduce(self._flat.buf, op=dist.ReduceOp.SUM, group=self.group)
         self._flat.buf.mul_(1.0 / self.world_size)
 
+    def all_reduce_sum_async(self, t: torch.Tensor):
+        """Start a SUM all-reduce of ``t``; returns a work handle (``wait()`` makes the current stream wait) or None.
+        With the nccl (RCCL) backend the collective runs on the process group's own HIP stream, ordered after the
+        work already queued on the current stream, so kernels launched afterwards overlap it."""
+        if self.world_size == 1:
+            return None
+        return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+
     def destroy(self):
         if self.world_size > 1 and dist.is_initialized():
             dist.destroy_process_group()
