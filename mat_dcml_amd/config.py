@@ -135,6 +135,33 @@ _MPE_FLAGS = [
     ("num_adversaries", int, 3, "adversaries (tag / world_comm / attack)"),
 ]
 
+# MA-MuJoCo (``mat_src/mat/scripts/train/train_mujoco.py:64-86`` + the env_args it builds, ``:20-27``)
+_MUJOCO_FLAGS = [
+    ("scenario", str, "Hopper-v2", "MuJoCo robot (HalfCheetah-v2, Ant-v2, Hopper-v2, Walker2d-v2, Swimmer-v2, "
+                                   "Reacher-v2, coupled_half_cheetah, manyagent_swimmer, manyagent_ant)"),
+    ("agent_conf", str, "3x1", "joint partition, e.g. 6x1 / 2x3 / 2x4 / 4x2"),
+    ("agent_obsk", int, 0, "observe joints within k hops of the agent's own"),
+    ("k_categories", str, None, "per-hop observed categories, e.g. 'qpos,qvel|qpos'"),
+    ("global_categories", str, None, "categories of the global joints"),
+    ("episode_limit", int, 1000, "env time limit"),
+    ("faulty_node", int, -1, "agent whose actions are zeroed during training (-1: none)"),
+    ("random_agent_order", "true", F, "RandomMujocoMulti: permute the agents every episode"),
+    ("add_move_state", "true", F, ""), ("add_local_obs", "true", F, ""), ("add_distance_state", "true", F, ""),
+    ("add_enemy_action_state", "true", F, ""), ("add_agent_id", "true", F, ""), ("add_visible_state", "true", F, ""),
+    ("add_xy_state", "true", F, ""), ("use_state_agent", "true", F, ""), ("use_mustalive", "false", T, ""),
+    ("add_center_xy", "true", F, ""),
+]
+
+# Google Research Football (``mat_src/mat/scripts/train/train_football.py:64-86``)
+_FOOTBALL_FLAGS = [
+    ("scenario", str, "academy_3_vs_1_with_keeper", "GRF academy scenario"),
+    ("n_agent", int, 3, "controlled left-team players"),
+    ("add_move_state", "true", F, ""), ("add_local_obs", "true", F, ""), ("add_distance_state", "true", F, ""),
+    ("add_enemy_action_state", "true", F, ""), ("add_agent_id", "true", F, ""), ("add_visible_state", "true", F, ""),
+    ("add_xy_state", "true", F, ""), ("use_state_agent", "true", F, ""), ("use_mustalive", "false", T, ""),
+    ("add_center_xy", "true", F, ""),
+]
+
 # framework (new)
 _FRAMEWORK_FLAGS = [
     ("n_workers", int, 100, "DCML worker count W (agents = W + 1); 4 / 32 / 100 / 128 in the BASELINE configs"),

@@ -65,13 +65,15 @@ class SMACRunner(DCMLRunner):
         self.num_agents = self.envs.n_agents
         obs_dim = self.envs.observation_space[0][0]
         share_dim = self.envs.share_observation_space[0][0]
-        act_space = self.envs.action_space[0]
+        act_space = getattr(self.envs, "policy_action_space", None) or self.envs.action_space[0]
         torch.manual_seed(a.seed)
         self.policy = TransformerPolicy(a, [obs_dim], [share_dim], act_space, self.num_agents, device=self.device)
         self.comm.broadcast_module_(self.policy.transformer)
         self.comm.attach_flat_grads(self.policy.transformer.parameters())
         self.trainer = MATTrainer(a, self.policy, self.num_agents, device=self.device, comm=self.comm)
-        self.buffer = RolloutBuffer(a.episode_length, E, self.num_agents, obs_dim, share_dim, act_space.n,
+        pol = self.policy
+        self.buffer = RolloutBuffer(a.episode_length, E, self.num_agents, obs_dim, share_dim, pol.act_dim,
+                                    pol.act_output_num, pol.act_prob_dim,
                                     gamma=a.gamma, gae_lambda=a.gae_lambda, use_valuenorm=a.use_valuenorm or a.use_popart,
                                     n_objective=1, device=self.device, store_share=False)
         self.log_dir = os.path.join(str(self.run_dir), "logs") if self.run_dir else None

@@ -100,7 +100,7 @@ class ScalarWriter:
         value = float(value)
         wall = time.time()
         self.scalars.setdefault(tag, []).append([wall, int(step), value])
-        if not self.enabled:
+        if not self.enabled or self._jsonl is None:   # disabled rank, or written after close()
             return
         self._jsonl.write(json.dumps({"tag": tag, "step": int(step), "wall": wall, "value": value}) + "\n")
         self._jsonl.flush()
