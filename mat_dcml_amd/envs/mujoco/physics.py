@@ -23,6 +23,7 @@ surrogate — documented, not MuJoCo:
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -240,6 +241,10 @@ class PlanarSim:
         self.k_contact = model.mass * w * w / npts
         self.c_contact = 2.0 * model.mass * w / npts
         self.mu = 0.9
+        self.gravity = torch.tensor([0.0, -9.81 * model.mass], **f)
+        # launch-bound inner loop (nsub sub-steps x ~50 small kernels): captured once into a hipGraph on GPU
+        self.use_graph = self.dev.type == "cuda" and os.environ.get("MAT_DCML_ENV_GRAPHS", "1") != "0"
+        self._graph = None
         self.target = torch.zeros(self.B, 2, **f)
         self.p = torch.zeros(self.B, 2, **f)
         self.th = torch.zeros(self.B, **f)
@@ -336,7 +341,7 @@ class PlanarSim:
         tau = tau + cpf @ self.down.t() - _cross(start, Fd)
         Ftot = F.sum(1)
         if m.kind == "ground":
-            Ftot = Ftot + torch.tensor([0.0, -9.81 * m.mass], device=self.dev)
+            Ftot = Ftot + self.gravity
         rel = pts - self.p[:, None, :]
         tau_root = _cross(rel, F).sum(1) - (tau_motor * self.root_attached).sum(1) + tau_root_motor
         self.f_end = Fl
@@ -349,9 +354,41 @@ class PlanarSim:
         self.q = self.q + h * self.qd
         self.tau = tau_motor
 
+    _STATE = ("p", "th", "v", "w", "q", "qd", "tau", "f_end", "f_root")
+
     def step(self, a):
         """a: (E, nu) in [-1, 1] (coupled twin: (E, 2·nu))."""
-        a = a.reshape(self.B, -1).clamp(-1.0, 1.0)
+        a = a.reshape(self.B, -1).float()
+        if not self.use_graph:
+            return self._step(a)
+        if self._graph is None:
+            self._capture(a)
+        self._a_in.copy_(a)
+        self._graph.replay()
+
+    def _capture(self, a):
+        """Record one env step (all sub-steps) as a hipGraph whose inputs / outputs are the state buffers."""
+        self._a_in = a.clone()
+        saved = {k: getattr(self, k).clone() for k in self._STATE}
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):          # warm-up outside capture (allocator / library init)
+            self._step(self._a_in)
+        torch.cuda.current_stream().wait_stream(side)
+        bufs = {k: v.clone() for k, v in saved.items()}
+        for k, v in bufs.items():
+            setattr(self, k, v)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._step(self._a_in)
+            for k in self._STATE:
+                bufs[k].copy_(getattr(self, k))
+        for k, v in bufs.items():              # the state lives in the graph's input buffers
+            setattr(self, k, v)
+        self._graph = g
+
+    def _step(self, a):
+        a = a.clamp(-1.0, 1.0)
         full = (a * self.gear) @ self.act_map                           # (B, J + 1)
         tau_m, tau_root = full[:, :self.J], full[:, self.J]
         for _ in range(self.nsub):
@@ -375,7 +412,7 @@ class PlanarSim:
         B, J = self.B, self.J
         mask = torch.ones(self.E, dtype=torch.bool, device=self.dev) if mask is None else mask
         mk = mask.repeat_interleave(self.twins)
-        sel = lambda new, old: torch.where(mk.view(-1, *([1] * (old.dim() - 1))), new, old)
+        sel = lambda new, old: old.copy_(torch.where(mk.view(-1, *([1] * (old.dim() - 1))), new, old))
         rp, rv = m.reset_pos, m.reset_vel
         vel = (lambda s: torch.randn(s, generator=self.gen, device=self.dev) * rv) if m.reset_vel_normal else \
             (lambda s: self._u(s, rv))
@@ -392,14 +429,14 @@ class PlanarSim:
             zs = self._fk(self.p, self.th, self.q)[0][..., 1]
             rz = (self.p[:, None, :] + _rot(self.th, self.root_ends))[..., 1]
             lift = (0.002 - torch.cat([zs, rz], 1).min(1).values).clamp_min(0.0)
-            self.p = self.p + torch.stack([torch.zeros_like(lift), lift * mk], -1)
+            self.p += torch.stack([torch.zeros_like(lift), lift * mk], -1)
         if m.kind == "arm":
             tgt = self._u((B, 2), 0.2)
             for _ in range(8):     # rejection: ‖goal‖ < 0.2 (reacher.py reset_model)
                 bad = tgt.norm(dim=-1) >= 0.2
                 tgt = torch.where(bad[:, None], self._u((B, 2), 0.2), tgt)
             self.target = sel(tgt, self.target)
-        self.f_end = torch.where(mk[:, None, None], torch.zeros_like(self.f_end), self.f_end)
+        self.f_end.copy_(torch.where(mk[:, None, None], torch.zeros_like(self.f_end), self.f_end))
 
     def fingertip(self):
         end = self._fk(self.p, self.th, self.q)[0]

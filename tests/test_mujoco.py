@@ -194,3 +194,23 @@ def test_mujoco_env_and_policy_on_gpu():
         obs, share, rew, dones, info, ava = env.step(torch.rand(64, 4, 2, device="cuda") * 2 - 1)
     torch.cuda.synchronize()
     assert torch.isfinite(obs).all() and obs.device.type == "cuda"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scenario,conf", [("HalfCheetah-v2", "6x1"), ("Ant-v2", "2x4"), ("Reacher-v2", "2x1"),
+                                           ("coupled_half_cheetah", "1p1"), ("manyagent_swimmer", "4x2")])
+def test_graph_captured_step_matches_eager(scenario, conf, monkeypatch):
+    """the hipGraph replay of the sub-step loop must give the eager result (same kernels, same order)"""
+    envs = []
+    for graphs in ("1", "0"):
+        monkeypatch.setenv("MAT_DCML_ENV_GRAPHS", graphs)
+        envs.append(MujocoMultiVec(scenario, conf, 32, agent_obsk=1, device="cuda", seed=4))
+    assert envs[0].sim.use_graph and not envs[1].sim.use_graph
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for t in range(12):
+        act = torch.rand(32, envs[0].A, envs[0].n_actions, device="cuda", generator=g) * 2 - 1
+        outs = [e.step(act) for e in envs]
+        torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(outs[0][2], outs[1][2], rtol=1e-4, atol=1e-4)
+    for k in ("p", "th", "q", "qd"):
+        torch.testing.assert_close(getattr(envs[0].sim, k), getattr(envs[1].sim, k), rtol=1e-4, atol=1e-4)
