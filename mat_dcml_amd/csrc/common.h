@@ -35,7 +35,9 @@ __host__ __device__ __forceinline__ u4 philox4x32_10(uint32_t c0, uint32_t c1, u
   return {c0, c1, c2, c3};
 }
 
-// uniform in (0,1) from the 24 high bits, centred — matches utils/philox.py:u01_open (exact in fp32 and fp64)
+// uniform in (0,1) from the 24 high bits, centred — matches utils/philox.py:u01_open.  Exact in fp64.  The fp32
+// variant rounds the top value (u >> 8 == 2^24 - 1) up to exactly 1.0f (found by tests/native/host_checks.hip);
+// its one user (workload noise in [0.8, 1.2]) is closed at the top by design and the torch path rounds the same way.
 __host__ __device__ __forceinline__ double u01_open(uint32_t u) { return ((double)(u >> 8) + 0.5) * (1.0 / 16777216.0); }
 __host__ __device__ __forceinline__ float u01_open_f(uint32_t u) { return ((float)(u >> 8) + 0.5f) * (1.0f / 16777216.0f); }
 

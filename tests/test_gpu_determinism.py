@@ -1,0 +1,105 @@
+"""Determinism harness for the HIP kernels (run twice with the same Philox seed, require
+bitwise-equal outputs — a missing barrier or an LDS race shows up as run-to-run differences).
+
+* DCML env reset / step kernels: bitwise equal across two envs with the same seed and actions;
+* persistent decode kernel (stochastic and deterministic, stride 1 and stride blocks): bitwise equal actions /
+  log-probs for the same inputs and draws, also with other work interleaved on the stream;
+* fused training forward (values, log-probs, entropies): bitwise equal;
+* fused backward: weight gradients are accumulated with fp32 atomics into an 8-copy workspace, whose summation
+  order may differ between runs — required to agree to fp32 rounding (relative 1e-5), and the max deviation is
+  printed;
+* the whole fused PPO iteration (rollout + 2 epochs): parameters after two identical runs agree to 1e-5.
+"""
+import pytest
+import torch
+
+from mat_dcml_amd.envs.dcml.config import DCMLConfig
+from mat_dcml_amd.envs.dcml.vec_env import DeviceDCMLEnv
+from mat_dcml_amd.ops import mat_fused, mat_train
+
+from test_gpu_decode import inputs as dec_inputs, make as dec_make
+from test_gpu_train import make as train_make
+
+pytestmark = pytest.mark.gpu
+
+
+def _same(a, b):
+    return a.shape == b.shape and torch.equal(a, b)
+
+
+def test_env_kernels_bitwise_repeatable(gpu):
+    cfg = DCMLConfig(n_workers=32)
+    envs = [DeviceDCMLEnv(128, cfg, device=gpu, seed=11, backend="hip") for _ in range(2)]
+    outs = [e.reset() for e in envs]
+    assert all(_same(a, b) for a, b in zip(*outs))
+    g = torch.Generator(device=gpu).manual_seed(0)
+    for _ in range(8):
+        act = (torch.rand(128, 33, device=gpu, generator=g) < 0.5).float()
+        act[:, -1] = torch.rand(128, device=gpu, generator=g)
+        r = [e.step(act) for e in envs]
+        assert all(_same(a, b) for a, b in zip(*r))
+
+
+@pytest.mark.parametrize("det,stride", [(False, 1), (True, 1), (True, 10)])
+def test_decode_bitwise_repeatable(gpu, det, stride):
+    L, B = 33, 200
+    m = dec_make(L, gpu)
+    obs, ava, rep, rand = dec_inputs(m, B, L, gpu)
+    a1, lp1 = mat_fused.decode(m, rep, ava, det, stride, rand)
+    junk = torch.randn(4096, 4096, device=gpu) @ torch.randn(4096, 4096, device=gpu)   # perturb timing / caches
+    a2, lp2 = mat_fused.decode(m, rep, ava, det, stride, rand)
+    torch.cuda.synchronize()
+    del junk
+    assert _same(a1, a2) and _same(lp1, lp2)
+
+
+def test_fused_training_repeatable(gpu):
+    L, B = 33, 160
+    m = train_make(L, gpu, seed=5)
+    g = torch.Generator(device=gpu).manual_seed(6)
+    obs = torch.rand(B, L, 7, device=gpu, generator=g)
+    ava = torch.ones(B, L, 2, device=gpu)
+    ava[:, 2::5, 1] = 0
+    actions = (torch.rand(B, L, 1, device=gpu, generator=g) < 0.5).float()
+    actions[ava[..., 1:] == 0] = 0
+    actions[:, -1, 0] = torch.rand(B, device=gpu, generator=g)
+    w = [torch.randn(B, L, 1, device=gpu, generator=g) for _ in range(3)]
+    fwd, grads = [], []
+    for _ in range(2):
+        for p in m.parameters():
+            p.grad = torch.zeros_like(p)
+        v, lp, ent = mat_train.evaluate_actions(m, obs, actions, ava)
+        ((lp * w[0]).sum() + (v * w[1]).sum() + (ent * w[2]).sum()).backward()
+        torch.cuda.synchronize()
+        fwd.append((v.detach().clone(), lp.detach().clone(), ent.detach().clone()))
+        grads.append({n: p.grad.detach().clone() for n, p in m.named_parameters()})
+    assert all(_same(a, b) for a, b in zip(*fwd)), "fused forward is not bitwise repeatable"
+    worst = 0.0
+    # key biases get ~zero gradient (softmax is shift invariant): measure them against a floor of the global norm
+    floor = 1e-3 * torch.stack([g.norm() for g in grads[0].values()]).norm()
+    for n, g1 in grads[0].items():
+        g2 = grads[1][n]
+        d = ((g1 - g2).norm() / (g1.norm() + floor)).item()
+        worst = max(worst, d)
+        assert d < 1e-5, (n, d)
+    print(f"max relative run-to-run gradient deviation (fp32 atomic order): {worst:.2e}")
+
+
+def test_fused_ppo_iteration_repeatable(gpu):
+    from mat_dcml_amd.config import get_config, parse_args
+    from mat_dcml_amd.parallel.comm import Comm
+    from mat_dcml_amd.runner.dcml_runner import DCMLRunner
+    flats = []
+    for _ in range(2):
+        args = parse_args(["--n_workers", "32", "--n_rollout_threads", "32", "--episode_length", "10", "--ppo_epoch",
+                           "2", "--num_mini_batch", "2", "--use_valuenorm", "--env_name", "DCML", "--seed", "3"],
+                          get_config(), warn=False)
+        r = DCMLRunner({"all_args": args, "device": gpu, "run_dir": None, "comm": Comm(device=gpu)})
+        assert r.trainer.fused
+        r.warmup()
+        r.train_iteration()
+        torch.cuda.synchronize()
+        flats.append(torch.cat([p.detach().reshape(-1) for p in r.policy.transformer.parameters()]).double())
+    d = ((flats[0] - flats[1]).norm() / flats[0].norm()).item()
+    print(f"run-to-run parameter deviation after one PPO iteration: {d:.2e}")
+    assert d < 1e-5
