@@ -23,7 +23,7 @@ import os
 import torch
 import torch.nn as nn
 
-from ..ops import mat_fused, rl_ops
+from ..ops import kernels, mat_fused, rl_ops
 from .valuenorm import ValueNorm
 
 
@@ -223,16 +223,29 @@ class MATTrainer:
         lp_f = buffer.flat("action_log_probs")
         vp_f = buffer.flat("value_preds")
         am_f = buffer.flat("active_masks")
+        # HIP path: advantage statistics by a fixed-order fp64 reduction kernel, and each minibatch gathered by ONE
+        # launch that also standardises the advantages of the rows it reads (no full normalised copy)
+        native = self.fused and kernels.use_hip(obs_f)
         for epoch in range(self.ppo_epoch):
             if epoch == 0 or self.recompute_gae_every_epoch:
                 next_values = pol.get_values(None, buffer.obs[-1], buffer.available_actions[-1])
                 buffer.compute_returns(next_values, self.value_normalizer)
-                adv = self._advantages(buffer)
-                adv_f = adv.reshape(T * E, *adv.shape[2:])
+                if native:
+                    sums = kernels.masked_sums(buffer.advantages, buffer.active_masks[:-1])
+                    if self.comm is not None and self.comm.world_size > 1:
+                        self.comm.all_reduce_sum_(sums)
+                    adv_f = buffer.flat("advantages")
+                else:
+                    adv = self._advantages(buffer)
+                    adv_f = adv.reshape(T * E, *adv.shape[2:])
                 ret_f = buffer.flat("returns")
             for idx in buffer.minibatch_indices(self.num_mini_batch, self.generator):
-                mb = {"obs": obs_f[idx], "actions": act_f[idx], "ava": ava_f[idx], "old_logp": lp_f[idx],
-                      "value_preds": vp_f[idx], "returns": ret_f[idx], "active": am_f[idx], "adv": adv_f[idx]}
+                src = {"obs": obs_f, "actions": act_f, "ava": ava_f, "old_logp": lp_f, "value_preds": vp_f,
+                       "returns": ret_f, "active": am_f, "adv": adv_f}
+                if native:
+                    mb = kernels.gather_rows(src, idx, sums, ("adv",))
+                else:
+                    mb = {k: v[idx] for k, v in src.items()}
                 if self.fused:
                     acc[3:5] += self.ppo_update_fused(mb)
                     continue

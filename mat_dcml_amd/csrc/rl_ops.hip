@@ -75,3 +75,102 @@ MDL_API int mdl_pack_weights(const void* tab, int n, hipStream_t s) {
   MDL_CHECK_LAUNCH();
   return 0;
 }
+
+// ---------------------------------------------------------------------------------------------------------------
+// Advantage statistics + minibatch gather (reference mat_trainer.py:193-197 and shared_buffer.py:260-314).
+//
+// masked_sums: (Σ x, Σ x², count) over entries whose active mask is non-zero, in fp64 — a fixed-order two-pass
+// reduction (per-block partials, then one block), so the statistics are bitwise repeatable (no float atomics).
+// The mask has one entry per `mdiv` consecutive x entries (active_masks (…, 1) against advantages (…, n_obj)).
+constexpr int SUM_BLOCKS = 240;
+
+__global__ __launch_bounds__(256) void masked_sums_partial_kernel(const float* __restrict__ x,
+                                                                   const float* __restrict__ mask, int n, int mdiv,
+                                                                   double* __restrict__ part) {
+  double s = 0.0, sq = 0.0, c = 0.0;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    if (mask[i / mdiv] != 0.f) {
+      const double v = (double)x[i];
+      s += v;
+      sq += v * v;
+      c += 1.0;
+    }
+  }
+  __shared__ double red[3][256];
+  red[0][threadIdx.x] = s;
+  red[1][threadIdx.x] = sq;
+  red[2][threadIdx.x] = c;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w)
+      for (int k = 0; k < 3; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x < 3) part[blockIdx.x * 3 + threadIdx.x] = red[threadIdx.x][0];
+}
+
+__global__ __launch_bounds__(256) void masked_sums_final_kernel(const double* __restrict__ part, int nb,
+                                                                 double* __restrict__ out) {
+  __shared__ double red[3][256];
+  for (int k = 0; k < 3; ++k) red[k][threadIdx.x] = threadIdx.x < nb ? part[threadIdx.x * 3 + k] : 0.0;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w)
+      for (int k = 0; k < 3; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x < 3) out[threadIdx.x] = red[threadIdx.x][0];
+}
+
+// out[3] and part[3 * SUM_BLOCKS] are device fp64 buffers
+MDL_API int mdl_masked_sums(const float* x, const float* mask, int n, int mdiv, double* part, double* out,
+                            hipStream_t s) {
+  if (n < 0 || mdiv < 1) return -1;
+  hipLaunchKernelGGL(masked_sums_partial_kernel, dim3(SUM_BLOCKS), dim3(256), 0, s, x, mask, n, mdiv, part);
+  hipLaunchKernelGGL(masked_sums_final_kernel, dim3(1), dim3(256), 0, s, part, SUM_BLOCKS, out);
+  MDL_CHECK_LAUNCH();
+  return 0;
+}
+
+// gather_rows: dst_k[r, :] = src_k[idx[r], :] for up to 10 row-major fp32 tensors in ONE launch (blockIdx.y = k);
+// entries flagged `norm` are standardised on the fly with the masked_sums statistics:
+// (x - mean) / (std + eps), std the population std — the normalised advantage of the reference, computed only for
+// the rows a minibatch actually reads.
+constexpr int GATHER_MAX = 10;
+struct GatherEnt { const float* src; float* dst; int width; int norm; };
+struct GatherArgs { GatherEnt e[GATHER_MAX]; const int64_t* idx; const double* sums; int rows; int n; float eps; };
+
+__global__ __launch_bounds__(256) void gather_rows_kernel(GatherArgs a) {
+  const GatherEnt e = a.e[blockIdx.y];
+  const int total = a.rows * e.width;
+  float mean = 0.f, sd = 0.f;
+  if (e.norm) {
+    const double cnt = a.sums[2] < 1.0 ? 1.0 : a.sums[2];
+    const double m = a.sums[0] / cnt;
+    double var = a.sums[1] / cnt - m * m;
+    var = var < 0.0 ? 0.0 : var;
+    mean = (float)m;
+    sd = (float)sqrt(var);
+  }
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int r = i / e.width, c = i - r * e.width;
+    float v = e.src[(size_t)a.idx[r] * e.width + c];
+    if (e.norm) v = (v - mean) / (sd + a.eps);
+    e.dst[i] = v;
+  }
+}
+
+MDL_API int mdl_gather_rows(const GatherArgs* a, hipStream_t s) {
+  if (a->n < 1 || a->n > GATHER_MAX || a->rows < 0) return -1;
+  long long most = 0;
+  for (int k = 0; k < a->n; ++k) {
+    const long long t = (long long)a->rows * a->e[k].width;
+    if (a->e[k].width < 1 || t >= (1ll << 31)) return -2;
+    most = t > most ? t : most;
+  }
+  long long gx = (most + 255) / 256;
+  gx = gx < 1 ? 1 : (gx > 1024 ? 1024 : gx);
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)gx, a->n), dim3(256), 0, s, *a);
+  MDL_CHECK_LAUNCH();
+  return 0;
+}

@@ -112,6 +112,57 @@ def philox_fill(n, c1, c2, c3, k0, k1, device):
     return out
 
 
+# ----------------------------------------------------------------------------------------- minibatch / adv stats
+sig("mdl_masked_sums", vp, vp, i32, i32, vp, vp, vp)
+_SUMS_WS = {}
+
+
+def masked_sums(x, mask):
+    """(Σx, Σx², count) over active entries as a device fp64[3] (fixed-order reduction, no host sync)."""
+    assert x.is_contiguous() and mask.is_contiguous() and x.dtype == mask.dtype == torch.float32
+    mdiv = x.numel() // mask.numel()
+    assert mdiv * mask.numel() == x.numel()
+    ws = _SUMS_WS.get(x.device)
+    if ws is None:
+        ws = _SUMS_WS[x.device] = torch.empty(3 * 240, dtype=torch.float64, device=x.device)
+    out = torch.empty(3, dtype=torch.float64, device=x.device)
+    check(lib().mdl_masked_sums(P(x), P(mask), x.numel(), mdiv, P(ws), P(out), _stream()), "masked_sums")
+    return out
+
+
+class GatherEnt(ctypes.Structure):
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("width", ctypes.c_int), ("norm", ctypes.c_int)]
+
+
+class GatherArgs(ctypes.Structure):
+    _fields_ = [("e", GatherEnt * 10), ("idx", ctypes.c_void_p), ("sums", ctypes.c_void_p), ("rows", ctypes.c_int),
+                ("n", ctypes.c_int), ("eps", ctypes.c_float)]
+
+
+sig("mdl_gather_rows", vp, vp)
+
+
+def gather_rows(srcs, idx, norm_sums=None, norm_keys=(), eps=1e-5):
+    """{name: src (N, …) fp32 contiguous} -> {name: src[idx]} in one launch; entries in ``norm_keys`` are
+    standardised with ``norm_sums`` (from ``masked_sums``) on the fly."""
+    assert idx.dtype == torch.int64 and idx.is_contiguous() and len(srcs) <= 10
+    a = GatherArgs()
+    out, keep = {}, []
+    for k, (name, src) in enumerate(srcs.items()):
+        assert src.is_contiguous() and src.dtype == torch.float32
+        dst = torch.empty((idx.numel(), *src.shape[1:]), dtype=torch.float32, device=src.device)
+        width = src[0].numel()
+        a.e[k] = GatherEnt(src.data_ptr(), dst.data_ptr(), width, int(name in norm_keys))
+        out[name] = dst
+        keep.append(src)
+    if norm_keys:
+        assert norm_sums is not None and norm_sums.dtype == torch.float64
+    a.idx, a.sums, a.rows, a.n, a.eps = idx.data_ptr(), norm_sums.data_ptr() if norm_sums is not None else 0, \
+        idx.numel(), len(srcs), eps
+    check(lib().mdl_gather_rows(ctypes.byref(a), _stream()), "gather_rows")
+    return out
+
+
 # ----------------------------------------------------------------------------------------- DCML env
 class EnvCfg(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in ("E", "W", "A", "P", "obs_dim", "share_dim", "fixed", "preset",

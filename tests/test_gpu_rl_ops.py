@@ -69,3 +69,28 @@ def test_mat_learns_on_dcml(gpu):
     first, last = sum(curve[:5]) / 5, sum(curve[-5:]) / 5
     print(f"mean step reward: first 5 iters {first:.1f} -> last 5 iters {last:.1f}")
     assert last > first + 0.1 * abs(first), (first, last)
+
+
+def test_masked_sums_and_gather_match_torch(gpu):
+    """minibatch gather (+ on-the-fly advantage standardisation) and the masked fp64 statistics vs torch"""
+    from mat_dcml_amd.ops import kernels, rl_ops
+    g = torch.Generator(device=gpu).manual_seed(0)
+    T, E, A = 50, 64, 33
+    adv = torch.randn(T, E, A, 1, device=gpu, generator=g) * 3 + 1
+    active = (torch.rand(T, E, A, 1, device=gpu, generator=g) < 0.8).float()
+    sums = kernels.masked_sums(adv, active)
+    ref = rl_ops.masked_sums(adv, active)
+    torch.testing.assert_close(sums, ref, rtol=1e-12, atol=1e-9)
+    assert torch.equal(sums, kernels.masked_sums(adv, active))          # fixed-order: bitwise repeatable
+    # 2-objective advantages share one active mask per (t, e, agent)
+    adv2 = torch.randn(T, E, A, 2, device=gpu, generator=g)
+    torch.testing.assert_close(kernels.masked_sums(adv2, active), rl_ops.masked_sums(adv2, active), rtol=1e-12,
+                               atol=1e-9)
+    obs = torch.randn(T * E, A, 7, device=gpu, generator=g)
+    act = torch.randn(T * E, A, 1, device=gpu, generator=g)
+    adv_f = adv.reshape(T * E, A, 1)
+    idx = torch.randperm(T * E, device=gpu, generator=g)[:800]
+    out = kernels.gather_rows({"obs": obs, "actions": act, "adv": adv_f}, idx, sums, ("adv",))
+    assert torch.equal(out["obs"], obs[idx]) and torch.equal(out["actions"], act[idx])
+    norm = rl_ops.normalize_from_sums(adv, ref).reshape(T * E, A, 1)[idx]
+    torch.testing.assert_close(out["adv"], norm, rtol=1e-6, atol=1e-6)
