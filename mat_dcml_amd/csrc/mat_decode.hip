@@ -19,9 +19,12 @@
 //     8 lanes per (tile row, head);
 //   * the action head, availability masking, inverse-CDF categorical sampling / Normal sampling, log-probs and
 //     the next row's action-embedding token are fused into the last phase.
-// Inputs rep (encoder output, f32), ava, and the uniform / normal draws come from HBM; outputs are actions and
-// log-probs (B, L).  Numerics: bf16 MFMA operands, f32 accumulation, f32 LayerNorm / softmax / log-softmax.
+// Inputs rep (encoder output, f32), ava, and the uniform / normal draws come from HBM — staged into LDS once at
+// kernel start when they fit (`stage`), so no row of the sequential agent loop waits on an HBM miss (the rep row
+// of phase D and the mask / draws of the head phase were first-touch loads on the critical path); outputs are
+// actions and log-probs (B, L).  Numerics: bf16 MFMA operands, f32 accumulation, f32 LayerNorm / softmax / log-softmax.
 #include "common.h"
+#include <cstdlib>
 
 using namespace mdl;
 
@@ -40,6 +43,7 @@ struct DecParams {
   float* out_a;          // [B][L]
   float* out_lp;         // [B][L]
   int B, L, act_dim, n_disc, stride, deterministic, epw, rmax, n_tok, tok_start, tok_zero;
+  int stage;             // 1: rep / ava / draws of the workgroup's envs are staged in LDS at kernel start
 };
 
 constexpr int SP = 68;   // f32 staging row pitch (floats)
@@ -50,6 +54,15 @@ __device__ __forceinline__ int kv_off(int b, int kind, int m, int j, int col, in
   const int chunk = (col >> 3) ^ (j & 7);
   return ((((b * 4 + kind) * epw + m) * L + j) << 6) + (chunk << 3) + (col & 7);
 }
+
+#ifdef MDL_DECODE_PROF
+__device__ unsigned long long g_attn_prof[8];
+#define MDL_ATT_MARK(k) do { if (aprof) { const unsigned long long t_ = clock64(); g_attn_prof[k] += t_ - at_; at_ = t_; } } while (0)
+#define MDL_ATT_INIT() const bool aprof = blockIdx.x == 0 && tid == 0; unsigned long long at_ = clock64()
+#else
+#define MDL_ATT_INIT() do { } while (0)
+#define MDL_ATT_MARK(k) do { } while (0)
+#endif
 
 __device__ __forceinline__ f32x4 mfma2(const bf16x8 a[2], const bf16x8 w[2], f32x4 acc) {
   acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], w[0], acc, 0, 0, 0);
@@ -124,68 +137,114 @@ __device__ __forceinline__ void store_xf(float* X, int lane, const float xf[16])
 }
 
 
-// Causal attention of the pass's tile rows over cached rows 0..i of their env.  32 lanes (half a wave) per
-// (tile row, head): scores with lanes striding over the keys; P·V with the 32 lanes split into 8 groups of 4 output
-// dims x 4 key groups (each lane sums ~i/4 keys, the 4 key groups are combined by two xor-shuffles).  An item's
-// lanes live in one wave, so the score -> P·V hand-off through PR needs only a wave-level LDS wait.
+// Causal attention of the pass's live tile rows over cached rows 0..i of their env.  lpi lanes (half a wave at
+// the rollout shape) per (tile row, head): scores with lanes striding over the keys; P·V with the lanes split
+// into 8 groups of 4 output dims x lpi/8 key groups (each lane sums ~i/(lpi/8) keys, the key groups combined by
+// DPP / permlane shuffles).  An item's lanes live in one wave, so the score -> P·V hand-off through PR needs only
+// a wave-level LDS wait.  Latency structure (the decode runs one row per env per step): only live items are
+// visited (dead tile rows' XA rows are never consumed by a live row — MFMA rows are independent — and XA is
+// zeroed once at kernel start), and the score / P·V loops issue all their LDS loads before using any of them
+// (indices clamped to row i and masked, instead of per-key branches that serialised the load latencies).
 template <int lpi>
 __device__ __forceinline__ void attention_phase_t(const bf16_t* KV, const float* Q, float* PR, bf16_t* XA,
                                                   const int* ROWI, int R, int EPW, int L, int b, int kind,
-                                                  float scale, int tid) {
-  // lpi = lanes per (row, head) item: 32 when <= 4 tile rows are live (rollout), 16 / 8 for the wider stride-mode
-  // passes, so every pass uses all 256 lanes
+                                                  float scale, int tid, int live) {
   const int u = tid & (lpi - 1);
   const int dg = u & 7, kg = u >> 3, nkg = lpi >> 3;
-  for (int item = tid / lpi; item < 32; item += 256 / lpi) {
+  MDL_ATT_INIT();
+  for (int item = tid / lpi; item < 2 * live; item += 256 / lpi) {
     const int t = item >> 1, h = item & 1;
-    const int i = ROWI[t];          // uniform over the 32 lanes of the item
-    if (i < 0) {                    // unused tile row: zero A-operand row for the projection
-      if (kg == 0) {
-        bf16_t* xa = XA + t * XP + 32 * h + 4 * dg;
-        xa[0] = 0; xa[1] = 0; xa[2] = 0; xa[3] = 0;
-      }
-      continue;
-    }
+    const int i = ROWI[t];          // uniform over the item's lanes; >= 0 for every live row
     const int m = t / R;
     float* pr = PR + (t * 2 + h) * L;
     float q[32];
 #pragma unroll
     for (int d = 0; d < 32; ++d) q[d] = Q[t * SP + 32 * h + d];
+    MDL_ATT_MARK(0);
+    auto krow_of = [&](int j) { return KV + kv_off(b, kind, m, j, 0, EPW, L) - ((0 ^ (j & 7)) << 3); };
+    // the first KR keys of every lane: loads for all of them first, then the dot products (four independent
+    // 8-long FMA chains per key), masked beyond row i
+    constexpr int KR = lpi >= 32 ? 2 : 4;
+    bf16x8 kv[KR][4];
+#pragma unroll
+    for (int kk = 0; kk < KR; ++kk) {
+      const int j = min(u + kk * lpi, i);
+      const bf16_t* krow = krow_of(j);
+#pragma unroll
+      for (int lc = 0; lc < 4; ++lc) kv[kk][lc] = *(const bf16x8*)(krow + (((4 * h + lc) ^ (j & 7)) << 3));
+    }
+    float scr[KR];
     float mx = -INFINITY;
-    for (int j = u; j <= i; j += lpi) {
-      const bf16_t* krow = KV + kv_off(b, kind, m, j, 0, EPW, L) - ((0 ^ (j & 7)) << 3);  // row base
-      float dot = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < KR; ++kk) {
+      float d4[4];
 #pragma unroll
       for (int lc = 0; lc < 4; ++lc) {
-        const int pc = (4 * h + lc) ^ (j & 7);
-        const bf16x8 kv8 = *(const bf16x8*)(krow + pc * 8);
+        float d = 0.f;
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) dot += q[lc * 8 + jj] * bf2f((bf16_t)kv8[jj]);
+        for (int jj = 0; jj < 8; ++jj) d += q[lc * 8 + jj] * bf2f((bf16_t)kv[kk][lc][jj]);
+        d4[lc] = d;
       }
-      const float sc = dot * scale;
+      scr[kk] = u + kk * lpi <= i ? ((d4[0] + d4[1]) + (d4[2] + d4[3])) * scale : -INFINITY;
+      mx = fmaxf(mx, scr[kk]);
+    }
+    for (int j = u + KR * lpi; j <= i; j += lpi) {      // long rows only (L > KR * lpi)
+      const bf16_t* krow = krow_of(j);
+      float d4[4];
+#pragma unroll
+      for (int lc = 0; lc < 4; ++lc) {
+        const bf16x8 k8 = *(const bf16x8*)(krow + (((4 * h + lc) ^ (j & 7)) << 3));
+        float d = 0.f;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) d += q[lc * 8 + jj] * bf2f((bf16_t)k8[jj]);
+        d4[lc] = d;
+      }
+      const float sc = ((d4[0] + d4[1]) + (d4[2] + d4[3])) * scale;
       pr[j] = sc;
       mx = fmaxf(mx, sc);
     }
+    MDL_ATT_MARK(1);
     mx = group_max<lpi>(mx);
+    MDL_ATT_MARK(2);
     float sum = 0.f;
-    for (int j = u; j <= i; j += lpi) {
+#pragma unroll
+    for (int kk = 0; kk < KR; ++kk) {
+      const int j = u + kk * lpi;
+      const float pj = j <= i ? __expf(scr[kk] - mx) : 0.f;
+      if (j <= i) pr[j] = pj;
+      sum += pj;
+    }
+    for (int j = u + KR * lpi; j <= i; j += lpi) {
       const float pj = __expf(pr[j] - mx);
       pr[j] = pj;
       sum += pj;
     }
     sum = group_sum<lpi>(sum);
+    MDL_ATT_MARK(3);
     __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // PR written by this item's lanes (same wave)
+    MDL_ATT_MARK(4);
     float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
     const int lc = 4 * h + (dg >> 1), off = 4 * (dg & 1);
-    for (int j = kg; j <= i; j += nkg) {
-      const float pj = pr[j];
-      const bf16_t* vrow = KV + kv_off(b, kind + 1, m, j, 0, EPW, L) - ((0 ^ (j & 7)) << 3);
-      const uint2 v4 = *(const uint2*)(vrow + ((lc ^ (j & 7)) << 3) + off);
-      acc0 += pj * __uint_as_float(v4.x << 16);
-      acc1 += pj * __uint_as_float(v4.x & 0xFFFF0000u);
-      acc2 += pj * __uint_as_float(v4.y << 16);
-      acc3 += pj * __uint_as_float(v4.y & 0xFFFF0000u);
+    for (int j0 = kg; j0 <= i; j0 += 4 * nkg) {         // 4 keys per lane per trip: loads first, then FMAs
+      float pj[4];
+      uint2 v4[4];
+#pragma unroll
+      for (int uu = 0; uu < 4; ++uu) {
+        const int j = j0 + uu * nkg, jc = min(j, i);
+        pj[uu] = pr[jc];
+        const bf16_t* vrow = KV + kv_off(b, kind + 1, m, jc, 0, EPW, L) - ((0 ^ (jc & 7)) << 3);
+        v4[uu] = *(const uint2*)(vrow + ((lc ^ (jc & 7)) << 3) + off);
+      }
+#pragma unroll
+      for (int uu = 0; uu < 4; ++uu) {
+        const float w = j0 + uu * nkg <= i ? pj[uu] : 0.f;
+        acc0 += w * __uint_as_float(v4[uu].x << 16);
+        acc1 += w * __uint_as_float(v4[uu].x & 0xFFFF0000u);
+        acc2 += w * __uint_as_float(v4[uu].y << 16);
+        acc3 += w * __uint_as_float(v4[uu].y & 0xFFFF0000u);
+      }
     }
+    MDL_ATT_MARK(5);
     if (lpi > 8) {   // reduce over the key groups kg: lane ^ 8 (DPP row_ror:8), then lane ^ 16
       acc0 += dppf<DPP_ROW_ROR8>(acc0); acc1 += dppf<DPP_ROW_ROR8>(acc1);
       acc2 += dppf<DPP_ROW_ROR8>(acc2); acc3 += dppf<DPP_ROW_ROR8>(acc3);
@@ -199,20 +258,28 @@ __device__ __forceinline__ void attention_phase_t(const bf16_t* KV, const float*
       bf16_t* xa = XA + t * XP + 32 * h + 4 * dg;
       xa[0] = f2bf(acc0 * inv); xa[1] = f2bf(acc1 * inv); xa[2] = f2bf(acc2 * inv); xa[3] = f2bf(acc3 * inv);
     }
+    MDL_ATT_MARK(6);
   }
+  MDL_ATT_MARK(7);
 }
 
 __device__ __forceinline__ void attention_phase(const bf16_t* KV, const float* Q, float* PR, bf16_t* XA,
                                                 const int* ROWI, int R, int EPW, int L, int b, int kind,
-                                                float scale, int tid, int lpi) {
-  if (lpi == 32) attention_phase_t<32>(KV, Q, PR, XA, ROWI, R, EPW, L, b, kind, scale, tid);
-  else if (lpi == 16) attention_phase_t<16>(KV, Q, PR, XA, ROWI, R, EPW, L, b, kind, scale, tid);
-  else attention_phase_t<8>(KV, Q, PR, XA, ROWI, R, EPW, L, b, kind, scale, tid);
+                                                float scale, int tid, int lpi, int live) {
+#ifdef MDL_LPI_ONLY32   // code-size experiment: rollout-only build (stride-mode passes need 16 / 8)
+  attention_phase_t<32>(KV, Q, PR, XA, ROWI, R, EPW, L, b, kind, scale, tid, live);
+#else
+  if (lpi == 32) attention_phase_t<32>(KV, Q, PR, XA, ROWI, R, EPW, L, b, kind, scale, tid, live);
+  else if (lpi == 16) attention_phase_t<16>(KV, Q, PR, XA, ROWI, R, EPW, L, b, kind, scale, tid, live);
+  else attention_phase_t<8>(KV, Q, PR, XA, ROWI, R, EPW, L, b, kind, scale, tid, live);
+#endif
 }
 
 // Action head: LN(head1 output) · W_h2 + b -> logits; availability mask, sampling, log-prob (16 lanes per row).
 __device__ __forceinline__ void head_phase(const DecParams& p, const float* H1, float* LG, const float* lnh,
-                                           const int* ROWI, int* PEND, int R, int s, int e, int env0, int tid) {
+                                           const int* ROWI, int* PEND, int R, int s, int e, int env0, int tid,
+                                           const float* AVA, const float* RU, const float* RN, bool stage,
+                                           const float* wh2, const float* bh2) {
   const int t = tid >> 4, q = tid & 15;
   const int i = ROWI[t];
   const int AD = p.act_dim, L = p.L;
@@ -231,17 +298,18 @@ __device__ __forceinline__ void head_phase(const DecParams& p, const float* H1, 
 #pragma unroll
   for (int k = 0; k < 4; ++k) hn[k] = (v[k] - mean) * rstd * lnh[4 * q + k] + lnh[64 + 4 * q + k];
   for (int a = 0; a < AD; ++a) {
-    const float* w = p.wh2 + a * 64 + 4 * q;
+    const float* w = wh2 + a * 64 + 4 * q;
     float part = w[0] * hn[0] + w[1] * hn[1] + w[2] * hn[2] + w[3] * hn[3];
     part = group_sum<16>(part);
-    if (q == 0) LG[t * SP + a] = part + p.bh2[a];
+    if (q == 0) LG[t * SP + a] = part + bh2[a];
   }
   if (q != 0 || i < 0 || i < s || i >= e) return;
   const int m = t / R, env = env0 + m;
   const float* lg = LG + t * SP;
   const size_t oi = (size_t)env * L + i;
+  const size_t li = (size_t)m * L + i;                  // row in the staged (workgroup-local) inputs
   if (i < p.n_disc) {
-    const float* av = p.ava ? p.ava + oi * AD : nullptr;
+    const float* av = p.ava ? (stage ? AVA + li * AD : p.ava + oi * AD) : nullptr;
     float mx = -INFINITY;
     int amax = 0;
     for (int a = 0; a < AD; ++a) {
@@ -253,7 +321,7 @@ __device__ __forceinline__ void head_phase(const DecParams& p, const float* H1, 
     const float lse = mx + __logf(se);
     int act = amax;
     if (!p.deterministic) {
-      const float uu = p.rnd_u[oi];
+      const float uu = stage ? RU[li] : p.rnd_u[oi];
       float cdf = 0.f;
       int cnt = 0;
       for (int a = 0; a < AD; ++a) {
@@ -269,7 +337,7 @@ __device__ __forceinline__ void head_phase(const DecParams& p, const float* H1, 
   } else {
     const int a = AD - 1;
     const float mean_a = lg[a], sd = p.stdv[a];
-    const float x = p.deterministic ? mean_a : mean_a + sd * p.rnd_n[oi * AD + a];
+    const float x = p.deterministic ? mean_a : mean_a + sd * (stage ? RN[li * AD + a] : p.rnd_n[oi * AD + a]);
     const float z = (x - mean_a) / sd;
     p.out_a[oi] = x;
     p.out_lp[oi] = -0.5f * z * z - __logf(sd) - 0.91893853320467274f;
@@ -277,8 +345,21 @@ __device__ __forceinline__ void head_phase(const DecParams& p, const float* H1, 
   }
 }
 
+// Optional phase profiler (build with -DMDL_DECODE_PROF): thread 0 of workgroup 0 accumulates the core-clock
+// cycles between consecutive barriers per phase; read back with mdl_decode_prof_read.
+#ifdef MDL_DECODE_PROF
+__device__ unsigned long long g_decode_prof[16];
+#define MDL_PROF_MARK(k) do { if (prof_on) { const unsigned long long t_ = clock64(); prof[k] += t_ - prof_t; prof_t = t_; } } while (0)
+#else
+#define MDL_PROF_MARK(k) do { } while (0)
+#endif
+
 template <int NB>
 __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
+#ifdef MDL_DECODE_PROF
+  const bool prof_on = blockIdx.x == 0 && threadIdx.x == 0;
+  unsigned long long prof[16] = {0}, prof_t = clock64();
+#endif
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NG = 10 * NB + 1;
   constexpr int NLN = 3 * NB + 1;
@@ -302,6 +383,14 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
   int* TOK = (int*)ptr;     ptr += ((EPW * L * 4 + 15) & ~15);
   int* PEND = (int*)ptr;    ptr += ((EPW * L * 4 + 15) & ~15);
   int* ROWI = (int*)ptr;    ptr += 16 * 4;
+  float* REP = (float*)ptr;                                  // staged inputs (p.stage): [EPW][L][64]
+  auto pad4 = [](size_t n) { return (n + 3) & ~(size_t)3; };  // keep every region 16-byte aligned
+  float* AVA = REP + pad4((size_t)EPW * L * 64);             // [EPW][L][AD]
+  float* RU = AVA + pad4((size_t)EPW * L * AD);              // [EPW][L]
+  float* RN = RU + pad4((size_t)EPW * L);                    // [EPW][L][AD]
+  float* EMB = RN + pad4((size_t)EPW * L * AD);              // [n_tok][64] action-embedding rows (float4 reads)
+  float* WH2 = EMB + (size_t)p.n_tok * 64;                   // [AD][64], then bh2 [AD]
+  const bool stage = p.stage != 0;
 
   // ---------------------------------------------------------------- one-time loads
   bf16x8 wb[NG][2];
@@ -316,6 +405,21 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
   for (int gi = 0; gi < NG; ++gi) bcol[gi] = p.bias[gi * 64 + 16 * wave + c16];
   for (int i = tid; i < NLN * 128; i += 256) LNP[i] = p.lnp[i];
   for (int i = tid; i < EPW * L; i += 256) { TOK[i] = (i % L == 0) ? p.tok_start : p.tok_zero; PEND[i] = -1; }
+  for (int i = tid; i < 16 * XP; i += 256) XA[i] = 0;   // dead tile rows keep finite A-operand rows
+  if (stage) {   // the workgroup's envs are contiguous in every input
+    const int nrow = n_env * L;
+    const float4* src = (const float4*)(p.rep + (size_t)env0 * L * 64);
+    float4* dst = (float4*)REP;
+    for (int i = tid; i < nrow * 16; i += 256) dst[i] = src[i];
+    if (p.ava) for (int i = tid; i < nrow * AD; i += 256) AVA[i] = p.ava[(size_t)env0 * L * AD + i];
+    if (p.rnd_u) for (int i = tid; i < nrow; i += 256) RU[i] = p.rnd_u[(size_t)env0 * L + i];
+    if (p.rnd_n) for (int i = tid; i < nrow * AD; i += 256) RN[i] = p.rnd_n[(size_t)env0 * L * AD + i];
+    for (int i = tid; i < p.n_tok * 64; i += 256) EMB[i] = p.emb[i];
+    for (int i = tid; i < AD * 65; i += 256) WH2[i] = i < AD * 64 ? p.wh2[i] : p.bh2[i - AD * 64];
+  }
+  const float* emb = stage ? EMB : p.emb;
+  const float* wh2 = stage ? WH2 : p.wh2;
+  const float* bh2 = stage ? WH2 + AD * 64 : p.bh2;
   __syncthreads();
 
   const float scale = 0.17677669529663687f;  // 1/sqrt(32)
@@ -332,6 +436,7 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
         ROWI[tid] = (m < n_env && rr < R && tid < EPW * R) ? plo + rr : -1;
       }
       __syncthreads();
+      MDL_PROF_MARK(0);
       // per-lane tile rows for the C layout (rows 4*g4 + r) and the A layout (row c16)
       int crow_i[4], crow_m[4];
 #pragma unroll
@@ -347,7 +452,7 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
         // ---------------- [A] x = emb(token) (b == 0) or LN3(S) ; q1, k1, v1
         if (b == 0) {
           const float* row = nullptr;
-          if (arow_i >= 0) row = p.emb + (size_t)TOK[arow_m * L + arow_i] * 64;
+          if (arow_i >= 0) row = emb + (size_t)TOK[arow_m * L + arow_i] * 64;
           afrag_rowf(row, lane, a, xf);
         } else {
           afrag_ln(S, LNP + (3 * (b - 1) + 2) * 128, LNP + (3 * (b - 1) + 2) * 128 + 64, lane, a, xf);
@@ -369,9 +474,11 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
           }
         }
         __syncthreads();
+        MDL_PROF_MARK(1);
         // ---------------- [B] causal self-attention over cached rows 0..i
-        attention_phase(KV, Q, PR, XA, ROWI, R, EPW, L, b, 0, scale, tid, lpi);
+        attention_phase(KV, Q, PR, XA, ROWI, R, EPW, L, b, 0, scale, tid, lpi, live);
         __syncthreads();
+        MDL_PROF_MARK(2);
         // ---------------- [C] proj1 + bias + residual x -> S
         afrag_xa(XA, lane, a);
         {
@@ -384,12 +491,15 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
           }
         }
         __syncthreads();
+        MDL_PROF_MARK(3);
         // ---------------- [D] x1 = LN1(S); k2, v2 from x1; q2 from rep_i
         afrag_ln(S, LNP + (3 * b + 0) * 128, LNP + (3 * b + 0) * 128 + 64, lane, a, xf);
         {
           bf16x8 ar[2];
           float rf[16];
-          const float* rrow = arow_i >= 0 ? p.rep + ((size_t)(env0 + arow_m) * L + arow_i) * 64 : nullptr;
+          const float* rrow = arow_i < 0 ? nullptr
+                              : stage ? REP + ((size_t)arow_m * L + arow_i) * 64
+                                      : p.rep + ((size_t)(env0 + arow_m) * L + arow_i) * 64;
           afrag_rowf(rrow, lane, ar, rf);
           f32x4 k2 = mfma2(a, wb[b * 10 + 5], f32x4{0, 0, 0, 0});
           f32x4 v2 = mfma2(a, wb[b * 10 + 6], f32x4{0, 0, 0, 0});
@@ -406,9 +516,11 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
           }
         }
         __syncthreads();
+        MDL_PROF_MARK(4);
         // ---------------- [E] causal cross-attention (q = rep rows, k/v = x1 rows)
-        attention_phase(KV, Q, PR, XA, ROWI, R, EPW, L, b, 2, scale, tid, lpi);
+        attention_phase(KV, Q, PR, XA, ROWI, R, EPW, L, b, 2, scale, tid, lpi, live);
         __syncthreads();
+        MDL_PROF_MARK(5);
         // ---------------- [F] proj2 + bias + rep_i -> S
         afrag_xa(XA, lane, a);
         {
@@ -418,11 +530,14 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
           for (int r = 0; r < 4; ++r) {
             const int row = 4 * g4 + r;
             float res = 0.f;
-            if (crow_i[r] >= 0) res = p.rep[((size_t)(env0 + crow_m[r]) * L + crow_i[r]) * 64 + col];
+            if (crow_i[r] >= 0)
+              res = stage ? REP[((size_t)crow_m[r] * L + crow_i[r]) * 64 + col]
+                          : p.rep[((size_t)(env0 + crow_m[r]) * L + crow_i[r]) * 64 + col];
             S[row * SP + col] = acc[r] + bcol[b * 10 + 7] + res;
           }
         }
         __syncthreads();
+        MDL_PROF_MARK(6);
         // ---------------- [G] x2 = LN2(S) -> XR ; h = GELU(mlp1(x2)) -> XA
         afrag_ln(S, LNP + (3 * b + 1) * 128, LNP + (3 * b + 1) * 128 + 64, lane, a, xf);
         if (wave == 0) store_xf(XR, lane, xf);
@@ -433,6 +548,7 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
           for (int r = 0; r < 4; ++r) XA[(4 * g4 + r) * XP + col] = f2bf(gelu_erf(acc[r] + bcol[b * 10 + 8]));
         }
         __syncthreads();
+        MDL_PROF_MARK(7);
         // ---------------- [H] mlp2 + bias + residual x2 -> S
         afrag_xa(XA, lane, a);
         {
@@ -445,6 +561,7 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
           }
         }
         __syncthreads();
+        MDL_PROF_MARK(8);
       }
       // ---------------- [I] head1: GELU(W_h1 · LN3(S) + b) -> Q (f32 staging)
       {
@@ -457,9 +574,11 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
         for (int r = 0; r < 4; ++r) Q[(4 * g4 + r) * SP + col] = gelu_erf(acc[r] + bcol[NG - 1]);
       }
       __syncthreads();
+      MDL_PROF_MARK(9);
       // ---------------- [J] head LN + W_h2 -> logits; mask, sample, log-prob; record pending tokens
-      head_phase(p, Q, S, LNP + 3 * NB * 128, ROWI, PEND, R, s, e, env0, tid);
+      head_phase(p, Q, S, LNP + 3 * NB * 128, ROWI, PEND, R, s, e, env0, tid, AVA, RU, RN, stage, wh2, bh2);
       __syncthreads();
+      MDL_PROF_MARK(10);
     }
     // apply the block's actions to the token rows of the next passes (in-block rows kept at zero, as the reference)
     for (int idx = tid; idx < n_env * L; idx += 256) {
@@ -470,11 +589,30 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
       }
     }
     __syncthreads();
+    MDL_PROF_MARK(11);
     prev_s = s;
     if (e >= L) break;
     if (e < p.n_disc) { s = e; e = min(e + p.stride, p.n_disc); }
     else { s = e; e = min(e + 1, L); }
   }
+#ifdef MDL_DECODE_PROF
+  if (prof_on)
+    for (int k = 0; k < 16; ++k) g_decode_prof[k] = prof[k];
+#endif
+}
+
+#ifdef MDL_DECODE_PROF
+MDL_API int mdl_decode_prof_read(unsigned long long* out) {
+  int rc = (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_decode_prof), sizeof(unsigned long long) * 16, 0,
+                                    hipMemcpyDeviceToHost);
+  if (rc == 0) rc = (int)hipMemcpyFromSymbol(out + 16, HIP_SYMBOL(g_attn_prof), sizeof(unsigned long long) * 8, 0,
+                                             hipMemcpyDeviceToHost);
+  return rc;
+}
+#endif
+
+size_t mat_decode_stage_bytes(int epw, int L, int AD, int n_tok) {
+  return ((size_t)epw * L * (64 + 2 * AD + 1) + (size_t)n_tok * 64 + (size_t)AD * 65) * 4 + 64;   // + padding
 }
 
 size_t mat_decode_lds_bytes(int NB, int epw, int rmax, int L) {
@@ -505,9 +643,16 @@ MDL_API int mdl_mat_decode(const DecParams* p, int NB, hipStream_t st) {
   const int epw = p->epw;
   if (epw <= 0 || p->act_dim > 64 || p->act_dim < 1) return -1;
   if (p->rmax < 1 || p->rmax * epw > 16) return -4;
-  const size_t lds = mat_decode_lds_bytes(NB, epw, p->rmax, p->L);
+  size_t lds = mat_decode_lds_bytes(NB, epw, p->rmax, p->L);
   if (lds > 160 * 1024) return -2;
   const int grid = (p->B + epw - 1) / epw;
+  // stage the per-row inputs in LDS when they fit next to the KV caches (MAT_DCML_DECODE_STAGE=0 disables)
+  DecParams q = *p;
+  static const bool stage_ok = [] { const char* e = getenv("MAT_DCML_DECODE_STAGE"); return !(e && e[0] == '0'); }();
+  const size_t sb = mat_decode_stage_bytes(epw, p->L, p->act_dim, p->n_tok);
+  q.stage = stage_ok && lds + sb <= 160 * 1024 && (p->rep != nullptr);
+  if (q.stage) lds += sb;
+  p = &q;
   switch (NB) {
     case 1:
       hipFuncSetAttribute((const void*)mat_decode_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

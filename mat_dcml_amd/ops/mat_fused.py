@@ -24,7 +24,7 @@ class DecParams(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in ("wpack", "bias", "lnp", "emb", "wh2", "bh2", "stdv", "rep", "ava",
                                                "rnd_u", "rnd_n", "out_a", "out_lp")] + \
                [(n, ctypes.c_int) for n in ("B", "L", "act_dim", "n_disc", "stride", "deterministic", "epw", "rmax", "n_tok",
-                                            "tok_start", "tok_zero")]
+                                            "tok_start", "tok_zero", "stage")]
 
 
 sig("mdl_mat_decode", ctypes.POINTER(DecParams), i32, vp)
@@ -120,7 +120,7 @@ def decode(model, rep, ava=None, deterministic=False, stride=1, rand=None):
                     P(pk["wh2"]).value, P(pk["bh2"]).value, P(pk["stdv"]).value, P(rep).value, P(ava_c).value,
                     P(u).value, P(n).value, P(out_a).value, P(out_lp).value,
                     B, L, A, _n_disc(model, L), int(stride if deterministic else 1), int(bool(deterministic)), epw, rmax,
-                    pk["n_tok"], 0, A + 1)
+                    pk["n_tok"], 0, A + 1, 0)
     check(lib().mdl_mat_decode(ctypes.byref(prm), model.n_block, kernels._stream()), "mat_decode")
     return out_a.unsqueeze(-1), out_lp.unsqueeze(-1)
 
