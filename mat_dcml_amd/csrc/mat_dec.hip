@@ -101,6 +101,7 @@ __device__ __forceinline__ void attn_cross_bwd(const Mat* m, const LNp& ln, RT* 
                                                const bf16_t* sv_x1, const bf16_t* sv_a, const float* sv_lse,
                                                const Ctx& c) {
   const int lane = c.lane;
+  TP_DECL();
   f32x4 dlg = {0, 0, 0, 0}, dlb = {0, 0, 0, 0}, dbp = {0, 0, 0, 0};
   RT dres[MAXRT];
   {
@@ -137,8 +138,10 @@ __device__ __forceinline__ void attn_cross_bwd(const Mat* m, const LNp& ln, RT* 
   flush_ln(dlg, dlb, ln, c);
   flush_cols(dbp, c.g(m[7].db), lane);
   __syncthreads();
+  TP_MARK(7);
   wgrad_tm(c.DQ, c.XB, c.NRP, c.g(m[7].dW), c.wave, lane);
   __syncthreads();
+  TP_MARK(12);
   // recompute k, v (from x1) and q (from rep)
   g2lds_rows(c.XB, sv_x1, c.tok0, c.NR, c.NT * 16, c.tid);
   load_lse(sv_lse, c);
@@ -189,10 +192,13 @@ __device__ __forceinline__ void attn_cross_bwd(const Mat* m, const LNp& ln, RT* 
     }
   }
   __syncthreads();
+  TP_MARK(13);
   attn_bwd_q(c.QB, c.KB, c.VB, c.DA, c.DQ, true, c);
   __syncthreads();
+  TP_MARK(14);
   attn_bwd_kv(c.QB, c.KB, c.VB, c.DA, true, c);
   __syncthreads();
+  TP_MARK(15);
   // q input (rep) back into QB for dW_q
 #pragma unroll
   for (int k = 0; k < MAXRT; ++k) {
@@ -207,6 +213,7 @@ __device__ __forceinline__ void attn_cross_bwd(const Mat* m, const LNp& ln, RT* 
   wgrad_tm(c.DQ, c.QB, c.NRP, c.g(m[4].dW), c.wave, lane);
   wgrad_tm(c.KB, c.XB, c.NRP, c.g(m[5].dW), c.wave, lane);
   wgrad_tm(c.VB, c.XB, c.NRP, c.g(m[6].dW), c.wave, lane);
+  TP_MARK(17);
   // d x1 = dk Wk + dv Wv ;  d rep += ds + dq Wq
   const bf16_t* dsrc[3] = {c.DQ, c.KB, c.VB};
 #pragma unroll
@@ -282,6 +289,31 @@ __device__ __forceinline__ float mask_logit(const DecP& p, int tok, int a, float
   return (p.ava && p.ava[(size_t)tok * p.A + a] == 0.f) ? -1e10f : l;
 }
 
+// Per-row head inputs of one row tile (this lane's 4 C-layout rows), loaded at the top of the tile iteration so
+// their L2 / HBM latency hides behind the head GEMM, GELU and LayerNorm instead of stalling the softmax (the
+// section profiler put the head at 17 % of the decoder backward): availability as a bitmask, the taken action,
+// and (backward) the log-prob / entropy gradients.
+struct HeadRows { float act[4], dlp[4], den[4]; unsigned am[4]; };
+__device__ __forceinline__ void head_rows(const DecP& p, const Ctx& c, int rt, int g, bool grads, HeadRows& h) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = rt * 16 + 4 * g + r;
+    const bool ok = row < c.NR;
+    const int tok = c.tok0 + (ok ? row : 0);
+    h.act[r] = p.act[tok];
+    h.dlp[r] = grads && ok ? p.dlogp[tok] : 0.f;
+    h.den[r] = grads && ok ? p.dent[tok] : 0.f;
+    unsigned am = 0;
+    if (p.ava) {
+#pragma unroll
+      for (int a = 0; a < 8; ++a)
+        if (a < p.A && p.ava[(size_t)tok * p.A + a] == 0.f) am |= 1u << a;
+    }
+    h.am[r] = am;
+  }
+}
+__device__ __forceinline__ float mask_logit_m(unsigned am, int a, float l) { return ((am >> a) & 1u) ? -1e10f : l; }
+
 // ============================================================================================== decoder forward
 template <int NB, bool SAVE>
 __device__ __forceinline__ void mat_dec_fwd_tile(const DecP& p, char* smem, int seq0, int nseq) {
@@ -318,6 +350,8 @@ __device__ __forceinline__ void mat_dec_fwd_tile(const DecP& p, char* smem, int 
   for (int k = 0; k < MAXRT; ++k) {
     const int rt = c.wave + 4 * k;
     if (rt < c.NT) {
+      HeadRows hr;
+      head_rows(p, c, rt, g, false, hr);
       st_tm_m(c.XB, rt, xr[k], row_mask(rt, c.NR, lane), lane);
       if (SAVE) { wave_lds_sync(); tile2g(p.sv_head, c.XB, rt, c); }
       wave_lds_sync();
@@ -339,17 +373,17 @@ __device__ __forceinline__ void mat_dec_fwd_tile(const DecP& p, char* smem, int 
           if (i < p.n_disc) {
             float mx = -INFINITY;
 #pragma unroll
-            for (int a = 0; a < 8; ++a) if (a < p.A) mx = fmaxf(mx, mask_logit(p, tok, a, lg[a][r]));
+            for (int a = 0; a < 8; ++a) if (a < p.A) mx = fmaxf(mx, mask_logit_m(hr.am[r], a, lg[a][r]));
             float se = 0.f;
 #pragma unroll
-            for (int a = 0; a < 8; ++a) if (a < p.A) se += __expf(mask_logit(p, tok, a, lg[a][r]) - mx);
+            for (int a = 0; a < 8; ++a) if (a < p.A) se += __expf(mask_logit_m(hr.am[r], a, lg[a][r]) - mx);
             const float lse = mx + __logf(se);
-            const int act = min(max((int)p.act[tok], 0), p.A - 1);
+            const int act = min(max((int)hr.act[r], 0), p.A - 1);
             float H = 0.f, la = 0.f;
 #pragma unroll
             for (int a = 0; a < 8; ++a) {
               if (a < p.A) {
-                const float l = mask_logit(p, tok, a, lg[a][r]) - lse;
+                const float l = mask_logit_m(hr.am[r], a, lg[a][r]) - lse;
                 const float pr = __expf(l);
                 H -= pr * l;
                 if (a == act) la = l;
@@ -362,7 +396,7 @@ __device__ __forceinline__ void mat_dec_fwd_tile(const DecP& p, char* smem, int 
             float mean = 0.f;
 #pragma unroll
             for (int aa = 0; aa < 8; ++aa) if (aa == a) mean = lg[aa][r];
-            const float sd = p.stdv[a], z = (p.act[tok] - mean) / sd;
+            const float sd = p.stdv[a], z = (hr.act[r] - mean) / sd;
             lp = -0.5f * z * z - __logf(sd) - 0.91893853320467274f;
             en = 0.5f + 0.91893853320467274f + __logf(sd);
           }
@@ -385,6 +419,7 @@ template <int NB>
 __device__ __forceinline__ void mat_dec_bwd_tile(const DecP& p, char* smem, int seq0, int nseq) {
   const Ctx c = make_ctx(p, smem, seq0, nseq);
   if (c.nseq <= 0) return;
+  TP_DECL();
   zero_lds(smem, mat_train_lds_bytes(p.NRP, p.SQ, p.L), c.tid);
   __syncthreads();
   const int lane = c.lane, g = lane >> 4, c16 = lane & 15;
@@ -403,6 +438,8 @@ __device__ __forceinline__ void mat_dec_bwd_tile(const DecP& p, char* smem, int 
     for (int k = 0; k < MAXRT; ++k) {
       const int rt = c.wave + 4 * k;
       if (rt < c.NT) {
+        HeadRows hr;
+        head_rows(p, c, rt, g, true, hr);
         const f32x4 vm = row_mask(rt, c.NR, lane);
         g2tile(c.XB, p.sv_head, rt, c);
         wave_lds_sync();
@@ -421,31 +458,31 @@ __device__ __forceinline__ void mat_dec_bwd_tile(const DecP& p, char* smem, int 
           const int row = rt * 16 + 4 * g + r;
           const bool ok = row < c.NR;
           const int tok = c.tok0 + (ok ? row : 0), i = row % c.L;
-          const float dlp = ok ? p.dlogp[tok] : 0.f, den = ok ? p.dent[tok] : 0.f;
+          const float dlp = hr.dlp[r], den = hr.den[r];
 #pragma unroll
           for (int a = 0; a < 8; ++a) dz[a][r] = 0.f;
           if (!ok) continue;
           if (i < p.n_disc) {
             float mx = -INFINITY;
 #pragma unroll
-            for (int a = 0; a < 8; ++a) if (a < p.A) mx = fmaxf(mx, mask_logit(p, tok, a, lg[a][r]));
+            for (int a = 0; a < 8; ++a) if (a < p.A) mx = fmaxf(mx, mask_logit_m(hr.am[r], a, lg[a][r]));
             float se = 0.f;
 #pragma unroll
-            for (int a = 0; a < 8; ++a) if (a < p.A) se += __expf(mask_logit(p, tok, a, lg[a][r]) - mx);
+            for (int a = 0; a < 8; ++a) if (a < p.A) se += __expf(mask_logit_m(hr.am[r], a, lg[a][r]) - mx);
             const float lse = mx + __logf(se);
-            const int act = min(max((int)p.act[tok], 0), p.A - 1);
+            const int act = min(max((int)hr.act[r], 0), p.A - 1);
             float H = 0.f;
 #pragma unroll
             for (int a = 0; a < 8; ++a) {
               if (a < p.A) {
-                const float l = mask_logit(p, tok, a, lg[a][r]) - lse;
+                const float l = mask_logit_m(hr.am[r], a, lg[a][r]) - lse;
                 H -= __expf(l) * l;
               }
             }
 #pragma unroll
             for (int a = 0; a < 8; ++a) {
               if (a < p.A) {
-                const float l = mask_logit(p, tok, a, lg[a][r]) - lse;
+                const float l = mask_logit_m(hr.am[r], a, lg[a][r]) - lse;
                 const float pr = __expf(l);
                 dz[a][r] = dlp * ((a == act ? 1.f : 0.f) - pr) - den * pr * (l + H);
               }
@@ -455,7 +492,7 @@ __device__ __forceinline__ void mat_dec_bwd_tile(const DecP& p, char* smem, int 
             float mean = 0.f;
 #pragma unroll
             for (int aa = 0; aa < 8; ++aa) if (aa == a) mean = lg[aa][r];
-            const float sd = p.stdv[a], diff = p.act[tok] - mean;
+            const float sd = p.stdv[a], diff = hr.act[r] - mean;
 #pragma unroll
             for (int aa = 0; aa < 8; ++aa) if (aa == a) dz[aa][r] = dlp * diff / (sd * sd);
             if (c16 == 0) {
@@ -512,15 +549,20 @@ __device__ __forceinline__ void mat_dec_bwd_tile(const DecP& p, char* smem, int 
     wgrad_tm(c.DQ, c.XB, c.NRP, c.g(p.h1.dW), c.wave, lane);
     __syncthreads();
   }
+  TP_MARK(11);
   // ---------------- blocks in reverse
 #pragma unroll 1
   for (int bb = NB - 1; bb >= 0; --bb) {
     const Blk& B = p.blk[bb];
     Ctx cc = c;
     asm volatile("" : "+v"(cc.lane), "+v"(cc.tid));
+    TP_DECL();
     mlp_bwd(B.m[8], B.m[9], B.ln[2], dx, p.sv[bb].x2, p.sv[bb].h, cc);
+    TP_MARK(8);
     attn_cross_bwd(B.m, B.ln[1], dx, p.rep, p.drep, p.sv[bb].x1, p.sv[bb].a2, p.sv[bb].lse2, cc);
+    TP_MARK(9);
     attn_self_bwd(B.m, B.ln[0], dx, p.sv[bb].xin, p.sv[bb].a1, p.sv[bb].lse1, true, cc);
+    TP_MARK(10);
   }
   // ---------------- embedding backward: dW_a[:, token] += dpre ; LN_dec params
   {
@@ -582,3 +624,9 @@ MDL_API int MDL_V(mdl_mat_dec_bwd)(const DecP* p, int NB, hipStream_t st) {
   if (NB == 3) return launch(MDL_V(mat_dec_bwd)<3>, p, st);
   return -3;
 }
+
+#ifdef MDL_TRAIN_PROF
+MDL_API int mdl_dec_prof_read(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tprof), sizeof(unsigned long long) * 32, 0, hipMemcpyDeviceToHost);
+}
+#endif

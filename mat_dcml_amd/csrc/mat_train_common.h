@@ -36,6 +36,17 @@ namespace {
 #ifndef MDL_WGPC
 #define MDL_WGPC 1   // resident workgroups per CU the kernels are sized for (LDS budget, register cap, grid)
 #endif
+// Optional section profiler (-DMDL_TRAIN_PROF): thread 0 of workgroup 0 accumulates core-clock cycles per code
+// section into g_tprof (read back by mdl_*_prof_read); each mark costs one global read-modify-write.
+#ifdef MDL_TRAIN_PROF
+__device__ unsigned long long g_tprof[32];
+#define TP_DECL() bool tp_on_ = blockIdx.x == 0 && threadIdx.x == 0; unsigned long long tp_t_ = clock64()
+#define TP_MARK(k) do { if (tp_on_) { const unsigned long long t_ = clock64(); g_tprof[k] += t_ - tp_t_; tp_t_ = t_; } } while (0)
+#else
+#define TP_DECL() do { } while (0)
+#define TP_MARK(k) do { } while (0)
+#endif
+
 constexpr int MAXRT = MDL_MAXRT;  // row tiles per wave (NT <= 4 * MAXRT)
 constexpr int WGPC = MDL_WGPC;
 constexpr int LDS_BUDGET = 160 * 1024 / WGPC;
@@ -685,6 +696,7 @@ __device__ __forceinline__ void mlp_bwd(const Mat& m1, const Mat& m2, const LNp&
 __device__ __forceinline__ void attn_self_bwd(const Mat* m, const LNp& ln, RT* dx, const bf16_t* sv_xin, const bf16_t* sv_a,
                               const float* sv_lse, bool causal, const Ctx& c) {
   const int lane = c.lane;
+  TP_DECL();
   f32x4 dlg = {0, 0, 0, 0}, dlb = {0, 0, 0, 0}, dbp = {0, 0, 0, 0};
   {
     BFr Bpf, Bpb;
@@ -719,8 +731,10 @@ __device__ __forceinline__ void attn_self_bwd(const Mat* m, const LNp& ln, RT* d
   flush_ln(dlg, dlb, ln, c);
   flush_cols(dbp, c.g(m[3].db), lane);
   __syncthreads();
+  TP_MARK(0);
   wgrad_tm(c.DQ, c.XB, c.NRP, c.g(m[3].dW), c.wave, lane);
   __syncthreads();
+  TP_MARK(1);
   // recompute q, k, v from the saved input (whole tile, cooperative copy)
   g2lds_rows(c.XB, sv_xin, c.tok0, c.NR, c.NT * 16, c.tid);
   load_lse(sv_lse, c);
@@ -744,13 +758,17 @@ __device__ __forceinline__ void attn_self_bwd(const Mat* m, const LNp& ln, RT* d
     }
   }
   __syncthreads();
+  TP_MARK(2);
   attn_bwd_q(c.QB, c.KB, c.VB, c.DA, c.DQ, causal, c);
   __syncthreads();
+  TP_MARK(3);
   attn_bwd_kv(c.QB, c.KB, c.VB, c.DA, causal, c);
   __syncthreads();
+  TP_MARK(4);
   wgrad_tm(c.DQ, c.XB, c.NRP, c.g(m[0].dW), c.wave, lane);
   wgrad_tm(c.KB, c.XB, c.NRP, c.g(m[1].dW), c.wave, lane);
   wgrad_tm(c.VB, c.XB, c.NRP, c.g(m[2].dW), c.wave, lane);
+  TP_MARK(5);
   const bf16_t* dsrc[3] = {c.DQ, c.KB, c.VB};
 #pragma unroll
   for (int mi = 0; mi < 3; ++mi) {
@@ -773,6 +791,7 @@ __device__ __forceinline__ void attn_self_bwd(const Mat* m, const LNp& ln, RT* d
     flush_cols(dbb, c.g(m[mi].db), lane);
   }
   __syncthreads();
+  TP_MARK(6);
 }
 
 // ------------------------------------------------------------------------------------------ context
