@@ -94,19 +94,8 @@ __device__ __forceinline__ void mat_enc_bwd_tile(const EncP& p, char* smem, int 
       const int rt = c.wave + 4 * k;
       if (rt < c.NT) {
         const f32x4 vm = row_mask(rt, c.NR, lane);
-        // every per-row global input of this row tile is requested up front: the value gradients and the
-        // incoming d rep then arrive while the head GEMM / GELU / LayerNorm run, instead of stalling after them
-        f32x4 dvv2[2];
-#pragma unroll
-        for (int o = 0; o < 2; ++o)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = rt * 16 + 4 * g + r;
-            dvv2[o][r] = (o < p.n_obj && row < c.NR) ? p.dv[(size_t)(c.tok0 + row) * p.n_obj + o] : 0.f;
-          }
-        RT rep, dr;
+        RT rep;
         ld_g_f(p.rep, c.tok0, rt, c.NR, rep, lane);
-        ld_g_f(p.drep, c.tok0, rt, c.NR, dr, lane);
         st_tm_m(c.XB, rt, rep, vm, lane);   // X of dW_h1
         wave_lds_sync();
         RT hh, gl, xh, n, dn, dg;
@@ -120,7 +109,12 @@ __device__ __forceinline__ void mat_enc_bwd_tile(const EncP& p, char* smem, int 
 #pragma unroll
         for (int o = 0; o < 2; ++o) {
           if (o >= p.n_obj) break;
-          const f32x4 dvv = dvv2[o];
+          f32x4 dvv;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = rt * 16 + 4 * g + r;
+            dvv[r] = row < c.NR ? p.dv[(size_t)(c.tok0 + row) * p.n_obj + o] : 0.f;
+          }
 #pragma unroll
           for (int ct = 0; ct < 4; ++ct) {
             const float w = p.wh2[o * 64 + 16 * ct + c16];
@@ -139,8 +133,9 @@ __device__ __forceinline__ void mat_enc_bwd_tile(const EncP& p, char* smem, int 
         colsum_acc(dg, dbh, vm);
         st_tm_m(c.DQ, rt, dg, vm, lane);    // dY of dW_h1
         wave_lds_sync();
-        RT t;
+        RT t, dr;
         gemm_rt(t, c.DQ, rt, Bb, lane, false);
+        ld_g_f(p.drep, c.tok0, rt, c.NR, dr, lane);
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct) dx[k].v[ct] = dr.v[ct] + t.v[ct];
       }
