@@ -44,6 +44,11 @@ struct DecParams {
   float* out_lp;         // [B][L]
   int B, L, act_dim, n_disc, stride, deterministic, epw, rmax, n_tok, tok_start, tok_zero;
   int stage;             // 1: rep / ava / draws of the workgroup's envs are staged in LDS at kernel start
+  int cont;              // 1: "Continuous" action type — every agent samples act_dim Gaussians and the next
+                         //    row's input is LN(GELU(W_a · x + b_a)) of the sampled vector (not a token row)
+  const float* wa;       // [64][act_dim] action-encoder weight (cont)
+  const float* ba;       // [64] action-encoder bias (cont)
+  const float* lnd;      // [2][64] decoder input LayerNorm (cont)
 };
 
 constexpr int SP = 68;   // f32 staging row pitch (floats)
@@ -279,7 +284,7 @@ __device__ __forceinline__ void attention_phase(const bf16_t* KV, const float* Q
 __device__ __forceinline__ void head_phase(const DecParams& p, const float* H1, float* LG, const float* lnh,
                                            const int* ROWI, int* PEND, int R, int s, int e, int env0, int tid,
                                            const float* AVA, const float* RU, const float* RN, bool stage,
-                                           const float* wh2, const float* bh2) {
+                                           const float* wh2, const float* bh2, float* EROW) {
   const int t = tid >> 4, q = tid & 15;
   const int i = ROWI[t];
   const int AD = p.act_dim, L = p.L;
@@ -302,6 +307,42 @@ __device__ __forceinline__ void head_phase(const DecParams& p, const float* H1, 
     float part = w[0] * hn[0] + w[1] * hn[1] + w[2] * hn[2] + w[3] * hn[3];
     part = group_sum<16>(part);
     if (q == 0) LG[t * SP + a] = part + bh2[a];
+  }
+  if (p.cont) {   // all act_dim dims are Gaussian; the 16 lanes of the row also build the next row's input
+    if (i < 0 || i < s || i >= e) return;
+    const int m = t / R;
+    const size_t oi = (size_t)(env0 + m) * L + i, li = (size_t)m * L + i;
+    const float* lg = LG + t * SP;
+    float ev[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ev[k] = p.ba[4 * q + k];
+    for (int a = 0; a < AD; ++a) {
+      const float mean_a = lg[a], sd = p.stdv[a];
+      const float x = p.deterministic ? mean_a : mean_a + sd * (stage ? RN[li * AD + a] : p.rnd_n[oi * AD + a]);
+      if (q == 0) {
+        const float z = (x - mean_a) / sd;
+        p.out_a[oi * AD + a] = x;
+        p.out_lp[oi * AD + a] = -0.5f * z * z - __logf(sd) - 0.91893853320467274f;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ev[k] += p.wa[(4 * q + k) * AD + a] * x;
+    }
+    if (i + 1 >= L) return;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ev[k] = gelu_erf(ev[k]);
+    float es = group_sum<16>(ev[0] + ev[1] + ev[2] + ev[3]);
+    const float emean = es * (1.f / 64.f);
+    float eq = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { const float d = ev[k] - emean; eq += d * d; }
+    eq = group_sum<16>(eq);
+    const float erstd = rsqrtf(eq * (1.f / 64.f) + 1e-5f);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int cidx = 4 * q + k;
+      EROW[m * 64 + cidx] = (ev[k] - emean) * erstd * p.lnd[cidx] + p.lnd[64 + cidx];
+    }
+    return;
   }
   if (q != 0 || i < 0 || i < s || i >= e) return;
   const int m = t / R, env = env0 + m;
@@ -383,6 +424,7 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
   int* TOK = (int*)ptr;     ptr += ((EPW * L * 4 + 15) & ~15);
   int* PEND = (int*)ptr;    ptr += ((EPW * L * 4 + 15) & ~15);
   int* ROWI = (int*)ptr;    ptr += 16 * 4;
+  float* EROW = (float*)ptr; ptr += EPW * 64 * 4;            // cont: next row's input embedding per env
   float* REP = (float*)ptr;                                  // staged inputs (p.stage): [EPW][L][64]
   auto pad4 = [](size_t n) { return (n + 3) & ~(size_t)3; };  // keep every region 16-byte aligned
   float* AVA = REP + pad4((size_t)EPW * L * 64);             // [EPW][L][AD]
@@ -452,7 +494,8 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
         // ---------------- [A] x = emb(token) (b == 0) or LN3(S) ; q1, k1, v1
         if (b == 0) {
           const float* row = nullptr;
-          if (arow_i >= 0) row = emb + (size_t)TOK[arow_m * L + arow_i] * 64;
+          if (arow_i >= 0)
+            row = (p.cont && arow_i > 0) ? EROW + arow_m * 64 : emb + (size_t)TOK[arow_m * L + arow_i] * 64;
           afrag_rowf(row, lane, a, xf);
         } else {
           afrag_ln(S, LNP + (3 * (b - 1) + 2) * 128, LNP + (3 * (b - 1) + 2) * 128 + 64, lane, a, xf);
@@ -576,7 +619,7 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
       __syncthreads();
       MDL_PROF_MARK(9);
       // ---------------- [J] head LN + W_h2 -> logits; mask, sample, log-prob; record pending tokens
-      head_phase(p, Q, S, LNP + 3 * NB * 128, ROWI, PEND, R, s, e, env0, tid, AVA, RU, RN, stage, wh2, bh2);
+      head_phase(p, Q, S, LNP + 3 * NB * 128, ROWI, PEND, R, s, e, env0, tid, AVA, RU, RN, stage, wh2, bh2, EROW);
       __syncthreads();
       MDL_PROF_MARK(10);
     }
@@ -619,7 +662,7 @@ size_t mat_decode_lds_bytes(int NB, int epw, int rmax, int L) {
   size_t kv = (size_t)NB * 4 * epw * L * 64 * 2;
   kv = (kv + 15) & ~(size_t)15;
   size_t rest = 3 * 16 * SP * 4 + 16 * XP * 2 + (3 * NB + 1) * 128 * 4 + ((epw * rmax * 2 * L * 4 + 15) & ~15) +
-                2 * ((epw * L * 4 + 15) & ~15) + 16 * 4;
+                2 * ((epw * L * 4 + 15) & ~15) + 16 * 4 + (size_t)epw * 64 * 4;
   return kv + rest;
 }
 
@@ -642,6 +685,7 @@ MDL_API int mdl_mat_decode_geometry(int NB, int L, int B) {
 MDL_API int mdl_mat_decode(const DecParams* p, int NB, hipStream_t st) {
   const int epw = p->epw;
   if (epw <= 0 || p->act_dim > 64 || p->act_dim < 1) return -1;
+  if (p->cont && (!p->wa || !p->ba || !p->lnd || p->n_disc != 0)) return -5;
   if (p->rmax < 1 || p->rmax * epw > 16) return -4;
   size_t lds = mat_decode_lds_bytes(NB, epw, p->rmax, p->L);
   if (lds > 160 * 1024) return -2;

@@ -24,23 +24,30 @@ class DecParams(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in ("wpack", "bias", "lnp", "emb", "wh2", "bh2", "stdv", "rep", "ava",
                                                "rnd_u", "rnd_n", "out_a", "out_lp")] + \
                [(n, ctypes.c_int) for n in ("B", "L", "act_dim", "n_disc", "stride", "deterministic", "epw", "rmax", "n_tok",
-                                            "tok_start", "tok_zero", "stage")]
+                                            "tok_start", "tok_zero", "stage", "cont")] + \
+               [(n, ctypes.c_void_p) for n in ("wa", "ba", "lnd")]
 
 
 sig("mdl_mat_decode", ctypes.POINTER(DecParams), i32, vp)
 sig("mdl_mat_decode_geometry", i32, i32, i32)
 
 
+def _is_cont(model):
+    return model.action_type in ("Continuous", "Continous")
+
+
 def _n_disc(model, L):
     if model.action_type == "Discrete":
         return L
+    if _is_cont(model):
+        return 0
     return L + model.semi_index if model.semi_index < 0 else model.semi_index
 
 
 def supports(model, L=None) -> bool:
     if not kernels.available():
         return False
-    if model.action_type not in ("Semi_Discrete", "Discrete") or model.decoder.dec_actor:
+    if model.action_type not in ("Semi_Discrete", "Discrete", "Continuous", "Continous") or model.decoder.dec_actor:
         return False
     if model.n_embd != 64 or model.n_head != 2 or model.n_block not in (1, 2, 3) or model.action_dim > 64:
         return False
@@ -84,16 +91,27 @@ def decoder_pack(model):
     lns.append(torch.stack([dec.head[2].weight.detach(), dec.head[2].bias.detach()]))
     A = model.action_dim
     dev = dec.ln.weight.device
-    # token table: 0 = start [1,0..], 1+a = one-hot action a, A+1 = zero row (in-block rows of the stride mode)
-    toks = torch.zeros(A + 2, A + 1, device=dev)
-    toks[0, 0] = 1
-    toks[torch.arange(1, A + 1), torch.arange(1, A + 1)] = 1
+    cont = _is_cont(model)
+    if cont:
+        # continuous inputs: row 0 = the zero start action; later rows are built in-kernel from the sampled vector
+        toks = torch.zeros(2, A, device=dev)
+        tok_start, tok_zero = 0, 1
+    else:
+        # token table: 0 = start [1,0..], 1+a = one-hot action a, A+1 = zero row (in-block rows of the stride mode)
+        toks = torch.zeros(A + 2, A + 1, device=dev)
+        toks[0, 0] = 1
+        toks[torch.arange(1, A + 1), torch.arange(1, A + 1)] = 1
+        tok_start, tok_zero = 0, A + 1
     emb = dec.ln(dec.action_encoder(toks)).float()
     std = model.action_std().float() if model.action_type != "Discrete" else torch.ones(A, device=dev)
     pack = dict(wpack=mp.decoder_fw, bias=torch.stack([l.bias.detach() for l in lins]).float().contiguous(),
                 lnp=torch.stack(lns).float().contiguous(), emb=emb.contiguous(),
                 wh2=dec.head[3].weight.detach().float().contiguous(), bh2=dec.head[3].bias.detach().float().contiguous(),
-                stdv=std.contiguous(), n_tok=A + 2)
+                stdv=std.contiguous(), n_tok=toks.shape[0], tok_start=tok_start, tok_zero=tok_zero, cont=int(cont))
+    if cont:
+        lin = dec.action_encoder[0]
+        pack.update(wa=lin.weight.detach().float().contiguous(), ba=lin.bias.detach().float().contiguous(),
+                    lnd=torch.stack([dec.ln.weight.detach(), dec.ln.bias.detach()]).float().contiguous())
     model._mdl_dec_pack = (ver, pack)
     return pack
 
@@ -110,8 +128,9 @@ def decode(model, rep, ava=None, deterministic=False, stride=1, rand=None):
     u = rand["u"].float().contiguous() if rand is not None else None
     n = rand["n"].float().contiguous() if rand is not None else None
     ava_c = ava.float().contiguous() if ava is not None else None
-    out_a = torch.empty(B, L, device=dev)
-    out_lp = torch.empty(B, L, device=dev)
+    cont = pk["cont"]
+    out_a = torch.empty(B, L, A if cont else 1, device=dev)
+    out_lp = torch.empty(B, L, A if cont else 1, device=dev)
     geo = lib().mdl_mat_decode_geometry(model.n_block, L, min(B, _EPW_CAP))
     epw, rmax = geo & 0xFF, geo >> 8
     if epw <= 0:
@@ -120,9 +139,10 @@ def decode(model, rep, ava=None, deterministic=False, stride=1, rand=None):
                     P(pk["wh2"]).value, P(pk["bh2"]).value, P(pk["stdv"]).value, P(rep).value, P(ava_c).value,
                     P(u).value, P(n).value, P(out_a).value, P(out_lp).value,
                     B, L, A, _n_disc(model, L), int(stride if deterministic else 1), int(bool(deterministic)), epw, rmax,
-                    pk["n_tok"], 0, A + 1, 0)
+                    pk["n_tok"], pk["tok_start"], pk["tok_zero"], 0, cont,
+                    P(pk.get("wa")).value, P(pk.get("ba")).value, P(pk.get("lnd")).value)
     check(lib().mdl_mat_decode(ctypes.byref(prm), model.n_block, kernels._stream()), "mat_decode")
-    return out_a.unsqueeze(-1), out_lp.unsqueeze(-1)
+    return out_a, out_lp
 
 
 def _encode(model, obs):
