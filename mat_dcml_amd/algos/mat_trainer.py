@@ -13,8 +13,10 @@ MI355X-specific:
   are all-reduced across ranks, and gradients are averaged with one flat all-reduce per minibatch
   (``parallel/comm.py``), so N ranks ≡ one process with the N-times-larger buffer;
 * the per-minibatch loss/backward/clip/Adam runs either in eager PyTorch or through the fused HIP path
-  (``ops/mat_fused.py`` teacher-forced encoder/decoder kernels + ``ops/rl_ops``), and can be replayed as a
-  hipGraph (``use_graph``) — no host sync inside an epoch.
+  (``ops/mat_fused.py`` teacher-forced encoder/decoder kernels + ``ops/rl_ops``) with no host sync inside an
+  epoch, so the host launches run ahead and the GPU never waits on Python (the rocprof kernel sum equals the
+  wall time per iteration, ``profiles/r1_kernel_stats_v9.csv``); hipGraph capture is used where launches do bound
+  the time (the MuJoCo surrogate's sub-step loop, ``envs/mujoco/physics.py``).
 """
 from __future__ import annotations
 

@@ -171,7 +171,6 @@ _FRAMEWORK_FLAGS = [
     ("dtype", str, "bf16", "bf16|fp32 compute dtype (master weights and optimizer state are fp32)"),
     ("train_stride", int, 1, "decision stride for rollouts (1 = exact per-agent sampling, the reference)"),
     ("eval_stride", int, 2, "batch decision stride for evaluation (dcml_runner.py:320)"),
-    ("use_graph", "true", F, "capture the PPO minibatch step in a hipGraph"),
     ("recompute_gae_every_epoch", "false", T, "recompute next-value/GAE every PPO epoch (reference semantics)"),
     ("results_dir", str, None, "root of results/ (default: ./results)"),
     ("resume", "true", F, "resume from the latest trainer_state_*.pt in the run dir"),
