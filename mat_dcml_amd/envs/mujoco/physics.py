@@ -280,6 +280,8 @@ class PlanarSim:
 
     # -------------------------------------------------------------------------------- dynamics
     def _forces(self, end, start, ang, d, v_end, ang_w):
+        """external forces F (B, P, 2) at points pts (B, P, 2): the root's points first (2 torso ends on the
+        ground, 1 torso midpoint in the fluid), then one per link"""
         m = self.m
         B, J = self.B, self.J
         if m.kind == "ground":
@@ -311,11 +313,9 @@ class PlanarSim:
             vt = (vel * t).sum(-1, keepdim=True)
             vn = (vel * n).sum(-1, keepdim=True)
             F = -(ct * vt * t + cn * vn * n) * ln
-            F = torch.cat([F[:, :1], F[:, 1:]], 1)
-            pts = torch.cat([pts[:, :1], pts[:, 1:]], 1)
         else:
-            return None, None, None
-        return pts, F, end
+            return None, None
+        return pts, F
 
     def substep(self, tau_motor, tau_root_motor):
         m = self.m
@@ -331,7 +331,7 @@ class PlanarSim:
             self.qd = (self.qd + h * qdd).clamp(-50, 50)
             self.q = self.q + h * self.qd
             return
-        pts, F, _ = self._forces(end, start, ang, d, v_end, ang_w)
+        pts, F = self._forces(end, start, ang, d, v_end, ang_w)
         nr = pts.shape[1] - self.J                                      # root points (2 ground / 1 fluid)
         Fl = F[:, nr:]                                                  # forces at link points (B, J, 2)
         Pl = pts[:, nr:]
