@@ -81,6 +81,7 @@ __device__ __forceinline__ void mat_enc_bwd_tile(const EncP& p, char* smem, int 
   if (c.nseq <= 0) return;
   zero_lds(smem, mat_train_lds_bytes(p.NRP, p.SQ, p.L), c.tid);
   __syncthreads();
+  TP_DECL();
   const int lane = c.lane, g = lane >> 4, c16 = lane & 15;
   RT dx[MAXRT];
   // ---------------- value head backward (+ incoming d rep from the decoder)
@@ -147,6 +148,7 @@ __device__ __forceinline__ void mat_enc_bwd_tile(const EncP& p, char* smem, int 
     __syncthreads();
     wgrad_tm(c.DQ, c.XB, c.NRP, c.g(p.h1.dW), c.wave, lane);
     __syncthreads();
+  TP_MARK(20);
   }
   // ---------------- blocks in reverse
 #pragma unroll 1
@@ -157,6 +159,7 @@ __device__ __forceinline__ void mat_enc_bwd_tile(const EncP& p, char* smem, int 
     mlp_bwd(B.m[8], B.m[9], B.ln[1], dx, p.sv[bb].x1, p.sv[bb].h, cc);
     attn_self_bwd(B.m, B.ln[0], dx, p.sv[bb].xin, p.sv[bb].a1, p.sv[bb].lse1, false, cc);
   }
+  TP_MARK(21);
   // ---------------- embedding backward: x0 = LN0(GELU(W_e · LN_obs(obs) + b_e))
   __syncthreads();   // QB becomes the per-wave LN_obs scratch
 #ifndef MDL_ABLATE_EMB
@@ -169,6 +172,13 @@ __device__ __forceinline__ void mat_enc_bwd_tile(const EncP& p, char* smem, int 
       for (int kk = 0; kk < 16; ++kk) dwe[ct][kk] = 0.f;
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) { dlog[kk] = 0.f; dlob[kk] = 0.f; }
+#ifndef MDL_ABLATE_DOH
+    float wreg[4][16];
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) wreg[ct][kk] = kk < p.od ? p.we[(16 * ct + c16) * p.od + kk] : 0.f;
+#endif
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
       const int rt = c.wave + 4 * k;
@@ -176,8 +186,11 @@ __device__ __forceinline__ void mat_enc_bwd_tile(const EncP& p, char* smem, int 
         const f32x4 vm = row_mask(rt, c.NR, lane);
         RT pre, e, xh, y, de;
         const float* ES = emb_scratch(c);
+        TP_MARK(29);
         embed_stage(p, rt, emb_scratch(c), c);
+        TP_MARK(23);
         embed_pre(p, rt, pre, ES, c);
+        TP_MARK(24);
         e = pre;
         gelu_rt(e);
         f32x4 mu, rs;
@@ -201,25 +214,36 @@ __device__ __forceinline__ void mat_enc_bwd_tile(const EncP& p, char* smem, int 
             }
           }
         }
+        TP_MARK(25);
         // d(LN_obs output)[row][kk] = sum_col dpre * W_e[col][kk]  -> LN_obs affine-parameter grads
 #ifndef MDL_ABLATE_DOH
+        // W_e columns of this lane in registers (loaded once per tile above), and the 16-lane reductions of
+        // one row issued back to back — they were serialised behind per-(row, kk) global loads (24 % of
+        // mat_enc_bwd in the section profile)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
+          float t[16];
 #pragma unroll
           for (int kk = 0; kk < 16; ++kk) {
-            if (kk < p.od) {
-              float t = 0.f;
+            t[kk] = 0.f;
 #pragma unroll
-              for (int ct = 0; ct < 4; ++ct) t += de.v[ct][r] * p.we[(16 * ct + c16) * p.od + kk];
-              t = group_sum<16>(t);
-              if (c16 == 0) { dlog[kk] += t * ES[(4 * g + r) * 32 + 16 + kk]; dlob[kk] += t; }
-            }
+            for (int ct = 0; ct < 4; ++ct) t[kk] += de.v[ct][r] * wreg[ct][kk];
+          }
+#pragma unroll
+          for (int kk = 0; kk < 16; ++kk)
+            if (kk < p.od) t[kk] = group_sum<16>(t[kk]);
+          if (c16 == 0) {
+#pragma unroll
+            for (int kk = 0; kk < 16; ++kk)
+              if (kk < p.od) { dlog[kk] += t[kk] * ES[(4 * g + r) * 32 + 16 + kk]; dlob[kk] += t[kk]; }
           }
         }
 #endif
+        TP_MARK(26);
         wave_lds_sync();   // scratch reads done before the next tile's staging overwrites it
       }
     }
+    TP_MARK(29);
     flush_ln(dlg, dlb, LNp{nullptr, nullptr, p.d_ln0_g, p.d_ln0_b}, c);
     flush_cols(dbe, c.g(p.d_be), lane);
 #pragma unroll
@@ -232,6 +256,7 @@ __device__ __forceinline__ void mat_enc_bwd_tile(const EncP& p, char* smem, int 
           if (g == 0 && p.d_we) atomicAdd(c.g(p.d_we) + (16 * ct + c16) * p.od + kk, x);
         }
       }
+    TP_MARK(27);
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) {
       if (kk < p.od) {
@@ -246,6 +271,7 @@ __device__ __forceinline__ void mat_enc_bwd_tile(const EncP& p, char* smem, int 
     }
   }
 #endif
+  TP_MARK(22);
 }
 
 template <int NB>
@@ -289,3 +315,9 @@ MDL_API int MDL_V(mdl_mat_enc_bwd)(const EncP* p, int NB, hipStream_t st) {
   return -3;
 }
 
+
+#ifdef MDL_TRAIN_PROF
+MDL_API int mdl_enc_prof_read(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tprof), sizeof(unsigned long long) * 32, 0, hipMemcpyDeviceToHost);
+}
+#endif

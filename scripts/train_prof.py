@@ -38,3 +38,17 @@ tot = out[11] + out[8] + out[9] + out[10]
 print(f"dec_bwd workgroup-0 cycles (4 launches): {tot}")
 for k in (11, 8, 9, 7, 12, 13, 14, 15, 17, 10, 0, 1, 2, 3, 4, 5, 6):
     print(f"  {NAMES[k]:26s} {out[k]:12d} {100 * out[k] / tot:5.1f}%")
+
+# encoder backward sections (value head, blocks (mlp + self-attention, marks 0-6 inside), embedding)
+lib.mdl_enc_prof_read.argtypes = [ctypes.c_void_p]
+eo = (ctypes.c_ulonglong * 32)()
+assert lib.mdl_enc_prof_read(ctypes.addressof(eo)) == 0
+etot = eo[20] + eo[21] + eo[22]
+print(f"enc_bwd workgroup-0 cycles (4 launches): {etot}")
+for k, n in ((20, "value head bwd"), (21, "blocks (mlp + self-attn)"), (22, "obs embedding bwd"), (0, " self: proj+LN bwd"),
+             (1, " self: wgrad proj"), (2, " self: recompute qkv"), (3, " self: attn bwd q"), (4, " self: attn bwd kv"),
+             (5, " self: wgrad qkv"), (6, " self: dx GEMMs")):
+    print(f"  {n:26s} {eo[k]:12d} {100 * eo[k] / max(etot, 1):5.1f}%")
+for k, n in ((23, "  emb: stage LN_obs"), (24, "  emb: pre GEMV"), (25, "  emb: LN/GELU bwd + dW_e acc"),
+             (26, "  emb: LN_obs param grads"), (27, "  emb: flush LN0/b_e/W_e"), (29, "  emb: (loop glue)")):
+    print(f"  {n:26s} {eo[k]:12d} {100 * eo[k] / max(etot, 1):5.1f}%")
