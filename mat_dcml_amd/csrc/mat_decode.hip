@@ -391,15 +391,18 @@ __device__ __forceinline__ void head_phase(const DecParams& p, const float* H1, 
 #ifdef MDL_DECODE_PROF
 __device__ unsigned long long g_decode_prof[16];
 #define MDL_PROF_MARK(k) do { if (prof_on) { const unsigned long long t_ = clock64(); prof[k] += t_ - prof_t; prof_t = t_; } } while (0)
+// sub-phase marks: cycles since the previous (sub-)mark, WITHOUT resetting the phase timer's reference
+#define MDL_PROF_SUB(k) do { if (prof_on) { const unsigned long long t_ = clock64(); prof[k] += t_ - prof_s; prof_s = t_; } } while (0)
 #else
 #define MDL_PROF_MARK(k) do { } while (0)
+#define MDL_PROF_SUB(k) do { } while (0)
 #endif
 
 template <int NB>
 __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
 #ifdef MDL_DECODE_PROF
   const bool prof_on = blockIdx.x == 0 && threadIdx.x == 0;
-  unsigned long long prof[16] = {0}, prof_t = clock64();
+  unsigned long long prof[16] = {0}, prof_t = clock64(), prof_s = prof_t;
 #endif
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NG = 10 * NB + 1;
@@ -582,14 +585,18 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
         __syncthreads();
         MDL_PROF_MARK(6);
         // ---------------- [G] x2 = LN2(S) -> XR ; h = GELU(mlp1(x2)) -> XA
+        MDL_PROF_SUB(12);
         afrag_ln(S, LNP + (3 * b + 1) * 128, LNP + (3 * b + 1) * 128 + 64, lane, a, xf);
+        MDL_PROF_SUB(13);
         if (wave == 0) store_xf(XR, lane, xf);
         {
           f32x4 acc = mfma2(a, wb[b * 10 + 8], f32x4{0, 0, 0, 0});
+          MDL_PROF_SUB(14);
           const int col = 16 * wave + c16;
 #pragma unroll
           for (int r = 0; r < 4; ++r) XA[(4 * g4 + r) * XP + col] = f2bf(gelu_erf(acc[r] + bcol[b * 10 + 8]));
         }
+        MDL_PROF_SUB(15);
         __syncthreads();
         MDL_PROF_MARK(7);
         // ---------------- [H] mlp2 + bias + residual x2 -> S
