@@ -98,6 +98,9 @@ def robot_obs(env, d):
         return torch.cat([d.qpos[:, 2:], d.qvel], 1)
     if sc in ("Ant-v2", "manyagent_ant"):
         return torch.cat([d.qpos[:, 2:], d.qvel, d.cfrc_ext.clamp(-1, 1).reshape(d.E, -1)], 1)
+    if sc in ("Humanoid-v2", "HumanoidStandup-v2"):   # humanoid.py _get_obs: 22 + 23 + 140 + 84 + 23 + 84 = 376
+        return torch.cat([d.qpos[:, 2:], d.qvel, d.cinert.reshape(d.E, -1), d.cvel.reshape(d.E, -1),
+                          d.qfrc_actuator, d.cfrc_ext.reshape(d.E, -1)], 1)
     if sc == "Reacher-v2":
         th = d.qpos[:, :2]
         return torch.cat([torch.cos(th), torch.sin(th), d.qpos[:, 2:], d.qvel[:, :2], d.fingertip_dist()], 1)
@@ -224,6 +227,13 @@ class MujocoMultiVec:
             contact = 0.5e-3 * d.cfrc_ext.clamp(-1, 1).square().sum((1, 2))
             ok = finite & (qp[:, 2] >= 0.2) & (qp[:, 2] <= 1.0)
             return fwd - 0.5 * ctrl - contact + 1.0, ~ok
+        if sc == "Humanoid-v2":     # humanoid.py: 1.25 * COM velocity + 5 alive - 0.1 ctrl - contact cost
+            contact = (5e-7 * d.cfrc_ext.square().sum((1, 2))).clamp(max=10.0)
+            ok = finite & (qp[:, 2] > 1.0) & (qp[:, 2] < 2.0)
+            return 1.25 * fwd + 5.0 - 0.1 * ctrl - contact, ~ok
+        if sc == "HumanoidStandup-v2":   # uphill reward (z / dt) - ctrl - impact + 1, never terminates
+            impact = (0.5e-6 * d.cfrc_ext.square().sum((1, 2))).clamp(max=10.0)
+            return qp[:, 2] / s.dt_env - 0.1 * ctrl - impact + 1.0, ~finite
         if sc == "Reacher-v2":
             dist = (s.fingertip() - s.target).norm(dim=-1)
             return -dist - ctrl, ~finite

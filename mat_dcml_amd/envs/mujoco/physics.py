@@ -1,7 +1,8 @@
 """Batched planar articulated-body simulator: a MuJoCo-shaped surrogate for the multi-agent MuJoCo tasks.
 
 mujoco-py and the MuJoCo binaries are not installable here, so the reference's MA-MuJoCo robots
-(``mat_src/mat/envs/ma_mujoco/multiagent_mujoco/``: gym HalfCheetah / Hopper / Walker2d / Swimmer / Ant / Reacher,
+(``mat_src/mat/envs/ma_mujoco/multiagent_mujoco/``: gym HalfCheetah / Hopper / Walker2d / Swimmer / Ant / Reacher /
+Humanoid(Standup),
 ``coupled_half_cheetah.py``, ``manyagent_swimmer.py``, ``manyagent_ant.py``) are re-modelled as planar link trees
 simulated for E envs at once on the device.  What is kept EXACTLY is the interface the multi-agent layer and the
 policy see: the gym ``qpos`` / ``qvel`` layouts (so ``graph.py``'s joint ids index the right entries), the
@@ -142,6 +143,38 @@ def _manyagent_ant(n_segs):
                  root_ends=((-half, 0.0), (half, 0.0)), h=0.0025, nbody=1 + 7 * n_segs)
 
 
+def _humanoid(name="Humanoid-v2"):
+    # planar biped with the XML's 17 hinge joints in qpos order: abdomen z, y, x (a 3-link waist chain down to
+    # the pelvis), right hip x, z, y + knee, left hip x, z, y + knee (legs hang off the waist), right shoulder1,
+    # shoulder2 + elbow, left likewise (arms hang off the chest).  Actuators in the XML order abdomen_y,
+    # abdomen_z, abdomen_x, … (gear 100, knees 200, arms 25).
+    P2 = PI / 2
+    L = [Link(-1, 0.12, -P2, (0.0, -0.10), 2.0, (-0.78, 0.78), 5.0, stiffness=20),      # 0 abdomen_z
+         Link(0, 0.10, 0.0, mass=2.0, rng=(-1.31, 0.52), damping=5.0, stiffness=10),     # 1 abdomen_y
+         Link(1, 0.08, 0.0, mass=2.5, rng=(-0.61, 0.61), damping=5.0, stiffness=10),     # 2 abdomen_x
+         Link(2, 0.04, 0.0, mass=1.0, rng=(-0.44, 0.09), damping=5.0),                   # 3 right_hip_x
+         Link(3, 0.04, 0.0, mass=1.0, rng=(-1.05, 0.61), damping=5.0),                   # 4 right_hip_z
+         Link(4, 0.34, 0.0, mass=4.5, rng=(-1.92, 0.35), damping=5.0),                   # 5 right_hip_y (thigh)
+         Link(5, 0.38, 0.0, mass=2.6, rng=(-2.79, 0.03), damping=1.0),                   # 6 right_knee (shin)
+         Link(2, 0.04, 0.0, mass=1.0, rng=(-0.44, 0.09), damping=5.0),                   # 7 left_hip_x
+         Link(7, 0.04, 0.0, mass=1.0, rng=(-1.05, 0.61), damping=5.0),                   # 8 left_hip_z
+         Link(8, 0.34, 0.0, mass=4.5, rng=(-1.92, 0.35), damping=5.0),                   # 9 left_hip_y
+         Link(9, 0.38, 0.0, mass=2.6, rng=(-2.79, 0.03), damping=1.0),                   # 10 left_knee
+         Link(-1, 0.06, -P2, (0.0, 0.15), 0.5, (-1.48, 1.05), 1.0),                      # 11 right_shoulder1
+         Link(11, 0.22, 0.0, mass=1.5, rng=(-1.48, 1.05), damping=1.0),                  # 12 right_shoulder2
+         Link(12, 0.25, 0.0, mass=1.2, rng=(-1.57, 0.87), damping=1.0),                  # 13 right_elbow
+         Link(-1, 0.06, -P2, (0.0, 0.15), 0.5, (-1.05, 1.48), 1.0),                      # 14 left_shoulder1
+         Link(14, 0.22, 0.0, mass=1.5, rng=(-1.05, 1.48), damping=1.0),                  # 15 left_shoulder2
+         Link(15, 0.25, 0.0, mass=1.2, rng=(-1.57, 0.87), damping=1.0)]                  # 16 left_elbow
+    gear = [100, 100, 100, 100, 100, 300, 200, 100, 100, 300, 200, 25, 25, 25, 25, 25, 25]
+    acts = [1, 0] + list(range(2, 17))
+    m = Model(name, "ground", "free", L, gear, acts, 40.0, root_ends=((0.0, 0.19), (0.0, -0.10)), dt=0.003,
+              frame_skip=5, h=0.0025, init_z=1.4, reset_pos=0.01, reset_vel=0.01, reset_vel_normal=False, nbody=14,
+              armature=0.2)
+    m.extra["standup"] = name == "HumanoidStandup-v2"
+    return m
+
+
 def _reacher():
     L = [Link(-1, 0.1, 0.0, (0.0, 0.0), 0.05, None, 1.0), Link(0, 0.11, 0.0, mass=0.05, rng=(-3.0, 3.0), damping=1.0)]
     return Model("Reacher-v2", "arm", "fixed", L, [200.0, 200.0], [0, 1], 1.0, dt=0.01, frame_skip=2, h=0.005,
@@ -171,9 +204,9 @@ def make_model(scenario, agent_conf=""):
         return _manyagent_ant(na * per)
     if scenario == "Reacher-v2":
         return _reacher()
-    raise NotImplementedError(
-        f"no surrogate dynamics for {scenario!r} (Humanoid needs MuJoCo's 3-D contact model; its partition graph "
-        f"is in graph.py)")
+    if scenario in ("Humanoid-v2", "HumanoidStandup-v2"):
+        return _humanoid(scenario)
+    raise NotImplementedError(f"no surrogate dynamics for {scenario!r}")
 
 
 def _cross(a, b):          # planar cross product (…, 2) × (…, 2) -> (…)

@@ -28,7 +28,8 @@ CONFS = [("HalfCheetah-v2", "2x3"), ("HalfCheetah-v2", "6x1"), ("Ant-v2", "2x4")
 
 SIM_CONFS = [("HalfCheetah-v2", "6x1"), ("HalfCheetah-v2", "2x3"), ("Hopper-v2", "3x1"), ("Walker2d-v2", "2x3"),
              ("Swimmer-v2", "2x1"), ("Ant-v2", "2x4"), ("Ant-v2", "4x2"), ("Reacher-v2", "2x1"),
-             ("coupled_half_cheetah", "1p1"), ("manyagent_swimmer", "4x2"), ("manyagent_ant", "2x2")]
+             ("coupled_half_cheetah", "1p1"), ("manyagent_swimmer", "4x2"), ("manyagent_ant", "2x2"),
+             ("Humanoid-v2", "9|8"), ("HumanoidStandup-v2", "17x1")]
 
 
 def _ref_obsk():
@@ -214,3 +215,11 @@ def test_graph_captured_step_matches_eager(scenario, conf, monkeypatch):
         torch.testing.assert_close(outs[0][2], outs[1][2], rtol=1e-4, atol=1e-4)
     for k in ("p", "th", "q", "qd"):
         torch.testing.assert_close(getattr(envs[0].sim, k), getattr(envs[1].sim, k), rtol=1e-4, atol=1e-4)
+
+
+def test_humanoid_layout():
+    """Humanoid surrogate: gym's 376-dim observation, 17 actuators in the XML order, 9|8 partition"""
+    env = MujocoMultiVec("Humanoid-v2", "9|8", 2, agent_obsk=None, seed=0)
+    assert env.state_dim == 376 + 2 and env.acdims == [9, 8]
+    d_qpos = env.sim.q.shape[1] + 7
+    assert d_qpos == 24
