@@ -199,7 +199,8 @@ def test_mujoco_env_and_policy_on_gpu():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("scenario,conf", [("HalfCheetah-v2", "6x1"), ("Ant-v2", "2x4"), ("Reacher-v2", "2x1"),
-                                           ("coupled_half_cheetah", "1p1"), ("manyagent_swimmer", "4x2")])
+                                           ("coupled_half_cheetah", "1p1"), ("manyagent_swimmer", "4x2"),
+                                           ("Humanoid-v2", "9|8")])
 def test_graph_captured_step_matches_eager(scenario, conf, monkeypatch):
     """the hipGraph replay of the sub-step loop must give the eager result (same kernels, same order)"""
     envs = []
