@@ -278,6 +278,9 @@ class PlanarSim:
         # launch-bound inner loop (nsub sub-steps x ~50 small kernels): captured once into a hipGraph on GPU
         self.use_graph = self.dev.type == "cuda" and os.environ.get("MAT_DCML_ENV_GRAPHS", "1") != "0"
         self._graph = None
+        # one-launch fused step (csrc/planar_sim.hip) on GPU; the tendon-coupled twin model keeps the torch path
+        self.use_fused = (self.dev.type == "cuda" and self.twins == 1 and J <= 64
+                          and os.environ.get("MAT_DCML_ENV_FUSED", "1") != "0")
         self.target = torch.zeros(self.B, 2, **f)
         self.p = torch.zeros(self.B, 2, **f)
         self.th = torch.zeros(self.B, **f)
@@ -392,12 +395,36 @@ class PlanarSim:
     def step(self, a):
         """a: (E, nu) in [-1, 1] (coupled twin: (E, 2·nu))."""
         a = a.reshape(self.B, -1).float()
+        if self.use_fused:
+            return self._step_fused(a)
         if not self.use_graph:
             return self._step(a)
         if self._graph is None:
             self._capture(a)
         self._a_in.copy_(a)
         self._graph.replay()
+
+    def _fused_consts(self):
+        m = self.m
+        parts = [self.anc, self.attach, self.length, self.rest, self.damp, self.stiff, self.lo, self.hi,
+                 self.inertia, self.root_attached.float(), self.root_ends, self.gear, self.act_map]
+        consts = torch.cat([t.reshape(-1).float() for t in parts]).contiguous()
+        kind = {"ground": 0, "fluid": 1, "arm": 2}[m.kind]
+        cn, ct = (m.extra["cn"], m.extra["ct"]) if m.kind == "fluid" else (0.0, 0.0)
+        return consts, (self.B, self.J, self.root_ends.shape[0], self.act_map.shape[0], self.nsub, kind, m.h, m.mass,
+                        self.root_I, self.k_contact, self.c_contact, self.mu, float(self.gravity[1]), cn, ct)
+
+    def _step_fused(self, a):
+        from ...ops import kernels
+        if getattr(self, "_fconsts", None) is None:
+            self._fconsts = self._fused_consts()
+        consts, scal = self._fconsts
+        for k in self._STATE:                  # state stays in place: the kernel updates it
+            t = getattr(self, k)
+            if not t.is_contiguous():
+                setattr(self, k, t.contiguous())
+        kernels.planar_step(consts, scal, a.contiguous(), self.p, self.th, self.v, self.w, self.q, self.qd,
+                            self.tau, self.f_end, self.f_root)
 
     def _capture(self, a):
         """Record one env step (all sub-steps) as a hipGraph whose inputs / outputs are the state buffers."""

@@ -228,3 +228,25 @@ def dcml_env_step(env, actions):
     so = StepOut(actions.data_ptr(), rew.data_ptr(), done.data_ptr(), delay.data_ptr(), pay.data_ptr())
     check(lib().mdl_dcml_env_step(ctypes.byref(ec), ctypes.byref(es), ctypes.byref(so), _stream()), "dcml_env_step")
     return env.obs, env.share_view(), rew, done, delay, pay, env.ava
+
+
+# ----------------------------------------------------------------------------------------- MuJoCo surrogate physics
+class PlanarConsts(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("B", "J", "R", "nu", "nsub", "kind")] + \
+               [(n, ctypes.c_float) for n in ("h", "mass", "root_I", "k_contact", "c_contact", "mu", "grav_y", "cn",
+                                              "ct")]
+
+
+sig("mdl_planar_step", vp, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp)
+
+
+def planar_step(consts, scal, act, p, th, v, w, q, qd, tau, f_end, f_root):
+    """All sub-steps of one PlanarSim env step in one launch (csrc/planar_sim.hip); state tensors updated in place."""
+    c = PlanarConsts(*scal)
+    B, J = c.B, c.J
+    for t, n in ((p, 2 * B), (th, B), (v, 2 * B), (w, B), (q, B * J), (qd, B * J), (tau, B * J), (f_end, 2 * B * J),
+                 (f_root, 2 * B), (act, B * c.nu)):
+        assert t.is_cuda and t.is_contiguous() and t.dtype == torch.float32 and t.numel() == n, (t.shape, n)
+    assert consts.is_contiguous() and consts.dtype == torch.float32
+    check(lib().mdl_planar_step(ctypes.byref(c), P(consts), consts.numel(), P(act), P(p), P(th), P(v), P(w), P(q),
+                                P(qd), P(tau), P(f_end), P(f_root), _stream()), "planar_step")

@@ -204,6 +204,7 @@ def test_mujoco_env_and_policy_on_gpu():
 def test_graph_captured_step_matches_eager(scenario, conf, monkeypatch):
     """the hipGraph replay of the sub-step loop must give the eager result (same kernels, same order)"""
     envs = []
+    monkeypatch.setenv("MAT_DCML_ENV_FUSED", "0")
     for graphs in ("1", "0"):
         monkeypatch.setenv("MAT_DCML_ENV_GRAPHS", graphs)
         envs.append(MujocoMultiVec(scenario, conf, 32, agent_obsk=1, device="cuda", seed=4))
@@ -216,6 +217,46 @@ def test_graph_captured_step_matches_eager(scenario, conf, monkeypatch):
         torch.testing.assert_close(outs[0][2], outs[1][2], rtol=1e-4, atol=1e-4)
     for k in ("p", "th", "q", "qd"):
         torch.testing.assert_close(getattr(envs[0].sim, k), getattr(envs[1].sim, k), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scenario,conf", [("HalfCheetah-v2", "6x1"), ("Ant-v2", "2x4"), ("Reacher-v2", "2x1"),
+                                           ("manyagent_swimmer", "4x2"), ("Swimmer-v2", "2x1"), ("Hopper-v2", "3x1"),
+                                           ("Humanoid-v2", "9|8")])
+def test_fused_planar_step_matches_torch(scenario, conf, monkeypatch):
+    """csrc/planar_sim.hip (all sub-steps in one launch) vs the torch sub-step loop, one env step at a time from
+    the same state (the torch state is copied into the fused sim before every step, so contact chaos cannot
+    amplify rounding differences across steps)"""
+    from mat_dcml_amd.ops import kernels
+    kernels.lib()   # the fused path must be the native one
+    envs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("MAT_DCML_ENV_FUSED", fused)
+        envs.append(MujocoMultiVec(scenario, conf, 96, agent_obsk=1, device="cuda", seed=4))
+    assert envs[0].sim.use_fused and not envs[1].sim.use_fused
+    fs, ts = envs[0].sim, envs[1].sim
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for t in range(20):
+        for k in fs._STATE:
+            getattr(fs, k).copy_(getattr(ts, k))
+        before = {k: getattr(fs, k) for k in fs._STATE}
+        act = torch.rand(96, envs[0].A, envs[0].n_actions, device="cuda", generator=g) * 2 - 1
+        outs = [e.step(act) for e in envs]
+        # a contact point sitting exactly at zero penetration switches its damping term on or off depending on
+        # the last bit of its height (fn = max(k pen - c vy, 0) * (pen > 0)), so an env may legitimately diverge
+        # in a step; require nearly every env to agree and none to go non-finite
+        ok = torch.ones(fs.B, dtype=torch.bool, device="cuda")
+        err = torch.zeros(fs.B, device="cuda")
+        for k in fs._STATE:
+            a, b = getattr(fs, k), getattr(ts, k)
+            assert a.data_ptr() == before[k].data_ptr()
+            assert torch.isfinite(a).all()
+            d = ((a - b).abs() / (1.0 + b.abs())).reshape(fs.B, -1).amax(1)
+            ok &= d <= 2e-3
+            err = torch.maximum(err, d)
+        frac = ok.float().mean().item()
+        assert frac >= 0.9, f"step {t}: only {frac:.3f} of envs match"
+        assert err.median().item() < 1e-4, f"step {t}: median per-env error {err.median().item():.2e}"
 
 
 def test_humanoid_layout():
