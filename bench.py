@@ -28,39 +28,92 @@ METRIC = "env-steps/sec (whole node) MAT-AS 32-worker DCML at 1/2/4/8 GPU; eval 
 BASELINE_BY_WORKERS = {32: 43.0, 100: 8.0}
 
 
-def main():
+def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=1,
+                   help="ranks = GPUs; without WORLD_SIZE in the env bench.py starts that many rank processes itself")
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--n_workers", type=int, default=32)
     p.add_argument("--envs", type=int, default=256, help="vectorised envs per GPU")
     p.add_argument("--episode_length", type=int, default=50)
+    p.add_argument("--ppo_epoch", type=int, default=15)
+    p.add_argument("--num_mini_batch", type=int, default=4)
     p.add_argument("--kernels", default="auto")
     p.add_argument("--dtype", default="bf16")
     p.add_argument("--phases", action="store_true")
     p.add_argument("--config", default="dcml", choices=["dcml", "smac"],
                    help="dcml: the headline 32-worker DCML config; smac: MAT on the SMAC-shaped 27m_vs_30m stress env")
-    p.add_argument("--no_eval", action="store_true", help="skip the post-timing eval latency probe")
-    a = p.parse_args()
+    p.add_argument("--no_eval", action="store_true", help="skip the post-timing eval sweep (ct / payment / latency)")
+    p.add_argument("--model_dir", default=None,
+                   help="trained checkpoint for the eval block (default: the committed 32-worker run, if it matches)")
+    return p.parse_args()
+
+
+def launch_ranks(n):
+    """``--gpus N`` without a torchrun launcher: start N rank processes (children, never exec) with the torchrun
+    env contract, before this process touches the GPU; exit with the first failing rank's code."""
+    import signal
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                code = p.poll()
+                if code is None:
+                    continue
+                procs.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in procs:   # a dead rank leaves the others blocked in a collective
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            p.kill()
+    return rc if rc >= 0 else 128 - rc
+
+
+def main():
+    a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a.gpus))
     if a.config == "smac":
         return bench_smac(a)
 
     from mat_dcml_amd.config import get_config, parse_args
+    from mat_dcml_amd.ops.paths import kernel_report
     from mat_dcml_amd.parallel.comm import init_from_env
     from mat_dcml_amd.runner.dcml_runner import DCMLRunner
 
     comm = init_from_env(prefer_gpu=True)
+    if comm.world_size != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={comm.world_size}: the launch does not match")
+    topo = comm.describe()
+    if comm.device.type == "cuda" and topo["shared_devices"] and os.environ.get("MAT_DCML_SHARE_DEVICES") != "1":
+        raise SystemExit(f"bench.py: ranks share GPUs {topo['devices']}")
     argv = ["--env_name", "DCML", "--scenario", "AS", "--algorithm_name", "mat", "--n_rollout_threads", str(a.envs),
-            "--episode_length", str(a.episode_length), "--lr", "5e-5", "--ppo_epoch", "15", "--num_mini_batch", "4",
-            "--gamma", "0.99", "--use_valuenorm", "--use_popart", "--entropy_coef", "0.01",
-            "--n_workers", str(a.n_workers), "--kernels", a.kernels, "--dtype", a.dtype, "--seed", "1"]
+            "--episode_length", str(a.episode_length), "--lr", "5e-5", "--ppo_epoch", str(a.ppo_epoch),
+            "--num_mini_batch", str(a.num_mini_batch), "--gamma", "0.99", "--use_valuenorm", "--use_popart",
+            "--entropy_coef", "0.01", "--n_workers", str(a.n_workers), "--kernels", a.kernels, "--dtype", a.dtype,
+            "--seed", "1"]
     if a.phases:
         argv.append("--profile_phases")
     args = parse_args(argv, get_config(), warn=False)
     runner = DCMLRunner({"all_args": args, "device": comm.device, "run_dir": None, "comm": comm})
     runner.warmup()
     dev = comm.device
+    paths = kernel_report(runner)
 
     def sync():
         if dev.type == "cuda":
@@ -87,14 +140,14 @@ def main():
     env_steps = a.steps * a.episode_length * a.envs * n
     value = env_steps / dt
     eval_info = None
-    if not a.no_eval and comm.is_main:   # "eval task time": batch-1 deterministic decision latency, stride 10
-        eval_info = eval_probe(runner, dev)
+    if not a.no_eval and comm.is_main and dev.type == "cuda":
+        eval_info = eval_block(a, args, runner, dev)
     if comm.is_main:
         if a.phases:
             print(runner.timers.summary(), file=sys.stderr)
         print(json.dumps({
             "metric": METRIC if a.n_workers == 32 else f"env-steps/sec (whole node) MAT-AS {a.n_workers}-worker DCML",
-            "value": round(value, 2), "unit": "env-steps/s", "n_gpus": n, "steps": a.steps,
+            "value": round(value, 2), "unit": "env-steps/s", "n_gpus": topo["distinct_devices"], "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": (round(value / BASELINE_BY_WORKERS[a.n_workers], 2)
                                            if a.n_workers in BASELINE_BY_WORKERS else None),
@@ -104,22 +157,55 @@ def main():
                                 f"({a.n_workers + 1} agents)",
                        "global_batch": a.envs * n, "seq_len": a.n_workers + 1,
                        "parallelism": f"dp{n}", "envs_per_gpu": a.envs, "episode_length": a.episode_length,
-                       "ppo_epoch": 15, "num_mini_batch": 4, "kernels": a.kernels,
+                       "ppo_epoch": a.ppo_epoch, "num_mini_batch": a.num_mini_batch,
                        "device": torch.cuda.get_device_name(dev) if dev.type == "cuda" else "cpu"},
+            "ranks": n, "backend": topo["backend"], "rank_devices": topo["devices"], "hosts": topo["hosts"],
+            "kernels": paths,
             "eval": eval_info,
         }), flush=True)
     comm.destroy()
 
 
-def eval_probe(runner, dev, n=30):
-    """Per-decision latency of the deterministic batch-decision path (stride 10, batch 1) and the mean task
-    completion time / payment over a short preset replay (DCML_MAT_ALT_Benchmark.py protocol, 1 point)."""
+DEFAULT_CKPT = {32: "profiles/r1_train32/transformer_799.pt"}
+
+
+def eval_block(a, args, runner, dev):
+    """"Eval task time": the reference benchmark protocol (``DCML_MAT_ALT_Benchmark.py:114-146``: preset replay,
+    11-point available-worker sweep, 1000 deterministic decisions per point, batch decision stride 10) for
+    (1) a fresh random-init MAT (``torch.manual_seed(1)``, BASELINE.md's random-init row), (2) the trained
+    checkpoint (``--model_dir``, default the committed 32-worker run) and (3) the fixed heuristic.  Independent of
+    ``--steps``: the benchmarked runner's weights are never used here."""
+    from mat_dcml_amd.algos.policy import TransformerPolicy
+    from mat_dcml_amd.envs.dcml.spaces import dcml_action_spaces
     from mat_dcml_amd.runner.benchmark import run_sweep
-    res = run_sweep(runner.policy, runner.dcml, dev, sweep="AW", n_points=1, steps=100, shards=10, stride=10,
-                    latency_b1=n, verbose=False)
-    return {"decision_ms_b1_stride10": round(res["decision_ms_b1"], 4),
-            "decision_ms_batched": round(res["decision_ms_batched"], 4), "ct_aw_all": round(res["ct"][0], 4),
-            "payment_aw_all": round(res["payment"][0], 4), "weights": "random-init"}
+
+    def fresh_policy():
+        torch.manual_seed(1)
+        envs = runner.envs
+        return TransformerPolicy(args, envs.observation_space[0], envs.share_observation_space[0],
+                                 dcml_action_spaces(runner.dcml.n_workers)[0], runner.num_agents, device=dev)
+
+    def summary(res):
+        out = {"ct": [round(x, 4) for x in res["ct"]], "payment": [round(x, 3) for x in res["payment"]],
+               "ct_mean": round(sum(res["ct"]) / len(res["ct"]), 4),
+               "payment_mean": round(sum(res["payment"]) / len(res["payment"]), 3)}
+        if "decision_ms_b1" in res:
+            out["decision_ms_b1_stride10"] = round(res["decision_ms_b1"], 4)
+            out["decision_ms_batched"] = round(res["decision_ms_batched"], 4)
+        return out
+
+    kw = dict(sweep="AW", n_points=11, steps=1000, shards=50, stride=10, verbose=False)
+    info = {"protocol": "DCML_MAT_ALT_Benchmark.py AW sweep: 11 points x 1000 preset decisions, stride 10, "
+                        f"{a.n_workers} workers (available-worker steps scaled to the pool)"}
+    info["random_init"] = summary(run_sweep(fresh_policy(), runner.dcml, dev, latency_b1=20, **kw))
+    ckpt = a.model_dir or DEFAULT_CKPT.get(a.n_workers)
+    if ckpt and os.path.exists(ckpt):
+        pol = fresh_policy()
+        pol.restore(ckpt)
+        info["trained"] = summary(run_sweep(pol, runner.dcml, dev, latency_b1=20, **kw))
+        info["trained"]["checkpoint"] = ckpt
+    info["fixed_heuristic"] = summary(run_sweep(None, runner.dcml, dev, fixed=True, latency_b1=0, **kw))
+    return info
 
 
 def bench_smac(a):
@@ -129,6 +215,8 @@ def bench_smac(a):
     from mat_dcml_amd.parallel.comm import init_from_env
     from mat_dcml_amd.runner.smac_runner import SMACRunner
     comm = init_from_env(prefer_gpu=True)
+    if comm.world_size != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={comm.world_size}: the launch does not match")
     envs = a.envs if a.envs != 256 else 32
     T = a.episode_length if a.episode_length != 50 else 100
     argv = ["--env_name", "StarCraft2", "--algorithm_name", "mat", "--map_name", "27m_vs_30m", "--n_rollout_threads",

@@ -69,20 +69,35 @@ class MATTrainer:
 
     def _setup_fused(self, args):
         """Fused minibatch step on GPU: fused fwd kernels → fused PPO loss/grad kernel → fused bwd kernels →
-        fused clip+Adam over the flat parameter buffer (no autograd graph, ~15 launches per minibatch)."""
+        fused clip+Adam over the flat parameter buffer (no autograd graph, ~15 launches per minibatch).
+        ``self.fused_reason`` records why the eager path was taken instead."""
         pol = self.policy
         flat = self.comm._flat if self.comm is not None else None
-        if flat is None or getattr(pol, "n_objective", 1) != 1 or not pol._fused():
+        self.fused_reason = None
+        if flat is None:
+            self.fused_reason = "no flat gradient buffer"
+        elif not pol._fused():
+            if pol.device.type != "cuda":
+                self.fused_reason = "cpu device"
+            elif pol.kernels == "torch" or not pol._is_mat():
+                self.fused_reason = f"kernels={pol.kernels}, model {type(pol.transformer).__name__}"
+            else:
+                self.fused_reason = "; ".join(mat_fused.unsupported_reasons(pol.transformer))
+        if self.fused_reason:
             return False
-        from ..ops import mat_train, ppo_fused
+        from ..ops import mat_train, paths, ppo_fused
         m = pol.transformer
-        if not mat_train.supported(m):
+        why = paths.train_unsupported_reasons(m)
+        if why:
+            self.fused_reason = "; ".join(why)
             return False
         fp = ppo_fused.flat_params_of(m)
         if fp is None or fp.numel() != flat.buf.numel():
+            self.fused_reason = "parameters are not one flat buffer"
             return False
         for p in self.params:   # grads and params must share one layout
             if p.grad is None or (p.grad.data_ptr() - flat.buf.data_ptr()) != (p.data_ptr() - fp.data_ptr()):
+                self.fused_reason = "gradient / parameter layouts differ"
                 return False
         self.loss_fused = ppo_fused.PPOLossFused(self, self.device)
         copies = int(os.environ.get("MAT_DCML_GRAD_COPIES", "8"))

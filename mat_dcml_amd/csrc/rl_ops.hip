@@ -2,22 +2,25 @@
 //
 // gae_reverse_scan: one lane per (env, agent, objective) sequence; the T-step reverse recurrence
 //   delta_t = r_t + gamma * V(t+1) * m(t+1) - V(t);  g_t = delta_t + gamma*lambda*m(t+1)*g_{t+1}
-// runs in registers, V = denormalised value (x*std + mean from the ValueNorm statistics in meanstd[2]).
-// Loads of step t are independent of the recurrence, so the compiler can issue them ahead (T is 50).
+// runs in registers, V = denormalised value (x*std + mean with the per-objective ValueNorm statistics
+// meanstd = [means(n_obj) | stds(n_obj)]); the mask is shared by the n_obj objectives of an (env, agent) pair
+// (mo_shared_buffer.py / dmo_shared_buffer.py keep one mask per agent).  Loads of step t are independent of the
+// recurrence, so the compiler can issue them ahead (T is 50).
 #include "common.h"
 
 __global__ __launch_bounds__(256) void gae_reverse_scan_kernel(
     const float* __restrict__ rew, const float* __restrict__ vpred, const float* __restrict__ masks,
     const float* __restrict__ meanstd, float* __restrict__ adv, float* __restrict__ ret,
-    int T, int n, float gamma, float lam) {
+    int T, int n, int n_obj, float gamma, float lam) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const float mean = meanstd[0], sd = meanstd[1];
+  const int o = i % n_obj, im = i / n_obj, nm = n / n_obj;
+  const float mean = meanstd[o], sd = meanstd[n_obj + o];
   float g = 0.f;
   float v_next = vpred[(size_t)T * n + i] * sd + mean;
   for (int t = T - 1; t >= 0; --t) {
     const float v = vpred[(size_t)t * n + i] * sd + mean;
-    const float m = masks[(size_t)(t + 1) * n + i];
+    const float m = masks[(size_t)(t + 1) * nm + im];
     const float delta = rew[(size_t)t * n + i] + gamma * v_next * m - v;
     g = delta + gamma * lam * m * g;
     adv[(size_t)t * n + i] = g;
@@ -27,10 +30,12 @@ __global__ __launch_bounds__(256) void gae_reverse_scan_kernel(
 }
 
 MDL_API int mdl_gae_reverse_scan(const float* rew, const float* vpred, const float* masks, const float* meanstd,
-                                 float* adv, float* ret, int T, int n, float gamma, float lam, hipStream_t s) {
+                                 float* adv, float* ret, int T, int n, int n_obj, float gamma, float lam,
+                                 hipStream_t s) {
+  if (n_obj <= 0 || n % n_obj) return -1;
   const int bs = 256;
   hipLaunchKernelGGL(gae_reverse_scan_kernel, dim3((n + bs - 1) / bs), dim3(bs), 0, s, rew, vpred, masks, meanstd,
-                     adv, ret, T, n, gamma, lam);
+                     adv, ret, T, n, n_obj, gamma, lam);
   MDL_CHECK_LAUNCH();
   return 0;
 }

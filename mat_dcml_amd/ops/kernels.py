@@ -36,12 +36,16 @@ def lib():
 
 
 def available():
+    """True when the HIP library is loaded.  On a GPU box a missing / unloadable library is an error, not a silent
+    fall-back to the eager path (``MAT_DCML_KERNELS=torch`` selects the eager path explicitly)."""
     if mode() == "torch":
         return False
     try:
         lib()
         return True
     except Exception:
+        if torch.cuda.is_available():
+            raise
         return False
 
 
@@ -89,17 +93,20 @@ def check(rc, name):
 
 # ----------------------------------------------------------------------------------------- RL ops
 vp, i32, f32, i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_int64
-sig("mdl_gae_reverse_scan", vp, vp, vp, vp, vp, vp, i32, i32, f32, f32, vp)
+sig("mdl_gae_reverse_scan", vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, f32, vp)
 
 
 def gae_reverse_scan(rewards, value_preds, masks, meanstd, gamma, lam, adv_out, ret_out):
+    """rewards (T, ..., n_obj), value_preds (T+1, ..., n_obj), masks (T+1, ..., 1) shared by the objectives,
+    meanstd [means(n_obj) | stds(n_obj)] fp32."""
     T = rewards.shape[0]
     n = rewards[0].numel()
-    assert value_preds.shape[0] == T + 1 and masks.numel() == (T + 1) * n
-    for t in (rewards, value_preds, masks, adv_out, ret_out):
+    n_obj = rewards.shape[-1]
+    assert value_preds.shape[0] == T + 1 and masks.numel() * n_obj == (T + 1) * n and meanstd.numel() == 2 * n_obj
+    for t in (rewards, value_preds, masks, adv_out, ret_out, meanstd):
         assert t.is_contiguous() and t.dtype == torch.float32
     check(lib().mdl_gae_reverse_scan(P(rewards), P(value_preds), P(masks), P(meanstd), P(adv_out), P(ret_out),
-                                     T, n, gamma, lam, _stream()), "gae_reverse_scan")
+                                     T, n, n_obj, gamma, lam, _stream()), "gae_reverse_scan")
 
 
 u32 = ctypes.c_uint32

@@ -44,17 +44,28 @@ def _n_disc(model, L):
     return L + model.semi_index if model.semi_index < 0 else model.semi_index
 
 
-def supports(model, L=None) -> bool:
+def unsupported_reasons(model, L=None) -> list:
+    """Why the fused decode cannot run this model (empty list = supported)."""
     if not kernels.available():
-        return False
-    if model.action_type not in ("Semi_Discrete", "Discrete", "Continuous", "Continous") or model.decoder.dec_actor:
-        return False
-    if model.n_embd != 64 or model.n_head != 2 or model.n_block not in (1, 2, 3) or model.action_dim > 64:
-        return False
+        return ["HIP library not loaded (kernels=torch or not built)"]
+    r = []
+    if model.action_type not in ("Semi_Discrete", "Discrete", "Continuous", "Continous"):
+        r.append(f"action_type {model.action_type}")
+    if model.decoder.dec_actor:
+        r.append("dec_actor (mat_dec) has no autoregressive decode")
+    if model.n_embd != 64 or model.n_head != 2 or model.n_block not in (1, 2, 3):
+        r.append(f"n_embd {model.n_embd} / n_head {model.n_head} / n_block {model.n_block} (kernel: 64 / 2 / 1-3)")
+    if model.action_dim > 64:
+        r.append(f"action_dim {model.action_dim} > 64")
     if model.action_type == "Semi_Discrete" and model.semi_index != -1:
-        return False
-    L = L or model.n_agent
-    return lib().mdl_mat_decode_geometry(model.n_block, L, 1) > 0
+        r.append(f"semi_index {model.semi_index} != -1")
+    if not r and lib().mdl_mat_decode_geometry(model.n_block, L or model.n_agent, 1) <= 0:
+        r.append(f"L={L or model.n_agent} does not fit the decode kernel's LDS")
+    return r
+
+
+def supports(model, L=None) -> bool:
+    return not unsupported_reasons(model, L)
 
 
 # envs per decode workgroup cap (kernel maximum 16).  The decode is latency bound (one dependent chain of ~20

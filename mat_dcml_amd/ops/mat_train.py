@@ -158,18 +158,49 @@ def _grad_sig(model):
 
 
 # ------------------------------------------------------------------------------------------------- support
-def encoder_supported(model):
+def _common_reasons(model):
+    if not kernels.available():
+        return ["HIP library not loaded (kernels=torch or not built)"]
+    r = []
+    if model.n_embd != 64 or model.n_head != 2 or model.n_block not in (1, 2, 3):
+        r.append(f"n_embd {model.n_embd} / n_head {model.n_head} / n_block {model.n_block} (kernel: 64 / 2 / 1-3)")
+    if geometry(model.n_agent)[0] <= 0:
+        r.append(f"L={model.n_agent} does not fit the training tiling")
+    return r
+
+
+def encoder_unsupported_reasons(model):
     enc = model.encoder
-    return (kernels.available() and model.n_embd == 64 and model.n_head == 2 and model.n_block in (1, 2, 3)
-            and not enc.encode_state and enc.obs_dim <= 16 and model.n_objective <= 2
-            and geometry(model.n_agent)[0] > 0)
+    r = _common_reasons(model)
+    if enc.encode_state:
+        r.append("encode_state")
+    if enc.obs_dim > 16:
+        r.append(f"obs_dim {enc.obs_dim} > 16")
+    if model.n_objective > 2:
+        r.append(f"n_objective {model.n_objective} > 2")
+    return r
+
+
+def decoder_unsupported_reasons(model):
+    dec = model.decoder
+    r = _common_reasons(model)
+    if dec.dec_actor:
+        r.append("dec_actor")
+    if model.action_type not in ("Semi_Discrete", "Discrete"):
+        r.append(f"action_type {model.action_type}")
+    if model.action_dim > 8:
+        r.append(f"action_dim {model.action_dim} > 8")
+    if model.action_type == "Semi_Discrete" and model.semi_index != -1:
+        r.append(f"semi_index {model.semi_index} != -1")
+    return r
+
+
+def encoder_supported(model):
+    return not encoder_unsupported_reasons(model)
 
 
 def decoder_supported(model):
-    dec = model.decoder
-    return (kernels.available() and not dec.dec_actor and model.action_type in ("Semi_Discrete", "Discrete")
-            and model.action_dim <= 8 and model.n_embd == 64 and model.n_head == 2 and model.n_block in (1, 2, 3)
-            and (model.action_type == "Discrete" or model.semi_index == -1) and geometry(model.n_agent)[0] > 0)
+    return not decoder_unsupported_reasons(model)
 
 
 def supported(model):

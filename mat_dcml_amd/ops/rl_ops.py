@@ -24,15 +24,22 @@ def gae_torch(rewards, value_preds, masks, gamma, lam, value_normalizer, adv_out
         ret_out[t] = g + v[t]
 
 
+GAE_MULTI_OBJECTIVE = True   # the HIP scan takes per-objective ValueNorm statistics (mo/dmo buffers)
+
+
 def gae(rewards, value_preds, masks, gamma, lam, value_normalizer, adv_out, ret_out):
-    if kernels.use_hip(rewards) and rewards.shape[-1] == value_preds.shape[-1]:
+    n_obj = rewards.shape[-1]
+    if kernels.use_hip(rewards) and value_preds.shape[-1] == n_obj and masks.shape[-1] == 1:
         if value_normalizer is not None:
             mean, var = value_normalizer.running_mean_var()
-            mv = torch.stack([mean.reshape(-1)[0], var.reshape(-1)[0].sqrt()]).float().contiguous()
-            if mean.numel() > 1:  # per-objective normalisers: fall back
-                return gae_torch(rewards, value_preds, masks, gamma, lam, value_normalizer, adv_out, ret_out)
+            mean, var = mean.reshape(-1).float(), var.reshape(-1).float()
+            if mean.numel() == 1 and n_obj > 1:
+                mean, var = mean.expand(n_obj), var.expand(n_obj)
+            if mean.numel() != n_obj:
+                raise ValueError(f"ValueNorm has {mean.numel()} objectives, rewards {n_obj}")
+            mv = torch.cat([mean, var.sqrt()]).contiguous()
         else:
-            mv = torch.tensor([0.0, 1.0], device=rewards.device)
+            mv = torch.cat([torch.zeros(n_obj, device=rewards.device), torch.ones(n_obj, device=rewards.device)])
         kernels.gae_reverse_scan(rewards, value_preds, masks, mv, gamma, lam, adv_out, ret_out)
         return
     gae_torch(rewards, value_preds, masks, gamma, lam, value_normalizer, adv_out, ret_out)

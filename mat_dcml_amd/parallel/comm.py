@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import datetime
 import os
+import socket
 
 import torch
 import torch.distributed as dist
@@ -27,6 +28,7 @@ class Comm:
         self.device = device
         self.group = group
         self._flat = None
+        self.backend = "none"
 
     @property
     def is_main(self):
@@ -69,6 +71,12 @@ class Comm:
         dist.all_gather_object(out, obj, group=self.group)
         return out
 
+    def seed_sampling_rng(self, seed: int):
+        """Call after the (identical, broadcast) weight init: every rank gets its own torch RNG stream, so the
+        rollout's exploration draws (decode uniforms / normals) are independent across ranks instead of repeating
+        rank 0's noise in every replica."""
+        torch.manual_seed(int(seed) + 1_000_003 * self.rank)
+
     # -------------------------------------------------------------------------------- gradients
     def attach_flat_grads(self, params):
         self._flat = FlatGrads(params)
@@ -90,6 +98,18 @@ class Comm:
         if self.world_size == 1:
             return None
         return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+
+    def describe(self) -> dict:
+        """Gathered rank → device map of the job (collective: every rank must call it).  ``distinct_devices`` counts
+        physical devices (host, device index); CPU ranks count as one device each."""
+        if self.device.type == "cuda":
+            me = (socket.gethostname(), f"cuda:{self.device.index}")
+        else:
+            me = (socket.gethostname(), f"cpu:rank{self.rank}")
+        allv = self.all_gather_object(me)
+        return {"backend": self.backend, "world_size": self.world_size, "devices": [d for _, d in allv],
+                "hosts": sorted({h for h, _ in allv}), "distinct_devices": len(set(allv)),
+                "shared_devices": len(set(allv)) < self.world_size}
 
     def destroy(self):
         if self.world_size > 1 and dist.is_initialized():
@@ -128,22 +148,36 @@ class FlatGrads:
                 p.grad = v
 
 
-def init_from_env(prefer_gpu=True, timeout_s=600) -> Comm:
+def init_from_env(prefer_gpu=True, timeout_s=600, share_devices=None) -> Comm:
+    """One process per device.  Under RCCL (``nccl``) every rank must own its own GPU: a LOCAL_RANK beyond the
+    visible device count is an error.  Sharing one GPU between ranks (rehearsals on a 1-GPU box) is an explicit
+    opt-in (``share_devices=True`` or ``MAT_DCML_SHARE_DEVICES=1``) and is allowed with the gloo backend only."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_gpu = prefer_gpu and torch.cuda.is_available()
-    # one process per GPU; ranks beyond the visible GPU count share devices round-robin (test rehearsal on a
-    # 1-GPU box together with MAT_DCML_DIST_BACKEND=gloo — RCCL wants one device per rank)
-    device = torch.device(f"cuda:{local % max(1, torch.cuda.device_count())}") if use_gpu else torch.device("cpu")
+    backend = os.environ.get("MAT_DCML_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
+    if share_devices is None:
+        share_devices = os.environ.get("MAT_DCML_SHARE_DEVICES", "0") == "1"
+    device = torch.device("cpu")
     if use_gpu:
+        ndev = torch.cuda.device_count()
+        if local >= ndev:
+            if not share_devices or backend == "nccl":
+                raise RuntimeError(
+                    f"rank {rank}: LOCAL_RANK {local} but only {ndev} visible GPU(s); backend {backend!r} needs one GPU "
+                    f"per rank (device sharing is opt-in via MAT_DCML_SHARE_DEVICES=1 and only with gloo)")
+            device = torch.device(f"cuda:{local % ndev}")
+        else:
+            device = torch.device(f"cuda:{local}")
         torch.cuda.set_device(device)
     group = None
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = os.environ.get("MAT_DCML_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
         if use_gpu and backend == "nccl":
             kw["device_id"] = device
         dist.init_process_group(**kw)
-    return Comm(rank, world, local, device, group)
+    c = Comm(rank, world, local, device, group)
+    c.backend = backend if world > 1 else "none"
+    return c

@@ -77,6 +77,7 @@ class BaselineRunner(DCMLRunner):
             self.policy = self.ac
             for m in (self.ac.actors, self.ac.critic):
                 self.comm.broadcast_module_(m)
+        self.comm.seed_sampling_rng(a.seed)
         ava_dim = _ava_dim(("mixed", (W, 2, 1))) if self.single else 2
         act_dim = self.ac.act_dim if self.ac is not None else 1
         self.buffer = SeparatedBuffer(a, E, self.num_agents, obs_dim, self.dcml.share_dim, act_dim, ava_dim, self.device)

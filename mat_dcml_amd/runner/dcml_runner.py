@@ -80,6 +80,7 @@ class DCMLRunner:
         self.policy = TransformerPolicy(a, self.envs.observation_space[0], self.envs.share_observation_space[0],
                                         act_space, self.num_agents, device=self.device)
         self.comm.broadcast_module_(self.policy.transformer)
+        self.comm.seed_sampling_rng(a.seed)
         # every .grad is a view of ONE flat fp32 buffer: one memset to zero, one all-reduce under DP, and the fused
         # backward kernels accumulate straight into it
         self.comm.attach_flat_grads(self.policy.transformer.parameters())
@@ -171,6 +172,8 @@ class DCMLRunner:
 
     # ---------------------------------------------------------------------------------------- main loop
     def run(self):
+        from ..ops.paths import log_kernel_report
+        log_kernel_report(self)
         self.warmup()
         start = time.time()
         episodes = int(self.num_env_steps) // self.episode_length // self.n_rollout_threads // self.comm.world_size

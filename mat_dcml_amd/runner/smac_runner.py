@@ -69,6 +69,7 @@ class SMACRunner(DCMLRunner):
         torch.manual_seed(a.seed)
         self.policy = TransformerPolicy(a, [obs_dim], [share_dim], act_space, self.num_agents, device=self.device)
         self.comm.broadcast_module_(self.policy.transformer)
+        self.comm.seed_sampling_rng(a.seed)
         self.comm.attach_flat_grads(self.policy.transformer.parameters())
         self.trainer = MATTrainer(a, self.policy, self.num_agents, device=self.device, comm=self.comm)
         pol = self.policy

@@ -1,0 +1,58 @@
+"""bench.py multi-rank contract and the kernel-path report (item 9), on CPU.
+
+* ``python bench.py --gpus 2`` with no launcher starts two rank processes itself (gloo here) and reports two
+  distinct ranks / devices;
+* a launch whose WORLD_SIZE disagrees with ``--gpus`` fails instead of benchmarking the wrong node size;
+* under RCCL (``nccl``) a rank without its own GPU is an error; GPU sharing is an explicit gloo-only opt-in.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SMALL = ["--steps", "1", "--warmup", "0", "--envs", "4", "--episode_length", "2", "--n_workers", "4", "--ppo_epoch",
+         "1", "--num_mini_batch", "1", "--no_eval"]
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(OMP_NUM_THREADS="1", **kw)
+    return env
+
+
+def test_bench_self_launches_two_ranks():
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *SMALL], cwd=ROOT, env=_env(), capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout          # rank 0 prints ONE JSON line
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["ranks"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["backend"] == "gloo" and len(set(out["rank_devices"])) == 2
+    assert out["config"]["global_batch"] == 8
+    assert set(out["kernels"]) >= {"env", "encoder", "decode", "train", "gae"}
+
+
+def test_bench_rejects_world_size_mismatch():
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *SMALL], cwd=ROOT,
+                       env=_env(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"), capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert "does not match" in r.stderr
+
+
+@pytest.mark.parametrize("backend,share", [("nccl", "0"), ("nccl", "1"), ("gloo", "0")])
+def test_rank_without_own_gpu_fails_loudly(monkeypatch, backend, share):
+    from mat_dcml_amd.parallel import comm as C
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("RANK", "1")
+    monkeypatch.setenv("LOCAL_RANK", "1")
+    monkeypatch.setenv("MAT_DCML_DIST_BACKEND", backend)
+    monkeypatch.setenv("MAT_DCML_SHARE_DEVICES", share)
+    with pytest.raises(RuntimeError, match="needs one GPU per rank"):
+        C.init_from_env(prefer_gpu=True)

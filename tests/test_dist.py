@@ -21,6 +21,7 @@ def _run(rank, world, port, fn, q, gpu=False):
                       LOCAL_RANK=str(rank))
     if gpu:   # ranks share the box's GPU(s); gloo carries the collectives (RCCL wants one GPU per rank)
         os.environ["MAT_DCML_DIST_BACKEND"] = "gloo"
+        os.environ["MAT_DCML_SHARE_DEVICES"] = "1"
     torch.set_num_threads(1)
     try:
         from mat_dcml_amd.parallel.comm import init_from_env
@@ -140,3 +141,21 @@ def test_dp_fused_gpu_path_keeps_ranks_in_sync(gpu):
     assert out[0][2] and out[1][2]
     assert out[0][0] == out[1][0] and out[0][1] == out[1][1]
     assert out[0][3] == out[1][3]
+
+
+def _rng_case(comm):
+    from mat_dcml_amd.config import get_config, parse_args
+    from mat_dcml_amd.runner.dcml_runner import DCMLRunner
+    args = parse_args(["--n_workers", "4", "--n_rollout_threads", "2", "--episode_length", "2", "--env_name", "DCML"],
+                      get_config(), warn=False)
+    r = DCMLRunner({"all_args": args, "device": comm.device, "run_dir": None, "comm": comm})
+    flat = torch.cat([p.detach().reshape(-1) for p in r.policy.transformer.parameters()]).double()
+    return float(flat.sum()), torch.rand(8).tolist()
+
+
+def test_dp_ranks_share_weights_but_not_exploration_noise():
+    """identical init on every rank, independent sampling streams (else every replica repeats rank 0's
+    exploration noise and the N-rank gradient average has less independent data than one N-times-larger batch)."""
+    out = spawn(_rng_case)
+    assert out[0][0] == out[1][0]
+    assert out[0][1] != out[1][1]

@@ -24,6 +24,23 @@ def test_gae_matches_torch(gpu):
     assert torch.allclose(ret1[:T], ret2[:T], atol=1e-3, rtol=1e-4)
 
 
+def test_gae_multi_objective_matches_torch(gpu):
+    """momat / dmomat buffers: two objectives with their own ValueNorm statistics, one mask per agent."""
+    T, E, A, K = 50, 32, 33, 2
+    g = torch.Generator(device=gpu).manual_seed(1)
+    rew = torch.randn(T, E, A, K, device=gpu, generator=g) * 10
+    vp = torch.randn(T + 1, E, A, K, device=gpu, generator=g)
+    masks = (torch.rand(T + 1, E, A, 1, device=gpu, generator=g) > 0.2).float()
+    vn = ValueNorm(K, device=gpu)
+    vn.update(torch.randn(1000, K, device=gpu) * torch.tensor([30.0, 3.0], device=gpu) + torch.tensor([5.0, -2.0], device=gpu))
+    adv1, ret1 = torch.zeros(T, E, A, K, device=gpu), torch.zeros(T + 1, E, A, K, device=gpu)
+    adv2, ret2 = adv1.clone(), ret1.clone()
+    rl_ops.gae_torch(rew, vp, masks, 0.99, 0.95, vn, adv1, ret1)
+    rl_ops.gae(rew, vp, masks, 0.99, 0.95, vn, adv2, ret2)
+    assert torch.allclose(adv1, adv2, atol=1e-3, rtol=1e-4)
+    assert torch.allclose(ret1[:T], ret2[:T], atol=1e-3, rtol=1e-4)
+
+
 def test_train_iteration_on_gpu(gpu):
     from mat_dcml_amd.config import get_config, parse_args
     from mat_dcml_amd.runner.dcml_runner import DCMLRunner
