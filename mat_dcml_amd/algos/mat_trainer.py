@@ -105,7 +105,8 @@ class MATTrainer:
             mat_train.attach_grad_workspace(m, flat.buf, copies=copies)
         pol.optimizer = ppo_fused.FlatAdam(fp, flat.buf, lr=pol.optimizer.param_groups[0]["lr"], eps=args.opti_eps,
                                            weight_decay=args.weight_decay,
-                                           max_grad_norm=args.max_grad_norm if self._use_max_grad_norm else None)
+                                           max_grad_norm=args.max_grad_norm if self._use_max_grad_norm else None,
+                                           layout=ppo_fused.param_offsets(m))
         return True
 
     # ------------------------------------------------------------------------------------------------

@@ -1,0 +1,598 @@
+// Fused MAT decoder (teacher-forced) forward / backward, token-on-lane tiles (mat_train_ct.h).  Reference:
+// ma_transformer.py:95-116 (DecodeBlock: causal self attention, causal cross attention on the encoder output, MLP),
+// :157-230 (Decoder: action embedding, blocks, action head), transformer_act.py:103-129,176-189 (teacher-forced
+// log-prob / entropy of the stored actions: masked Categorical, and the Normal ratio agent of Semi_Discrete).
+//
+// The action head's second linear (64 -> A, A <= 64) runs on MFMA in the transposed layout: the logits of a token
+// are spread over its 4 lanes (a = 16ma + 4g + r), so the softmax statistics are in-lane + 2 permlane swaps.
+// Logits use a hi/lo bf16 split of both operands (fp32-like: they feed exp(logp - old_logp)).
+#include "mat_train_ct.h"
+
+namespace {
+
+// token of row i: 0 = start, 1 + a = one-hot of the previous agent's (discrete) action   (transformer_act.py:103-111)
+__device__ __forceinline__ int dec_token_ct(const DecP& p, int tok, int i) {
+  if (i == 0) return 0;
+  int a = (int)p.act[tok - 1];
+  a = a < 0 ? 0 : (a >= p.A ? p.A - 1 : a);
+  return 1 + a;
+}
+
+// x0 pre-activation = W_a · onehot(token) — a column gather of W_a [64][A+1]
+__device__ __forceinline__ CT dec_embed_pre_ct(const DecP& p, int rt, int& tokid, const Ctx& c) {
+  const int lane = c.lane, g = lane >> 4;
+  const int row = rt * 16 + (lane & 15);
+  const bool ok = row < c.NR;
+  tokid = ok ? dec_token_ct(p, c.tok0 + row, row % c.L) : 0;
+  CT pre;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) pre.v[mt][r] = p.wa[(16 * mt + 4 * g + r) * (p.A + 1) + tokid];
+  return pre;
+}
+
+// ------------------------------------------------------------------------------------------ cross attention
+// x <- LN(rep + proj(attn(q = W_q rep, k = W_k x, v = W_v x)))   (ma_transformer.py:114)
+template <bool SAVE>
+__device__ __forceinline__ void cross_attn_fwd_ct(const Mat* m, const LNp& ln, CT* xr, const float* rep, bf16_t* sv_x1,
+                                                  bf16_t* sv_a, float* sv_lse, const Ctx& c) {
+  const int lane = c.lane;
+  {
+    AFr Wq, Wk, Wv;
+    loadA(Wq, m[4].fa, lane);
+    loadA(Wk, m[5].fa, lane);
+    loadA(Wv, m[6].fa, lane);
+    const CT bq = ld_vec(m[4].b, lane), bk = ld_vec(m[5].b, lane), bv = ld_vec(m[6].b, lane);
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) {
+        const bool ok = tok_ok(rt, c);
+        const CTr x = ct_pack(xr[k]);
+        if (SAVE) st_g(sv_x1, c.tok0, rt, c.NR, x, lane);
+        const CTr r = ct_pack(ld_gf(rep, c.tok0, rt, c.NR, lane));
+        CT q = bq, kk = bk, v = bv;
+        mm(q, Wq, r);
+        mm(kk, Wk, x);
+        mm(v, Wv, x);
+        st_lds(c.QB, rt, ct_pack(q), ok, lane);
+        st_lds(c.KB, rt, ct_pack(kk), ok, lane);
+        st_lds(c.VB, rt, ct_pack(v), ok, lane);
+      }
+    }
+  }
+  __syncthreads();
+  attn_fwd(c.QB, c.KB, c.VB, c.QB, true, SAVE ? sv_lse : nullptr, c);
+  __syncthreads();
+  AFr Wp;
+  loadA(Wp, m[7].fa, lane);
+  const CT bp = ld_vec(m[7].b, lane), gam = ld_vec(ln.g, lane), bet = ld_vec(ln.b, lane);
+#pragma unroll
+  for (int k = 0; k < MAXRT; ++k) {
+    const int rt = c.wave + 4 * k;
+    if (rt < c.NT) {
+      const CTr a = ld_lds(c.QB, rt, lane);
+      if (SAVE) st_g(sv_a, c.tok0, rt, c.NR, a, lane);
+      CT t = ct_add(bp, ld_gf(rep, c.tok0, rt, c.NR, lane)), xh;
+      mm(t, Wp, a);
+      ln_fwd_ct(t, xh, xr[k], gam, bet);
+    }
+  }
+}
+
+// backward: dx (w.r.t. the sublayer output) -> d x1 (returned in dx); d rep accumulated into global drep
+__device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, CT* dx, const float* rep, float* drep,
+                                                  const bf16_t* sv_x1, const bf16_t* sv_a, const float* sv_lse,
+                                                  const Ctx& c) {
+  const int lane = c.lane;
+  CT dres[MAXRT];
+  {
+    CT dlg, dlb;
+    ct_zero(dlg);
+    ct_zero(dlb);
+    AFr Wpf, Wpb;
+    loadA(Wpf, m[7].fa, lane);
+    loadA(Wpb, m[7].ba, lane);
+    const CT bp = ld_vec(m[7].b, lane), gam = ld_vec(ln.g, lane), bet = ld_vec(ln.b, lane);
+    CTr as[MAXRT];
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) as[k] = ld_g(sv_a, c.tok0, rt, c.NR, lane);
+    }
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) {
+        const bool ok = tok_ok(rt, c);
+        CT s = ct_add(bp, ld_gf(rep, c.tok0, rt, c.NR, lane)), xh, yy, ds;
+        mm(s, Wpf, as[k]);
+        const float rs = ln_fwd_ct(s, xh, yy, gam, bet);
+        ln_bwd_ct(dx[k], xh, rs, gam, ok, ds, dlg, dlb);
+        const CTr dsr = ct_pack(ds);
+        st_lds(c.DQ, rt, dsr, ok, lane);     // dY of Wp
+        st_lds(c.XB, rt, as[k], ok, lane);   // X of Wp
+        CT da;
+        ct_zero(da);
+        mm(da, Wpb, dsr);
+        st_lds(c.DA, rt, ct_pack(da), ok, lane);   // dO
+        dres[k] = ds;                              // residual path -> d rep
+      }
+    }
+    flush_vec(dlg, c.g(ln.dg), lane);
+    flush_vec(dlb, c.g(ln.db), lane);
+  }
+  __syncthreads();
+  wgrad64(c.DQ, c.XB, m[7], c);
+  __syncthreads();
+  {
+    AFr Wq, Wk, Wv;
+    loadA(Wq, m[4].fa, lane);
+    loadA(Wk, m[5].fa, lane);
+    loadA(Wv, m[6].fa, lane);
+    const CT bq = ld_vec(m[4].b, lane), bk = ld_vec(m[5].b, lane), bv = ld_vec(m[6].b, lane);
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) {
+        const bool ok = tok_ok(rt, c);
+        const CTr x1 = ld_g(sv_x1, c.tok0, rt, c.NR, lane);
+        const CTr r = ct_pack(ld_gf(rep, c.tok0, rt, c.NR, lane));
+        CT q = bq, kk = bk, v = bv;
+        mm(q, Wq, r);
+        mm(kk, Wk, x1);
+        mm(v, Wv, x1);
+        st_lds(c.QB, rt, ct_pack(q), ok, lane);
+        st_lds(c.KB, rt, ct_pack(kk), ok, lane);
+        st_lds(c.VB, rt, ct_pack(v), ok, lane);
+        st_lds(c.XB, rt, x1, ok, lane);   // X of dWk / dWv
+      }
+    }
+  }
+  load_lse(sv_lse, c);
+  __syncthreads();
+  attn_bwd_q(c.QB, c.KB, c.VB, c.DA, c.DQ, true, c);
+  __syncthreads();
+  attn_bwd_kv(c.QB, c.KB, c.VB, c.DA, true, c);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < MAXRT; ++k) {   // q input (rep) into QB for dW_q
+    const int rt = c.wave + 4 * k;
+    if (rt < c.NT) st_lds(c.QB, rt, ct_pack(ld_gf(rep, c.tok0, rt, c.NR, lane)), tok_ok(rt, c), lane);
+  }
+  __syncthreads();
+  wgrad64(c.DQ, c.QB, m[4], c);
+  wgrad64(c.KB, c.XB, m[5], c);
+  wgrad64(c.VB, c.XB, m[6], c);
+  {
+    AFr Wq, Wk, Wv;
+    loadA(Wq, m[4].ba, lane);
+    loadA(Wk, m[5].ba, lane);
+    loadA(Wv, m[6].ba, lane);
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) {
+        mm(dres[k], Wq, ld_lds(c.DQ, rt, lane));
+        ct_zero(dx[k]);
+        mm(dx[k], Wk, ld_lds(c.KB, rt, lane));
+        mm(dx[k], Wv, ld_lds(c.VB, rt, lane));
+        // d rep read-modify-write (each row owned by exactly one wave of one workgroup)
+        st_gf(drep, c.tok0, rt, c.NR, ct_add(ld_gf(drep, c.tok0, rt, c.NR, lane), dres[k]), lane);
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------------------------------ action head
+// logits = W_h2 · LN(GELU(W_h1 x + b)) + b_h2  (ma_transformer.py:202-203,228); MA = ceil(A / 16) logit tiles
+template <int MA>
+struct HeadW { bf16x8 hi[MA][2], lo[MA][2]; };
+
+template <int MA>
+__device__ __forceinline__ void head_w(const DecP& p, HeadW<MA>& W, int lane) {
+  const int c16 = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int ma = 0; ma < MA; ++ma)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int a = 16 * ma + c16, k = 32 * s + 16 * (j >> 2) + 4 * g + (j & 3);
+        const float w = a < p.A ? p.wh2[(a < p.A ? a : 0) * 64 + k] : 0.f;
+        const uint16_t h = f2bf(w);
+        W.hi[ma][s][j] = (short)h;
+        W.lo[ma][s][j] = (short)f2bf(w - bf2f(h));
+      }
+}
+
+template <int MA>
+__device__ __forceinline__ void head_logits_ct(const DecP& p, const HeadW<MA>& W, const CT& n, f32x4* L, int lane) {
+  const int g = lane >> 4;
+  CTr nh, nl;
+  ct_split(n, nh, nl);
+#pragma unroll
+  for (int ma = 0; ma < MA; ++ma) {
+    f32x4 acc;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int a = 16 * ma + 4 * g + r;
+      acc[r] = a < p.A ? p.bh2[a] : 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(W.hi[ma][s], rb(nh, s), acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(W.hi[ma][s], rb(nl, s), acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(W.lo[ma][s], rb(nh, s), acc, 0, 0, 0);
+    }
+    L[ma] = acc;
+  }
+}
+
+// availability bits of this lane's logit slots (a = 16ma + 4g + r): bit 4ma + r set = masked
+template <int MA>
+__device__ __forceinline__ unsigned slot_mask(const DecP& p, size_t tok, int lane) {
+  if (!p.ava) return 0u;
+  const int g = lane >> 4;
+  unsigned m = 0u;
+#pragma unroll
+  for (int ma = 0; ma < MA; ++ma)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int a = 16 * ma + 4 * g + r;
+      if (a < p.A && p.ava[tok * p.A + a] == 0.f) m |= 1u << (4 * ma + r);
+    }
+  return m;
+}
+
+// per-token softmax statistics of the masked logits (transformer_act.py:14-21: logit[ava == 0] = -1e10)
+struct HeadStat { float lse, H, la, mean; };
+template <int MA>
+__device__ __forceinline__ HeadStat head_stats(const DecP& p, const f32x4* L, unsigned am, int act, bool disc, int lane) {
+  const int g = lane >> 4;
+  float mx = -INFINITY;
+#pragma unroll
+  for (int ma = 0; ma < MA; ++ma)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int a = 16 * ma + 4 * g + r;
+      const float l = ((am >> (4 * ma + r)) & 1u) ? -1e10f : L[ma][r];
+      if (a < p.A) mx = fmaxf(mx, l);
+    }
+  mx = cross_row_max(mx);
+  float se = 0.f, mean = 0.f;
+#pragma unroll
+  for (int ma = 0; ma < MA; ++ma)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int a = 16 * ma + 4 * g + r;
+      const float l = ((am >> (4 * ma + r)) & 1u) ? -1e10f : L[ma][r];
+      se += a < p.A ? __expf(l - mx) : 0.f;
+      mean += a == p.A - 1 ? L[ma][r] : 0.f;
+    }
+  HeadStat st;
+  st.lse = mx + __logf(cross_row_sum(se));
+  st.mean = cross_row_sum(mean);
+  float H = 0.f, la = 0.f;
+  if (disc) {
+#pragma unroll
+    for (int ma = 0; ma < MA; ++ma)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int a = 16 * ma + 4 * g + r;
+        const float l = (((am >> (4 * ma + r)) & 1u) ? -1e10f : L[ma][r]) - st.lse;
+        H -= a < p.A ? __expf(l) * l : 0.f;
+        la += a == act ? l : 0.f;
+      }
+  }
+  st.H = cross_row_sum(H);
+  st.la = cross_row_sum(la);
+  return st;
+}
+
+constexpr float HALF_LOG_2PI = 0.91893853320467274f;
+
+template <int MA>
+__device__ __forceinline__ void head_fwd_ct(const DecP& p, const CT* xr, bool save, const Ctx& c) {
+  const int lane = c.lane, g = lane >> 4;
+  HeadW<MA> W;
+  head_w<MA>(p, W, lane);
+  AFr H;
+  loadA(H, p.h1.fa, lane);
+  const CT bh = ld_vec(p.h1.b, lane), gam = ld_vec(p.lnh.g, lane), bet = ld_vec(p.lnh.b, lane);
+#pragma unroll
+  for (int k = 0; k < MAXRT; ++k) {
+    const int rt = c.wave + 4 * k;
+    if (rt < c.NT) {
+      const int row = rt * 16 + (lane & 15);
+      const bool ok = row < c.NR;
+      const size_t tok = (size_t)(c.tok0 + (ok ? row : 0));
+      const unsigned am = slot_mask<MA>(p, tok, lane);
+      const float actf = p.act[tok];
+      const CTr x = ct_pack(xr[k]);
+      if (save) st_g(p.sv_head, c.tok0, rt, c.NR, x, lane);
+      CT hh = bh, xh, n;
+      mm(hh, H, x);
+      gelu_ct(hh);
+      ln_fwd_ct(hh, xh, n, gam, bet);
+      f32x4 L[MA];
+      head_logits_ct<MA>(p, W, n, L, lane);
+      const bool disc = (row % c.L) < p.n_disc;
+      const int act = min(max((int)actf, 0), p.A - 1);
+      const HeadStat st = head_stats<MA>(p, L, am, act, disc, lane);
+      float lp, en;
+      if (disc) {
+        lp = st.la;
+        en = st.H;
+      } else {
+        const float sd = p.stdv[p.A - 1], z = (actf - st.mean) / sd;
+        lp = -0.5f * z * z - __logf(sd) - HALF_LOG_2PI;
+        en = 0.5f + HALF_LOG_2PI + __logf(sd);
+      }
+      if (ok && g == 0) {
+        p.logp[tok] = lp;
+        p.ent[tok] = en;
+      }
+    }
+  }
+}
+
+template <int MA>
+__device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c) {
+  const int lane = c.lane, g = lane >> 4;
+  constexpr int SB = (MA + 1) / 2;   // k-steps over the logit axis in dn = W_h2ᵀ dz
+  CT dlg, dlb;
+  ct_zero(dlg);
+  ct_zero(dlb);
+  float dls = 0.f;
+  {
+    HeadW<MA> W;
+    head_w<MA>(p, W, lane);
+    // W_h2ᵀ as A fragments: rows = features 16mt + (lane&15), k = logit index perm(s, g, j)
+    bf16x8 WT[4][SB];
+    {
+      const int c16 = lane & 15;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int s = 0; s < SB; ++s)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int a = 32 * s + 16 * (j >> 2) + 4 * g + (j & 3);
+            const float w = a < p.A ? p.wh2[(a < p.A ? a : 0) * 64 + 16 * mt + c16] : 0.f;
+            WT[mt][s][j] = (short)f2bf(w);
+          }
+    }
+    AFr Hf, Hb;
+    loadA(Hf, p.h1.fa, lane);
+    loadA(Hb, p.h1.ba, lane);
+    const CT bh = ld_vec(p.h1.b, lane), gam = ld_vec(p.lnh.g, lane), bet = ld_vec(p.lnh.b, lane);
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) {
+        const int row = rt * 16 + (lane & 15);
+        const bool ok = row < c.NR;
+        const size_t tok = (size_t)(c.tok0 + (ok ? row : 0));
+        const unsigned am = slot_mask<MA>(p, tok, lane);
+        const float actf = p.act[tok];
+        const float dlp = ok ? p.dlogp[tok] : 0.f, den = ok ? p.dent[tok] : 0.f;
+        const CTr x = ld_g(p.sv_head, c.tok0, rt, c.NR, lane);
+        CT hh = bh;
+        mm(hh, Hf, x);
+        CT gl = hh, xh, n;
+        gelu_ct(gl);
+        const float rs = ln_fwd_ct(gl, xh, n, gam, bet);
+        f32x4 L[MA];
+        head_logits_ct<MA>(p, W, n, L, lane);
+        const bool disc = (row % c.L) < p.n_disc;
+        const int act = min(max((int)actf, 0), p.A - 1);
+        const HeadStat st = head_stats<MA>(p, L, am, act, disc, lane);
+        // d loss / d logits of this lane's slots
+        f32x4 Z[2 * SB];
+#pragma unroll
+        for (int ma = 0; ma < 2 * SB; ++ma) Z[ma] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (disc) {
+#pragma unroll
+          for (int ma = 0; ma < MA; ++ma)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int a = 16 * ma + 4 * g + r;
+              const float l = (((am >> (4 * ma + r)) & 1u) ? -1e10f : L[ma][r]) - st.lse;
+              const float pr = __expf(l);
+              const float z = dlp * ((a == act ? 1.f : 0.f) - pr) - den * pr * (l + st.H);
+              Z[ma][r] = (ok && a < p.A) ? z : 0.f;
+            }
+        } else {
+          const float sd = p.stdv[p.A - 1], diff = actf - st.mean;
+#pragma unroll
+          for (int ma = 0; ma < MA; ++ma)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              Z[ma][r] = (ok && 16 * ma + 4 * g + r == p.A - 1) ? dlp * diff / (sd * sd) : 0.f;
+          if (ok && g == 0) {
+            const float dsd = dlp * (diff * diff / (sd * sd * sd) - 1.f / sd) + den / sd;
+            const float sg = 1.f / (1.f + __expf(-p.log_std[p.A - 1]));
+            dls += dsd * 0.5f * sg * (1.f - sg);
+          }
+        }
+        // dn = W_h2ᵀ dz (hi / lo split of dz)
+        CT dn;
+        ct_zero(dn);
+        CTr zh, zl;   // dz as a CT-shaped operand: piece ma = logits 16ma + 4g .. +3
+        {
+          CT zc;
+#pragma unroll
+          for (int ma = 0; ma < 4; ++ma) zc.v[ma] = ma < 2 * SB ? Z[ma < 2 * SB ? ma : 0] : f32x4{0.f, 0.f, 0.f, 0.f};
+          ct_split(zc, zh, zl);
+        }
+#pragma unroll
+        for (int s = 0; s < SB; ++s)
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) {
+            dn.v[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(WT[mt][s], rb(zh, s), dn.v[mt], 0, 0, 0);
+            dn.v[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(WT[mt][s], rb(zl, s), dn.v[mt], 0, 0, 0);
+          }
+        st_lds(c.DA, rt, zh, ok, lane);            // dY of W_h2 (logit axis in the feature slots)
+        st_lds(c.XB, rt, ct_pack(n), ok, lane);    // X of W_h2
+        CT dgg;
+        ln_bwd_ct(dn, xh, rs, gam, ok, dgg, dlg, dlb);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) dgg.v[i][q] = ok ? dgg.v[i][q] * gelu_erf_grad(hh.v[i][q]) : 0.f;
+        const CTr dgr = ct_pack(dgg);
+        st_lds(c.DQ, rt, dgr, ok, lane);   // dY of W_h1
+        st_lds(c.KB, rt, x, ok, lane);     // X of W_h1
+        ct_zero(dx[k]);
+        mm(dx[k], Hb, dgr);
+      }
+    }
+  }
+  flush_vec(dlg, c.g(p.lnh.dg), lane);
+  flush_vec(dlb, c.g(p.lnh.db), lane);
+  {
+    const float t = wave_sum(dls);
+    if (lane == 0 && p.d_log_std && p.n_disc < p.L) atomicAdd(c.g(p.d_log_std) + (p.A - 1), t);
+  }
+  __syncthreads();
+  wgrad_g(c.DA, c.XB, c.NRP, c.g(p.d_wh2), 64, p.A, 64, c.g(p.d_bh2), c.wave, lane);
+  wgrad64(c.DQ, c.KB, p.h1, c);
+  __syncthreads();
+}
+
+// ============================================================================================== forward
+template <int NB, bool SAVE>
+__device__ __forceinline__ void dec_fwd_tile(const DecP& p, char* smem, int seq0, int nseq) {
+  const Ctx c = make_ctx(p, smem, seq0, nseq);
+  if (c.nseq <= 0) return;
+  zero_lds(smem, mat_train_lds_bytes(p.NRP, p.SQ, p.L), c.tid);
+  __syncthreads();
+  const int lane = c.lane;
+  CT xr[MAXRT];
+  {
+    const CT gam = ld_vec(p.lnd_g, lane), bet = ld_vec(p.lnd_b, lane);
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) {
+        int tk;
+        CT pre = dec_embed_pre_ct(p, rt, tk, c), xh;
+        gelu_ct(pre);
+        ln_fwd_ct(pre, xh, xr[k], gam, bet);
+      }
+    }
+  }
+#pragma unroll 1
+  for (int b = 0; b < NB; ++b) {
+    const Blk& B = p.blk[b];
+    Ctx cc = c;
+    asm volatile("" : "+v"(cc.lane), "+v"(cc.tid));
+    self_attn_fwd_ct<SAVE>(B.m, B.ln[0], xr, true, p.sv[b].xin, p.sv[b].a1, p.sv[b].lse1, cc);
+    cross_attn_fwd_ct<SAVE>(B.m, B.ln[1], xr, p.rep, p.sv[b].x1, p.sv[b].a2, p.sv[b].lse2, cc);
+    mlp_fwd_ct<SAVE>(B.m[8], B.m[9], B.ln[2], xr, p.sv[b].x2, p.sv[b].h, cc);
+  }
+  const int MA = (p.A + 15) >> 4;
+  if (MA == 1) head_fwd_ct<1>(p, xr, SAVE, c);
+  else if (MA == 2) head_fwd_ct<2>(p, xr, SAVE, c);
+  else if (MA == 3) head_fwd_ct<3>(p, xr, SAVE, c);
+  else head_fwd_ct<4>(p, xr, SAVE, c);
+}
+
+template <int NB, bool SAVE>
+__global__ __launch_bounds__(256, WGPC) void mat_dec_fwd_ct(DecP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  FOR_TILES(p, (dec_fwd_tile<NB, SAVE>(p, smem, s0, ns)));
+}
+
+// ============================================================================================== backward
+template <int NB>
+__device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0, int nseq) {
+  const Ctx c = make_ctx(p, smem, seq0, nseq);
+  if (c.nseq <= 0) return;
+  zero_lds(smem, mat_train_lds_bytes(p.NRP, p.SQ, p.L), c.tid);
+  __syncthreads();
+  const int lane = c.lane;
+  CT dx[MAXRT];
+  {
+    const int MA = (p.A + 15) >> 4;
+    if (MA == 1) head_bwd_ct<1>(p, dx, c);
+    else if (MA == 2) head_bwd_ct<2>(p, dx, c);
+    else if (MA == 3) head_bwd_ct<3>(p, dx, c);
+    else head_bwd_ct<4>(p, dx, c);
+  }
+#pragma unroll 1
+  for (int bb = NB - 1; bb >= 0; --bb) {
+    const Blk& B = p.blk[bb];
+    Ctx cc = c;
+    asm volatile("" : "+v"(cc.lane), "+v"(cc.tid));
+    mlp_bwd_ct(B.m[8], B.m[9], B.ln[2], dx, p.sv[bb].x2, p.sv[bb].h, cc);
+    cross_attn_bwd_ct(B.m, B.ln[1], dx, p.rep, p.drep, p.sv[bb].x1, p.sv[bb].a2, p.sv[bb].lse2, cc);
+    self_attn_bwd_ct(B.m, B.ln[0], dx, p.sv[bb].xin, p.sv[bb].a1, p.sv[bb].lse1, true, cc);
+  }
+  // ---------------- embedding backward: dW_a[:, token] += d pre ; LN_dec params
+  {
+    float* EMB = (float*)c.QB;   // [(A+1)][64] f32 accumulators (QB + KB: 2 NRP x 128 B >= 65 x 256 B)
+    for (int i = c.tid; i < (p.A + 1) * 64; i += 256) EMB[i] = 0.f;
+    __syncthreads();
+    CT dlg, dlb;
+    ct_zero(dlg);
+    ct_zero(dlb);
+    const CT gam = ld_vec(p.lnd_g, lane), bet = ld_vec(p.lnd_b, lane);
+    const int g = lane >> 4;
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) {
+        const bool ok = tok_ok(rt, c);
+        int tk;
+        const CT pre = dec_embed_pre_ct(p, rt, tk, c);
+        CT e = pre, xh, yy, de;
+        gelu_ct(e);
+        const float rs = ln_fwd_ct(e, xh, yy, gam, bet);
+        ln_bwd_ct(dx[k], xh, rs, gam, ok, de, dlg, dlb);
+        if (ok) {
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              atomicAdd(EMB + tk * 64 + 16 * mt + 4 * g + r, de.v[mt][r] * gelu_erf_grad(pre.v[mt][r]));
+        }
+      }
+    }
+    flush_vec(dlg, c.g(p.d_lnd_g), lane);
+    flush_vec(dlb, c.g(p.d_lnd_b), lane);
+    __syncthreads();
+    if (p.d_wa)
+      for (int i = c.tid; i < (p.A + 1) * 64; i += 256) {
+        const int t = i / 64, col = i % 64;
+        atomicAdd(c.g(p.d_wa) + col * (p.A + 1) + t, EMB[i]);
+      }
+  }
+}
+
+template <int NB>
+__global__ __launch_bounds__(256, WGPC) void mat_dec_bwd_ct(DecP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  FOR_TILES(p, (dec_bwd_tile<NB>(p, smem, s0, ns)));
+}
+
+}  // namespace
+
+MDL_API int mdl_mat_dec_fwd_ct(const DecP* p, int NB, int save, hipStream_t st) {
+  if (p->A > 64 || p->A < 1) return -1;
+  if (NB == 1) return save ? launch(mat_dec_fwd_ct<1, true>, p, st) : launch(mat_dec_fwd_ct<1, false>, p, st);
+  if (NB == 2) return save ? launch(mat_dec_fwd_ct<2, true>, p, st) : launch(mat_dec_fwd_ct<2, false>, p, st);
+  if (NB == 3) return save ? launch(mat_dec_fwd_ct<3, true>, p, st) : launch(mat_dec_fwd_ct<3, false>, p, st);
+  return -3;
+}
+
+MDL_API int mdl_mat_dec_bwd_ct(const DecP* p, int NB, hipStream_t st) {
+  if (p->A > 64 || p->A < 1 || 2 * p->NRP * 128 < (p->A + 1) * 256) return -1;
+  if (NB == 1) return launch(mat_dec_bwd_ct<1>, p, st);
+  if (NB == 2) return launch(mat_dec_bwd_ct<2>, p, st);
+  if (NB == 3) return launch(mat_dec_bwd_ct<3>, p, st);
+  return -3;
+}

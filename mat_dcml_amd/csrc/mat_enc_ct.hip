@@ -1,0 +1,372 @@
+// Fused MAT encoder forward / backward, token-on-lane tiles (mat_train_ct.h).  Reference: ma_transformer.py:72-92
+// (EncodeBlock), :119-154 (Encoder: obs_encoder = LN(obs_dim) -> Linear -> GELU, ln, blocks, value head).
+//
+// Observation embedding: obs_dim <= 16 runs in-kernel (LN_obs per lane, W_e on MFMA with a hi/lo split of the
+// LN output); larger observations (SMAC: 1288) come in as the embedding pre-activation `pre_in` computed by the
+// obs-embedding GEMM kernels (obs_embed.hip), and the backward hands d pre back through `dpre_out`.
+#include "mat_train_ct.h"
+
+namespace {
+
+struct EncX {   // EncP extension of the round-2 kernels (passed next to EncP)
+  const float* pre_in;   // [tok][64] embedding pre-activation (null: embed obs in-kernel, obs_dim <= 16)
+  float* dpre_out;       // [tok][64] gradient w.r.t. pre_in (backward, when pre_in is used)
+};
+
+// LN_obs of this lane's token (all od <= 16 dims in-lane); the lane's 4 dims 4g .. 4g+3 of (LN output, x-hat)
+__device__ __forceinline__ void obs_ln(const EncP& p, int rt, const Ctx& c, float oh[4], float hat[4]) {
+  const int lane = c.lane, g = lane >> 4, od = p.od;
+  const int row = rt * 16 + (lane & 15);
+  const bool ok = row < c.NR;
+  const float* src = p.obs + (size_t)(c.tok0 + (ok ? row : 0)) * od;
+  float o[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) o[k] = src[k < od ? k : 0];
+  float mean = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) mean += k < od ? o[k] : 0.f;
+  mean /= (float)od;
+  float var = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const float d = o[k] - mean;
+    var += k < od ? d * d : 0.f;
+  }
+  const float rstd = rsqrtf(var / (float)od + 1e-5f);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float hv = 0.f;
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) hv = g == gg ? (o[4 * gg + j] - mean) * rstd : hv;
+    const int kk = 4 * g + j;
+    const bool in = kk < od;
+    const int ks = in ? kk : 0;
+    hat[j] = in ? hv : 0.f;
+    oh[j] = in ? hv * p.lno_g[ks] + p.lno_b[ks] : 0.f;
+  }
+}
+
+// W_e (64 x od, fp32) as A fragments: rows 16mt + (lane&15), k = obs dim 4g + j (j < 4; j >= 4 -> dims >= 16: 0)
+__device__ __forceinline__ void we_frags(const EncP& p, bf16x8 W[4], int lane) {
+  const int c16 = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kk = 4 * g + j;
+      const bool in = j < 4 && kk < p.od;
+      const float w = p.we[(16 * mt + c16) * p.od + (in ? kk : 0)];
+      W[mt][j] = (short)f2bf(in ? w : 0.f);
+    }
+}
+// W_eᵀ as A fragments for d(LN_obs out) = W_eᵀ d pre: rows = obs dim (lane&15), k = features perm(s, g, j)
+__device__ __forceinline__ void weT_frags(const EncP& p, bf16x8 W[2], int lane) {
+  const int c16 = lane & 15, g = lane >> 4;
+  const bool in = c16 < p.od;
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int f = 32 * s + 16 * (j >> 2) + 4 * g + (j & 3);
+      const float w = p.we[f * p.od + (in ? c16 : 0)];
+      W[s][j] = (short)f2bf(in ? w : 0.f);
+    }
+}
+
+__device__ __forceinline__ CT embed_pre(const EncP& p, const EncX& x, int rt, const bf16x8 W[4], float oh[4], float hat[4],
+                                        const Ctx& c) {
+  if (x.pre_in) return ld_gf(x.pre_in, c.tok0, rt, c.NR, c.lane);
+  obs_ln(p, rt, c, oh, hat);
+  const uint32_t h01 = pk2(oh[0], oh[1]), h23 = pk2(oh[2], oh[3]);
+  const uint32_t l01 = pk2(oh[0] - blo(h01), oh[1] - bhi(h01)), l23 = pk2(oh[2] - blo(h23), oh[3] - bhi(h23));
+  const bf16x8 bh = mk8(h01, h23, 0u, 0u), bl = mk8(l01, l23, 0u, 0u);
+  CT pre = ld_vec(p.be, c.lane);
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    pre.v[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(W[mt], bh, pre.v[mt], 0, 0, 0);
+    pre.v[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(W[mt], bl, pre.v[mt], 0, 0, 0);
+  }
+  return pre;
+}
+
+// ============================================================================================== forward
+template <int NB, bool SAVE>
+__device__ __forceinline__ void enc_fwd_tile(const EncP& p, const EncX& ex, char* smem, int seq0, int nseq) {
+  const Ctx c = make_ctx(p, smem, seq0, nseq);
+  if (c.nseq <= 0) return;
+  zero_lds(smem, mat_train_lds_bytes(p.NRP, p.SQ, p.L), c.tid);
+  __syncthreads();
+  const int lane = c.lane, g = lane >> 4;
+  CT xr[MAXRT];
+  {
+    bf16x8 W[4];
+    if (!ex.pre_in) we_frags(p, W, lane);
+    const CT gam = ld_vec(p.ln0_g, lane), bet = ld_vec(p.ln0_b, lane);
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) {
+        float oh[4], hat[4];
+        CT pre = embed_pre(p, ex, rt, W, oh, hat, c), xh;
+        gelu_ct(pre);
+        ln_fwd_ct(pre, xh, xr[k], gam, bet);
+      }
+    }
+  }
+#pragma unroll 1
+  for (int b = 0; b < NB; ++b) {
+    const Blk& B = p.blk[b];
+    Ctx cc = c;   // opaque per-iteration lane id: keeps hipcc from hoisting (and spilling) every LDS address
+    asm volatile("" : "+v"(cc.lane), "+v"(cc.tid));
+    self_attn_fwd_ct<SAVE>(B.m, B.ln[0], xr, false, p.sv[b].xin, p.sv[b].a1, p.sv[b].lse1, cc);
+    mlp_fwd_ct<SAVE>(B.m[8], B.m[9], B.ln[1], xr, p.sv[b].x1, p.sv[b].h, cc);
+  }
+  // value head: v = W_v2 · LN(GELU(W_v1 · rep + b)) + b   (ma_transformer.py:138-139,152)
+  AFr H;
+  loadA(H, p.h1.fa, lane);
+  const CT bh = ld_vec(p.h1.b, lane), gam = ld_vec(p.lnh.g, lane), bet = ld_vec(p.lnh.b, lane);
+  const CT w0 = ld_vec(p.wh2, lane);
+  CT w1;
+  if (p.n_obj > 1) w1 = ld_vec(p.wh2 + 64, lane); else ct_zero(w1);
+#pragma unroll
+  for (int k = 0; k < MAXRT; ++k) {
+    const int rt = c.wave + 4 * k;
+    if (rt < c.NT) {
+      const bool ok = tok_ok(rt, c);
+      if (p.rep) st_gf(p.rep, c.tok0, rt, c.NR, xr[k], lane);
+      CT hh = bh, xh, n;
+      mm(hh, H, ct_pack(xr[k]));
+      gelu_ct(hh);
+      ln_fwd_ct(hh, xh, n, gam, bet);
+      float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          s0 += n.v[i][r] * w0.v[i][r];
+          s1 += n.v[i][r] * w1.v[i][r];
+        }
+      s0 = cross_row_sum(s0);
+      s1 = cross_row_sum(s1);
+      if (ok && g == 0) {
+        const size_t tok = (size_t)(c.tok0 + rt * 16 + (lane & 15));
+        p.v[tok * p.n_obj] = s0 + p.bh2[0];
+        if (p.n_obj > 1) p.v[tok * p.n_obj + 1] = s1 + p.bh2[1];
+      }
+    }
+  }
+}
+
+template <int NB, bool SAVE>
+__global__ __launch_bounds__(256, WGPC) void mat_enc_fwd_ct(EncP p, EncX ex) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  FOR_TILES(p, (enc_fwd_tile<NB, SAVE>(p, ex, smem, s0, ns)));
+}
+
+// ============================================================================================== backward
+template <int NB>
+__device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char* smem, int seq0, int nseq) {
+  const Ctx c = make_ctx(p, smem, seq0, nseq);
+  if (c.nseq <= 0) return;
+  zero_lds(smem, mat_train_lds_bytes(p.NRP, p.SQ, p.L), c.tid);
+  __syncthreads();
+  const int lane = c.lane;
+  CT dx[MAXRT];
+  // ---------------- value head backward (+ incoming d rep from the decoder)
+  {
+    CT dlg, dlb, dw0, dw1;
+    ct_zero(dlg);
+    ct_zero(dlb);
+    ct_zero(dw0);
+    ct_zero(dw1);
+    AFr Hf, Hb;
+    loadA(Hf, p.h1.fa, lane);
+    loadA(Hb, p.h1.ba, lane);
+    const CT bh = ld_vec(p.h1.b, lane), gam = ld_vec(p.lnh.g, lane), bet = ld_vec(p.lnh.b, lane);
+    const CT w0 = ld_vec(p.wh2, lane);
+    CT w1;
+    if (p.n_obj > 1) w1 = ld_vec(p.wh2 + 64, lane); else ct_zero(w1);
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) {
+        const bool ok = tok_ok(rt, c);
+        const size_t tok = (size_t)(c.tok0 + (ok ? rt * 16 + (lane & 15) : 0));
+        const float dv0 = ok ? p.dv[tok * p.n_obj] : 0.f;
+        const float dv1 = (ok && p.n_obj > 1) ? p.dv[tok * p.n_obj + 1] : 0.f;
+        const CTr r = ct_pack(ld_gf(p.rep, c.tok0, rt, c.NR, lane));
+        CT hh = bh;
+        mm(hh, Hf, r);
+        CT gl = hh, xh, n, dn, dg;
+        gelu_ct(gl);
+        const float rs = ln_fwd_ct(gl, xh, n, gam, bet);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            dn.v[i][q] = dv0 * w0.v[i][q] + dv1 * w1.v[i][q];
+            dw0.v[i][q] += dv0 * n.v[i][q];
+            dw1.v[i][q] += dv1 * n.v[i][q];
+          }
+        ln_bwd_ct(dn, xh, rs, gam, ok, dg, dlg, dlb);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) dg.v[i][q] = ok ? dg.v[i][q] * gelu_erf_grad(hh.v[i][q]) : 0.f;
+        const CTr dgr = ct_pack(dg);
+        st_lds(c.DQ, rt, dgr, ok, lane);   // dY of W_h1
+        st_lds(c.XB, rt, r, ok, lane);     // X of W_h1
+        CT t = ld_gf(p.drep, c.tok0, rt, c.NR, lane);
+        mm(t, Hb, dgr);
+        dx[k] = t;
+      }
+    }
+    flush_vec(dlg, c.g(p.lnh.dg), lane);
+    flush_vec(dlb, c.g(p.lnh.db), lane);
+    flush_vec(dw0, c.g(p.d_wh2), lane);
+    if (p.n_obj > 1) flush_vec(dw1, c.g(p.d_wh2 ? p.d_wh2 + 64 : nullptr), lane);
+    __syncthreads();
+    wgrad64(c.DQ, c.XB, p.h1, c);
+    __syncthreads();
+  }
+  // ---------------- blocks in reverse
+#pragma unroll 1
+  for (int bb = NB - 1; bb >= 0; --bb) {
+    const Blk& B = p.blk[bb];
+    Ctx cc = c;
+    asm volatile("" : "+v"(cc.lane), "+v"(cc.tid));
+    mlp_bwd_ct(B.m[8], B.m[9], B.ln[1], dx, p.sv[bb].x1, p.sv[bb].h, cc);
+    self_attn_bwd_ct(B.m, B.ln[0], dx, p.sv[bb].xin, p.sv[bb].a1, p.sv[bb].lse1, false, cc);
+  }
+  // ---------------- embedding backward: x0 = LN0(GELU(pre)), pre = W_e · LN_obs(obs) + b_e
+  {
+    CT dlg, dlb, dbe;
+    ct_zero(dlg);
+    ct_zero(dlb);
+    ct_zero(dbe);
+    f32x4 dog = {0.f, 0.f, 0.f, 0.f}, dob = {0.f, 0.f, 0.f, 0.f};
+    bf16x8 W[4], WT[2];
+    if (!ex.pre_in) {
+      we_frags(p, W, lane);
+      weT_frags(p, WT, lane);
+    }
+    const CT gam = ld_vec(p.ln0_g, lane), bet = ld_vec(p.ln0_b, lane);
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) {
+        const bool ok = tok_ok(rt, c);
+        float oh[4] = {0.f, 0.f, 0.f, 0.f}, hat[4] = {0.f, 0.f, 0.f, 0.f};
+        const CT pre = embed_pre(p, ex, rt, W, oh, hat, c);
+        CT e = pre, xh, yy, de;
+        gelu_ct(e);
+        const float rs = ln_fwd_ct(e, xh, yy, gam, bet);
+        ln_bwd_ct(dx[k], xh, rs, gam, ok, de, dlg, dlb);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) de.v[i][q] = ok ? de.v[i][q] * gelu_erf_grad(pre.v[i][q]) : 0.f;
+        if (ex.pre_in) {
+          st_gf(ex.dpre_out, c.tok0, rt, c.NR, de, lane);
+          continue;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dbe.v[i] += de.v[i];
+        CTr dh, dl;
+        ct_split(de, dh, dl);
+        st_lds(c.DA, rt, dh, ok, lane);   // dY of W_e
+        CTr xo = ct_zero_r();
+        xo.q[0] = make_uint2(pk2(oh[0], oh[1]), pk2(oh[2], oh[3]));
+        st_lds(c.XB, rt, xo, ok, lane);   // X of W_e (obs dims 0..15 = features 0..15 of the LDS row)
+        // d(LN_obs output)[dim 4g + r] of this lane's token
+        f32x4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(WT[s], rb(dh, s), d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(WT[s], rb(dl, s), d, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          dog[r] += ok ? d[r] * hat[r] : 0.f;
+          dob[r] += ok ? d[r] : 0.f;
+        }
+      }
+    }
+    flush_vec(dlg, c.g(p.d_ln0_g), lane);
+    flush_vec(dlb, c.g(p.d_ln0_b), lane);
+    if (!ex.pre_in) {
+      flush_vec(dbe, c.g(p.d_be), lane);
+      const int c16 = lane & 15, g = lane >> 4;
+      float og = 0.f, ob = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float a = group_sum<16>(dog[r]), b = group_sum<16>(dob[r]);
+        og = c16 == r ? a : og;
+        ob = c16 == r ? b : ob;
+      }
+      const int dim = 4 * g + c16;
+      if (c16 < 4 && dim < p.od) {
+        if (p.d_lno_g) atomicAdd(c.g(p.d_lno_g) + dim, og);
+        if (p.d_lno_b) atomicAdd(c.g(p.d_lno_b) + dim, ob);
+      }
+      __syncthreads();
+      wgrad_g(c.DA, c.XB, c.NRP, c.g(p.d_we), p.od, 64, p.od, nullptr, c.wave, lane);
+    }
+  }
+}
+
+template <int NB>
+__global__ __launch_bounds__(256, WGPC) void mat_enc_bwd_ct(EncP p, EncX ex) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  FOR_TILES(p, (enc_bwd_tile<NB>(p, ex, smem, s0, ns)));
+}
+
+template <typename K>
+int launch_x(K kern, const EncP* p, const EncX& ex, hipStream_t st) {
+  if (p->SQ <= 0 || p->NRP <= 0 || (p->SQ * p->L + 15) / 16 > 4 * MAXRT) return -4;
+  const size_t lds = mat_train_lds_bytes(p->NRP, p->SQ, p->L);
+  if (lds > LDS_BUDGET) return -2;
+  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return (int)e;
+  const int tiles = (p->Bs + p->SQ - 1) / p->SQ;
+  const int grid = tiles < n_cus() * WGPC ? tiles : n_cus() * WGPC;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, *p, ex);
+  MDL_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace
+
+// ============================================================================================== host API
+MDL_API int mdl_mat_train_geometry_ct(int L) {
+  const int MAXROWS = 64 * MAXRT;
+  int SQ = MAXROWS / L;
+  if (SQ < 1) return 0;
+  int NRP = ((SQ * L + 31) / 32) * 32;
+  if (NRP < 64) NRP = 64;
+  while (SQ > 1 && (NRP > MAXROWS || mat_train_lds_bytes(NRP, SQ, L) > LDS_BUDGET)) {
+    --SQ;
+    NRP = ((SQ * L + 31) / 32) * 32;
+    if (NRP < 64) NRP = 64;
+  }
+  if (mat_train_lds_bytes(NRP, SQ, L) > LDS_BUDGET || (SQ * L + 15) / 16 > 4 * MAXRT) return 0;
+  return SQ | (NRP << 16);
+}
+
+MDL_API int mdl_mat_enc_fwd_ct(const EncP* p, const float* pre_in, int NB, int save, hipStream_t st) {
+  if ((!pre_in && (p->od > 16 || p->od < 1)) || p->n_obj > 2 || p->n_obj < 1) return -1;
+  const EncX ex{pre_in, nullptr};
+  if (NB == 1) return save ? launch_x(mat_enc_fwd_ct<1, true>, p, ex, st) : launch_x(mat_enc_fwd_ct<1, false>, p, ex, st);
+  if (NB == 2) return save ? launch_x(mat_enc_fwd_ct<2, true>, p, ex, st) : launch_x(mat_enc_fwd_ct<2, false>, p, ex, st);
+  if (NB == 3) return save ? launch_x(mat_enc_fwd_ct<3, true>, p, ex, st) : launch_x(mat_enc_fwd_ct<3, false>, p, ex, st);
+  return -3;
+}
+
+MDL_API int mdl_mat_enc_bwd_ct(const EncP* p, const float* pre_in, float* dpre_out, int NB, hipStream_t st) {
+  if ((!pre_in && (p->od > 16 || p->od < 1)) || p->n_obj > 2 || p->n_obj < 1 || (pre_in && !dpre_out)) return -1;
+  const EncX ex{pre_in, dpre_out};
+  if (NB == 1) return launch_x(mat_enc_bwd_ct<1>, p, ex, st);
+  if (NB == 2) return launch_x(mat_enc_bwd_ct<2>, p, ex, st);
+  if (NB == 3) return launch_x(mat_enc_bwd_ct<3>, p, ex, st);
+  return -3;
+}

@@ -51,7 +51,9 @@ constexpr int MAXRT = MDL_MAXRT;  // row tiles per wave (NT <= 4 * MAXRT)
 constexpr int WGPC = MDL_WGPC;
 constexpr int LDS_BUDGET = 160 * 1024 / WGPC;
 
-struct Mat { const bf16_t* fw; const bf16_t* bw; const float* b; float* dW; float* db; };
+// fw / bw: B fragments of W / Wᵀ (row-layout tiles); fa / ba: A fragments of W / Wᵀ with the permuted k order of
+// the token-on-lane tiles (mat_train_ct.h)
+struct Mat { const bf16_t* fw; const bf16_t* bw; const float* b; float* dW; float* db; const bf16_t* fa; const bf16_t* ba; };
 struct LNp { const float* g; const float* b; float* dg; float* db; };
 struct Blk { Mat m[10]; LNp ln[3]; };
 struct Sv { bf16_t* xin; bf16_t* a1; float* lse1; bf16_t* x1; bf16_t* a2; float* lse2; bf16_t* x2; bf16_t* h; };

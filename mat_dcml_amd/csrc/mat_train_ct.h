@@ -1,0 +1,533 @@
+// Round-2 fused MAT training tiles for gfx950: token-on-lane ("CT") register layout.
+//
+// Round 1 kept every activation in the MFMA C layout of Y = X·Wᵀ (rows = tokens in registers, one feature column
+// per lane).  The next linear needs the token on the lane, so EVERY linear went through LDS: 16 ds_write_b16 +
+// 16 cvt + 16 mask multiplies per lane, an lgkmcnt(0) drain, two ds_read_b128 — and LayerNorm needed 4 DPP
+// steps per row.  At one wave per SIMD those drains were most of the kernels' 57 % s_waitcnt time and the
+// conversion work most of their 27 VALU instructions per MFMA (profiles/r1_occupancy_ab.md).
+//
+// CT computes the transposed product Yᵀ = W·Xᵀ instead: A operand = weight rows, B operand = the activation with
+// the TOKEN on the lane (lane&15) and 8 features per lane.  Its C layout (lane (g, c) holds features 16mt+4g+r of
+// token c) is already the next product's B operand once two 16-row tiles are packed to bf16 — provided the weight
+// fragment uses the same permuted k order perm(s, g, j) = 32s + 16(j>>2) + 4g + (j&3) (packed once per optimizer
+// step, csrc/rl_ops.hip pack_weights "fa"/"ba").  So:
+//  * linear → bias → GELU → linear → residual → LayerNorm chains never touch LDS (MLP forward: zero LDS ops);
+//  * biases / residuals initialise the MFMA accumulators (no separate adds);
+//  * per-token statistics (LayerNorm, softmax of the action head, value head) reduce 16 values in-lane and then
+//    only across the 4 lanes of the token (v_permlane16/32_swap, no LDS);
+//  * the operands of the attention (Q/K/V) and of the weight gradients (dY, X) go to the token-major swizzled LDS
+//    tiles of round 1 with one ds_write_b64 per 4 features (was 4 ds_write_b16), so the round-1 MFMA attention and
+//    the transposed-read weight-gradient GEMMs are reused unchanged;
+//  * bias gradients come out of the weight-gradient MFMA loop (one extra MFMA against a ones fragment).
+// Reference semantics: ma_transformer.py:24-230 (encoder / decoder blocks), transformer_act.py:103-129 (heads).
+#pragma once
+#include "mat_train_common.h"
+
+namespace {
+
+struct CT { f32x4 v[4]; };          // v[mt][r] = feature 16mt + 4g + r of token (lane & 15) of a 16-token tile
+struct CTr { uint2 q[4]; };         // the same as packed bf16: q[mt] = features 16mt+4g .. +3
+struct AFr { bf16x8 f[4][2]; };     // A fragments of a 64x64 weight (rows 16mt + lane&15, k-step s, perm k order)
+
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t pk2(float a, float b) {   // one v_cvt_pk_bf16_f32 (RNE)
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){a, b}, bf16x2v));
+}
+__device__ __forceinline__ bf16x8 mk8(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  return __builtin_bit_cast(bf16x8, (u32x4v){a, b, c, d});
+}
+__device__ __forceinline__ float blo(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bhi(uint32_t u) { return __uint_as_float(u & 0xFFFF0000u); }
+
+__device__ __forceinline__ void ct_zero(CT& t) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) t.v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+__device__ __forceinline__ CT ct_add(const CT& a, const CT& b) {
+  CT o;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o.v[i] = a.v[i] + b.v[i];
+  return o;
+}
+__device__ __forceinline__ CTr ct_pack(const CT& x) {
+  CTr r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r.q[i] = make_uint2(pk2(x.v[i][0], x.v[i][1]), pk2(x.v[i][2], x.v[i][3]));
+  return r;
+}
+__device__ __forceinline__ CT ct_unpack(const CTr& r) {
+  CT x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) x.v[i] = f32x4{blo(r.q[i].x), bhi(r.q[i].x), blo(r.q[i].y), bhi(r.q[i].y)};
+  return x;
+}
+__device__ __forceinline__ CTr ct_zero_r() {
+  CTr r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r.q[i] = make_uint2(0u, 0u);
+  return r;
+}
+// k-step s of the B operand (features perm(s, g, j))
+__device__ __forceinline__ bf16x8 rb(const CTr& r, int s) {
+  return mk8(r.q[2 * s].x, r.q[2 * s].y, r.q[2 * s + 1].x, r.q[2 * s + 1].y);
+}
+// x ≈ hi + lo, both bf16 (≈16 significant bits) for the few products that need fp32-like accuracy
+__device__ __forceinline__ void ct_split(const CT& x, CTr& hi, CTr& lo) {
+  hi = ct_pack(x);
+  const CT h = ct_unpack(hi);
+  CT d;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) d.v[i] = x.v[i] - h.v[i];
+  lo = ct_pack(d);
+}
+
+__device__ __forceinline__ void loadA(AFr& W, const bf16_t* pk, int lane) {
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) W.f[mt][s] = *(const bf16x8*)(pk + ((size_t)((mt * 2 + s) * 64 + lane)) * 8);
+}
+
+// acc += W · x  (acc initialised by the caller: zero, bias, bias + residual)
+__device__ __forceinline__ void mm(CT& acc, const AFr& W, const CTr& x) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const bf16x8 b = rb(x, s);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) acc.v[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(W.f[mt][s], b, acc.v[mt], 0, 0, 0);
+  }
+}
+
+// 64-float parameter vector as a CT (16-byte aligned: parameters are padded to 16 floats, ops/ppo_fused.PAD)
+__device__ __forceinline__ CT ld_vec(const float* p, int lane) {
+  const int g = lane >> 4;
+  CT x;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) x.v[mt] = *(const f32x4*)(p + 16 * mt + 4 * g);
+  return x;
+}
+
+__device__ __forceinline__ void gelu_ct(CT& t) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) t.v[i][r] = gelu_erf(t.v[i][r]);
+}
+
+__device__ __forceinline__ float cross_row_max(float x) {
+  float a, b;
+  swap16(x, a, b);
+  x = fmaxf(a, b);
+  swap32(x, a, b);
+  return fmaxf(a, b);
+}
+
+__device__ __forceinline__ bool tok_ok(int rt, const Ctx& c) { return rt * 16 + (c.lane & 15) < c.NR; }
+
+// ------------------------------------------------------------------------------------------ LDS / global moves
+// token-major swizzled LDS rows (tile.h tmo): piece mt of lane (g, c) = 8 bytes at column 16mt + 4g of row c
+__device__ __forceinline__ void st_lds(bf16_t* buf, int rt, const CTr& x, bool ok, int lane) {
+  const int g = lane >> 4, row = rt * 16 + (lane & 15);
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) *(uint2*)(buf + tmo(row, 16 * mt + 4 * g)) = ok ? x.q[mt] : make_uint2(0u, 0u);
+}
+__device__ __forceinline__ CTr ld_lds(const bf16_t* buf, int rt, int lane) {
+  const int g = lane >> 4, row = rt * 16 + (lane & 15);
+  CTr x;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) x.q[mt] = *(const uint2*)(buf + tmo(row, 16 * mt + 4 * g));
+  return x;
+}
+// plain global [tok][64] bf16 (rows >= NR read as zero / not written)
+__device__ __forceinline__ CTr ld_g(const bf16_t* src, int tok0, int rt, int NR, int lane) {
+  const int g = lane >> 4, row = rt * 16 + (lane & 15);
+  const bool ok = row < NR;
+  const bf16_t* base = src + (size_t)(tok0 + (ok ? row : 0)) * 64 + 4 * g;
+  CTr x;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    const uint2 v = *(const uint2*)(base + 16 * mt);
+    x.q[mt] = ok ? v : make_uint2(0u, 0u);
+  }
+  return x;
+}
+__device__ __forceinline__ void st_g(bf16_t* dst, int tok0, int rt, int NR, const CTr& x, int lane) {
+  const int g = lane >> 4, row = rt * 16 + (lane & 15);
+  if (row < NR) {
+    bf16_t* base = dst + (size_t)(tok0 + row) * 64 + 4 * g;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) *(uint2*)(base + 16 * mt) = x.q[mt];
+  }
+}
+// plain global [tok][64] f32
+__device__ __forceinline__ CT ld_gf(const float* src, int tok0, int rt, int NR, int lane) {
+  const int g = lane >> 4, row = rt * 16 + (lane & 15);
+  const bool ok = row < NR;
+  const float* base = src + (size_t)(tok0 + (ok ? row : 0)) * 64 + 4 * g;
+  CT x;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    const f32x4 v = *(const f32x4*)(base + 16 * mt);
+    x.v[mt] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  return x;
+}
+__device__ __forceinline__ void st_gf(float* dst, int tok0, int rt, int NR, const CT& x, int lane) {
+  const int g = lane >> 4, row = rt * 16 + (lane & 15);
+  if (row < NR) {
+    float* base = dst + (size_t)(tok0 + row) * 64 + 4 * g;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) *(f32x4*)(base + 16 * mt) = x.v[mt];
+  }
+}
+
+// ------------------------------------------------------------------------------------------ LayerNorm (per token)
+__device__ __forceinline__ float tok_sum(const CT& x) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) s += (x.v[i][0] + x.v[i][1]) + (x.v[i][2] + x.v[i][3]);
+  return cross_row_sum(s);
+}
+// y = LN(x) * gamma + beta; returns rstd, xh = normalised x
+__device__ __forceinline__ float ln_fwd_ct(const CT& x, CT& xh, CT& y, const CT& gam, const CT& bet) {
+  const float mean = tok_sum(x) * (1.f / 64.f);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float d = x.v[i][r] - mean;
+      xh.v[i][r] = d;
+      q += d * d;
+    }
+  const float rstd = rsqrtf(cross_row_sum(q) * (1.f / 64.f) + 1e-5f);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      xh.v[i][r] *= rstd;
+      y.v[i][r] = xh.v[i][r] * gam.v[i][r] + bet.v[i][r];
+    }
+  return rstd;
+}
+// dx from dy (tokens with ok == false contribute nothing); per-lane gamma / beta gradient partials in dg / db
+__device__ __forceinline__ void ln_bwd_ct(const CT& dy, const CT& xh, float rstd, const CT& gam, bool ok, CT& dx, CT& dg,
+                                          CT& db) {
+  CT gy;
+  float a = 0.f, b = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float d = ok ? dy.v[i][r] : 0.f;
+      gy.v[i][r] = d * gam.v[i][r];
+      a += gy.v[i][r];
+      b += gy.v[i][r] * xh.v[i][r];
+      dg.v[i][r] += d * xh.v[i][r];
+      db.v[i][r] += d;
+    }
+  a = cross_row_sum(a) * (1.f / 64.f);
+  b = cross_row_sum(b) * (1.f / 64.f);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dx.v[i][r] = (gy.v[i][r] - a - xh.v[i][r] * b) * rstd;
+}
+
+// per-lane feature partials (summed over the tokens the lane saw) -> one atomic per feature: reduce over the 16
+// token lanes of each row (DPP), then lane (g, c) adds feature 16(c>>2) + 4g + (c&3)
+__device__ __forceinline__ void flush_vec(const CT& acc, float* dst, int lane) {
+  if (!dst) return;
+  const int c = lane & 15, g = lane >> 4;
+  float out = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float s = group_sum<16>(acc.v[i][r]);
+      out = (c == 4 * i + r) ? s : out;
+    }
+  atomicAdd(dst + 16 * (c >> 2) + 4 * g + (c & 3), out);
+}
+
+// ------------------------------------------------------------------------------------------ weight gradients
+// dW[n][k] (row stride ld) += Σ_t Y[t][n] X[t][k] for n < nrows, k < ncols, and db[n] += Σ_t Y[t][n], from
+// token-major swizzled LDS tiles of KP rows (KP % 32 == 0, padded rows zero).  Wave w owns dW rows [16w, 16w+16).
+// The bias gradient is one extra MFMA per k-step against a ones fragment.  fp32 atomics.
+__device__ __forceinline__ void wgrad_g(const bf16_t* Y, const bf16_t* X, int KP, float* dW, int ld, int nrows, int ncols,
+                                        float* db, int wave, int lane) {
+  if ((!dW && !db) || 16 * wave >= nrows) return;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int nct = dW ? (ncols + 15) >> 4 : 0;
+  RT acc;
+  rt_zero(acc);
+  f32x4 accb = {0.f, 0.f, 0.f, 0.f};
+  const bf16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
+  for (int k0 = 0; k0 < KP; k0 += 32) {
+    const bf16x8 a = ld_frag_T(Y, k0, 16 * wave, lane);
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      if (ct < nct) {
+        const bf16x8 b = ld_frag_T(X, k0, 16 * ct, lane);
+        acc.v[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc.v[ct], 0, 0, 0);
+      }
+    }
+    if (db) accb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ones, accb, 0, 0, 0);
+  }
+  if (dW) {
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = 16 * wave + 4 * g + r, k = 16 * ct + c16;
+        if (ct < nct && n < nrows && k < ncols) atomicAdd(dW + n * ld + k, acc.v[ct][r]);
+      }
+  }
+  if (db && c16 < 4) {
+    const float v = c16 == 0 ? accb[0] : c16 == 1 ? accb[1] : c16 == 2 ? accb[2] : accb[3];
+    const int n = 16 * wave + 4 * g + c16;
+    if (n < nrows) atomicAdd(db + n, v);
+  }
+}
+__device__ __forceinline__ void wgrad64(const bf16_t* Y, const bf16_t* X, const Mat& m, const Ctx& c) {
+  wgrad_g(Y, X, c.NRP, c.g(m.dW), 64, 64, 64, c.g(m.db), c.wave, c.lane);
+}
+
+// ------------------------------------------------------------------------------------------ sublayers (forward)
+// self attention: x <- LN(x + proj(attn(q(x), k(x), v(x))))   (ma_transformer.py:89-92,112)
+template <bool SAVE>
+__device__ __forceinline__ void self_attn_fwd_ct(const Mat* m, const LNp& ln, CT* xr, bool causal, bf16_t* sv_xin,
+                                                 bf16_t* sv_a, float* sv_lse, const Ctx& c) {
+  const int lane = c.lane;
+  {
+    AFr Wq, Wk, Wv;
+    loadA(Wq, m[0].fa, lane);
+    loadA(Wk, m[1].fa, lane);
+    loadA(Wv, m[2].fa, lane);
+    const CT bq = ld_vec(m[0].b, lane), bk = ld_vec(m[1].b, lane), bv = ld_vec(m[2].b, lane);
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) {
+        const bool ok = tok_ok(rt, c);
+        const CTr x = ct_pack(xr[k]);
+        if (SAVE) st_g(sv_xin, c.tok0, rt, c.NR, x, lane);
+        CT q = bq, kk = bk, v = bv;
+        mm(q, Wq, x);
+        mm(kk, Wk, x);
+        mm(v, Wv, x);
+        st_lds(c.QB, rt, ct_pack(q), ok, lane);
+        st_lds(c.KB, rt, ct_pack(kk), ok, lane);
+        st_lds(c.VB, rt, ct_pack(v), ok, lane);
+      }
+    }
+  }
+  __syncthreads();
+  attn_fwd(c.QB, c.KB, c.VB, c.QB, causal, SAVE ? sv_lse : nullptr, c);
+  __syncthreads();
+  AFr Wp;
+  loadA(Wp, m[3].fa, lane);
+  const CT bp = ld_vec(m[3].b, lane), gam = ld_vec(ln.g, lane), bet = ld_vec(ln.b, lane);
+#pragma unroll
+  for (int k = 0; k < MAXRT; ++k) {
+    const int rt = c.wave + 4 * k;
+    if (rt < c.NT) {
+      const CTr a = ld_lds(c.QB, rt, lane);
+      if (SAVE) st_g(sv_a, c.tok0, rt, c.NR, a, lane);
+      CT t = ct_add(bp, xr[k]), xh;
+      mm(t, Wp, a);
+      ln_fwd_ct(t, xh, xr[k], gam, bet);
+    }
+  }
+}
+
+// MLP: x <- LN(x + W2 GELU(W1 x + b1) + b2)   (ma_transformer.py:84-86,91-92)
+template <bool SAVE>
+__device__ __forceinline__ void mlp_fwd_ct(const Mat& m1, const Mat& m2, const LNp& ln, CT* xr, bf16_t* sv_x, bf16_t* sv_h,
+                                           const Ctx& c) {
+  const int lane = c.lane;
+  AFr W1, W2;
+  loadA(W1, m1.fa, lane);
+  loadA(W2, m2.fa, lane);
+  const CT b1 = ld_vec(m1.b, lane), b2 = ld_vec(m2.b, lane), gam = ld_vec(ln.g, lane), bet = ld_vec(ln.b, lane);
+#pragma unroll
+  for (int k = 0; k < MAXRT; ++k) {
+    const int rt = c.wave + 4 * k;
+    if (rt < c.NT) {
+      const CTr x = ct_pack(xr[k]);
+      if (SAVE) st_g(sv_x, c.tok0, rt, c.NR, x, lane);
+      CT h = b1;
+      mm(h, W1, x);
+      if (SAVE) st_g(sv_h, c.tok0, rt, c.NR, ct_pack(h), lane);
+      gelu_ct(h);
+      CT mo = ct_add(b2, xr[k]), xh;
+      mm(mo, W2, ct_pack(h));
+      ln_fwd_ct(mo, xh, xr[k], gam, bet);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------ sublayers (backward)
+__device__ __forceinline__ void mlp_bwd_ct(const Mat& m1, const Mat& m2, const LNp& ln, CT* dx, const bf16_t* sv_x,
+                                           const bf16_t* sv_h, const Ctx& c) {
+  const int lane = c.lane;
+  CT dlg, dlb;
+  ct_zero(dlg);
+  ct_zero(dlb);
+  {
+    AFr W2f, W2b, W1b;
+    loadA(W2f, m2.fa, lane);
+    loadA(W2b, m2.ba, lane);
+    loadA(W1b, m1.ba, lane);
+    const CT b2 = ld_vec(m2.b, lane), gam = ld_vec(ln.g, lane), bet = ld_vec(ln.b, lane);
+    CTr xs[MAXRT], hs[MAXRT];
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {   // every saved-activation load of the wave issued up front
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) {
+        xs[k] = ld_g(sv_x, c.tok0, rt, c.NR, lane);
+        hs[k] = ld_g(sv_h, c.tok0, rt, c.NR, lane);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) {
+        const bool ok = tok_ok(rt, c);
+        const CT h = ct_unpack(hs[k]);
+        CT gl = h;
+        gelu_ct(gl);
+        const CTr glr = ct_pack(gl);
+        CT mo = ct_add(b2, ct_unpack(xs[k])), xh, yy, ds;
+        mm(mo, W2f, glr);
+        const float rs = ln_fwd_ct(mo, xh, yy, gam, bet);
+        ln_bwd_ct(dx[k], xh, rs, gam, ok, ds, dlg, dlb);
+        const CTr dsr = ct_pack(ds);
+        st_lds(c.DA, rt, dsr, ok, lane);     // dY of W2
+        st_lds(c.XB, rt, glr, ok, lane);     // X of W2
+        CT dg;
+        ct_zero(dg);
+        mm(dg, W2b, dsr);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dg.v[i][r] = ok ? dg.v[i][r] * gelu_erf_grad(h.v[i][r]) : 0.f;
+        const CTr dgr = ct_pack(dg);
+        st_lds(c.KB, rt, dgr, ok, lane);     // dY of W1
+        st_lds(c.QB, rt, xs[k], ok, lane);   // X of W1
+        CT t = ds;
+        mm(t, W1b, dgr);
+        dx[k] = t;
+      }
+    }
+  }
+  flush_vec(dlg, c.g(ln.dg), lane);
+  flush_vec(dlb, c.g(ln.db), lane);
+  __syncthreads();
+  wgrad64(c.DA, c.XB, m2, c);
+  wgrad64(c.KB, c.QB, m1, c);
+  __syncthreads();
+}
+
+// recompute + store q / k / v of the saved input, attention backward, weight gradients; returns through dx (+=) the
+// input gradient of the q / k / v projections.  Self: q-input = kv-input = x (sv_xin).  The attention output
+// gradient dO must already be in DA.
+__device__ __forceinline__ void self_attn_bwd_ct(const Mat* m, const LNp& ln, CT* dx, const bf16_t* sv_xin,
+                                                 const bf16_t* sv_a, const float* sv_lse, bool causal, const Ctx& c) {
+  const int lane = c.lane;
+  CTr xin[MAXRT];
+  {
+    CT dlg, dlb;
+    ct_zero(dlg);
+    ct_zero(dlb);
+    AFr Wpf, Wpb;
+    loadA(Wpf, m[3].fa, lane);
+    loadA(Wpb, m[3].ba, lane);
+    const CT bp = ld_vec(m[3].b, lane), gam = ld_vec(ln.g, lane), bet = ld_vec(ln.b, lane);
+    CTr as[MAXRT];
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) {
+        as[k] = ld_g(sv_a, c.tok0, rt, c.NR, lane);
+        xin[k] = ld_g(sv_xin, c.tok0, rt, c.NR, lane);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) {
+        const bool ok = tok_ok(rt, c);
+        CT s = ct_add(bp, ct_unpack(xin[k])), xh, yy, ds;
+        mm(s, Wpf, as[k]);
+        const float rs = ln_fwd_ct(s, xh, yy, gam, bet);
+        ln_bwd_ct(dx[k], xh, rs, gam, ok, ds, dlg, dlb);
+        const CTr dsr = ct_pack(ds);
+        st_lds(c.DQ, rt, dsr, ok, lane);     // dY of Wp
+        st_lds(c.XB, rt, as[k], ok, lane);   // X of Wp
+        CT da;
+        ct_zero(da);
+        mm(da, Wpb, dsr);
+        st_lds(c.DA, rt, ct_pack(da), ok, lane);   // dO
+        dx[k] = ds;                                // residual path
+      }
+    }
+    flush_vec(dlg, c.g(ln.dg), lane);
+    flush_vec(dlb, c.g(ln.db), lane);
+  }
+  __syncthreads();
+  wgrad64(c.DQ, c.XB, m[3], c);
+  __syncthreads();
+  {
+    AFr Wq, Wk, Wv;
+    loadA(Wq, m[0].fa, lane);
+    loadA(Wk, m[1].fa, lane);
+    loadA(Wv, m[2].fa, lane);
+    const CT bq = ld_vec(m[0].b, lane), bk = ld_vec(m[1].b, lane), bv = ld_vec(m[2].b, lane);
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) {
+        const bool ok = tok_ok(rt, c);
+        CT q = bq, kk = bk, v = bv;
+        mm(q, Wq, xin[k]);
+        mm(kk, Wk, xin[k]);
+        mm(v, Wv, xin[k]);
+        st_lds(c.QB, rt, ct_pack(q), ok, lane);
+        st_lds(c.KB, rt, ct_pack(kk), ok, lane);
+        st_lds(c.VB, rt, ct_pack(v), ok, lane);
+        st_lds(c.XB, rt, xin[k], ok, lane);   // X of dWq / dWk / dWv
+      }
+    }
+  }
+  load_lse(sv_lse, c);
+  __syncthreads();
+  attn_bwd_q(c.QB, c.KB, c.VB, c.DA, c.DQ, causal, c);
+  __syncthreads();
+  attn_bwd_kv(c.QB, c.KB, c.VB, c.DA, causal, c);
+  __syncthreads();
+  wgrad64(c.DQ, c.XB, m[0], c);
+  wgrad64(c.KB, c.XB, m[1], c);
+  wgrad64(c.VB, c.XB, m[2], c);
+  {
+    AFr Wq, Wk, Wv;
+    loadA(Wq, m[0].ba, lane);
+    loadA(Wk, m[1].ba, lane);
+    loadA(Wv, m[2].ba, lane);
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) {
+        mm(dx[k], Wq, ld_lds(c.DQ, rt, lane));
+        mm(dx[k], Wk, ld_lds(c.KB, rt, lane));
+        mm(dx[k], Wv, ld_lds(c.VB, rt, lane));
+      }
+    }
+  }
+  __syncthreads();
+}
+
+}  // namespace

@@ -197,7 +197,7 @@ struct AdamArgs {
   int n;
   float* p; const float* g; float* m; float* v;
   float* sumsq;       // [0] sum of squared grads (adam_norm), [1] grad norm (logging), [2] skipped steps
-  float lr, beta1, beta2, eps, wd, bc1, bc2, max_norm;
+  float lr, beta1, beta2, eps, wd, t, max_norm;   // t = optimizer steps attempted so far, this one included
   int clip;
 };
 
@@ -226,7 +226,10 @@ __global__ __launch_bounds__(256) void adam_step_kernel(AdamArgs a) {
   }
   if (!isfinite(norm)) return;   // non-finite guard: skip the whole step (params and moments untouched)
   const float scale = a.clip ? fminf(1.f, a.max_norm / (norm + 1e-6f)) : 1.f;
-  const float ib1 = 1.f / a.bc1, ib2 = 1.f / a.bc2;
+  // bias corrections from the APPLIED step count (attempted minus skipped non-finite steps, both on device), as
+  // torch.optim.Adam, which never sees a skipped step; nobody writes sumsq[2] on a non-skipped step
+  const float t = a.t - a.sumsq[2];
+  const float ib1 = 1.f / (1.f - powf(a.beta1, t)), ib2 = 1.f / (1.f - powf(a.beta2, t));
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
     float g = a.g[i] * scale;
     float p = a.p[i];

@@ -59,10 +59,13 @@ MDL_API int mdl_philox_fill(int64_t* out, int n, uint32_t c1, uint32_t c2, uint3
   return 0;
 }
 
-// Repack fp32 Linear weights (64 x 64, [out][in]) into the MFMA B-fragment order used by the fused kernels, for W
+// Repack fp32 Linear weights (64 x 64, [out][in]) into the MFMA fragment orders used by the fused kernels, for W
 // (forward) and W^T (backward) — all matrices of the model in ONE launch after each optimizer step.
-// fragment element (ct, ks, lane, j) = M[16*ct + (lane & 15)][32*ks + 8*(lane >> 4) + j]
-struct PackEnt { const float* src; unsigned short* fw; unsigned short* bw; };
+//  * B fragments (decode kernel, round-1 row-layout tiles):
+//      element (ct, ks, lane, j) = M[16*ct + (lane & 15)][32*ks + 8*(lane >> 4) + j]
+//  * A fragments with the permuted k order of the token-on-lane training tiles (mat_train_ct.h):
+//      element (mt, s, lane, j) = M[16*mt + (lane & 15)][32*s + 16*(j >> 2) + 4*(lane >> 4) + (j & 3)]
+struct PackEnt { const float* src; unsigned short* fw; unsigned short* bw; unsigned short* fa; unsigned short* ba; };
 
 __global__ __launch_bounds__(256) void pack_weights_kernel(const PackEnt* tab) {
   const PackEnt e = tab[blockIdx.x];
@@ -71,6 +74,9 @@ __global__ __launch_bounds__(256) void pack_weights_kernel(const PackEnt* tab) {
     const int n = 16 * ct + (lane & 15), k = 32 * ks + 8 * (lane >> 4) + j;
     if (e.fw) e.fw[idx] = mdl::f2bf(e.src[n * 64 + k]);
     if (e.bw) e.bw[idx] = mdl::f2bf(e.src[k * 64 + n]);
+    const int kp = 32 * ks + 16 * (j >> 2) + 4 * (lane >> 4) + (j & 3);
+    if (e.fa) e.fa[idx] = mdl::f2bf(e.src[n * 64 + kp]);
+    if (e.ba) e.ba[idx] = mdl::f2bf(e.src[kp * 64 + n]);
   }
 }
 

@@ -22,7 +22,7 @@ VP = ctypes.c_void_p
 
 
 class Mat(ctypes.Structure):
-    _fields_ = [("fw", VP), ("bw", VP), ("b", VP), ("dW", VP), ("db", VP)]
+    _fields_ = [("fw", VP), ("bw", VP), ("b", VP), ("dW", VP), ("db", VP), ("fa", VP), ("ba", VP)]
 
 
 class LNp(ctypes.Structure):
@@ -60,15 +60,26 @@ class DecP(ctypes.Structure):
 # (three 16-row tiles per wave, one workgroup per CU, L <= 192) ships: an occupancy-2 build (one tile per wave, two
 # workgroups per CU) measured 1.6x / 2.9x slower backward kernels (register spills, 5x more weight-gradient atomics;
 # profiles/r1_occupancy_ab.md).
-VARIANTS = ("",)
-for _v in VARIANTS:
+#
+# Round 2 ("ct", csrc/mat_train_ct.h): token-on-lane tiles, weight A fragments in permuted k order, register-
+# chained linears; the default.  MAT_DCML_TRAIN_KERNELS=v1 selects the round-1 row-layout kernels (A/B runs).
+TRAIN_KERNELS = os.environ.get("MAT_DCML_TRAIN_KERNELS", "ct").lower()
+VARIANTS = ("_ct",) if TRAIN_KERNELS == "ct" else ("",)
+for _v in ("",):
     sig("mdl_mat_train_geometry" + _v, ctypes.c_int)
     sig("mdl_mat_enc_fwd" + _v, ctypes.POINTER(EncP), ctypes.c_int, ctypes.c_int, VP)
     sig("mdl_mat_enc_bwd" + _v, ctypes.POINTER(EncP), ctypes.c_int, VP)
     sig("mdl_mat_dec_fwd" + _v, ctypes.POINTER(DecP), ctypes.c_int, ctypes.c_int, VP)
     sig("mdl_mat_dec_bwd" + _v, ctypes.POINTER(DecP), ctypes.c_int, VP)
+sig("mdl_mat_train_geometry_ct", ctypes.c_int)
+sig("mdl_mat_enc_fwd_ct", ctypes.POINTER(EncP), VP, ctypes.c_int, ctypes.c_int, VP)
+sig("mdl_mat_enc_bwd_ct", ctypes.POINTER(EncP), VP, VP, ctypes.c_int, VP)
+sig("mdl_mat_dec_fwd_ct", ctypes.POINTER(DecP), ctypes.c_int, ctypes.c_int, VP)
+sig("mdl_mat_dec_bwd_ct", ctypes.POINTER(DecP), ctypes.c_int, VP)
 sig("mdl_grad_reduce", VP, VP, ctypes.c_int, ctypes.c_longlong, ctypes.c_int, VP)
 sig("mdl_pack_weights", VP, ctypes.c_int, VP)
+
+MAX_ACTION_DIM = 64 if TRAIN_KERNELS == "ct" else 8
 
 
 def geometry(L):
@@ -78,6 +89,18 @@ def geometry(L):
         if v:
             return v & 0xFFFF, v >> 16, sfx
     return 0, 0, ""
+
+
+def _enc_fwd(sfx, p, pre_in, nb, save):
+    if sfx == "_ct":
+        return lib().mdl_mat_enc_fwd_ct(ctypes.byref(p), pre_in, nb, int(save), kernels._stream())
+    return getattr(lib(), "mdl_mat_enc_fwd" + sfx)(ctypes.byref(p), nb, int(save), kernels._stream())
+
+
+def _enc_bwd(sfx, p, pre_in, dpre_out, nb):
+    if sfx == "_ct":
+        return lib().mdl_mat_enc_bwd_ct(ctypes.byref(p), pre_in, dpre_out, nb, kernels._stream())
+    return getattr(lib(), "mdl_mat_enc_bwd" + sfx)(ctypes.byref(p), nb, kernels._stream())
 
 
 def _ptr(t):
@@ -118,8 +141,11 @@ class ModelPack:
         dev = lins[0].weight.device
         self.fw = torch.empty(self.n, 4096, dtype=torch.bfloat16, device=dev)
         self.bw = torch.empty(self.n, 4096, dtype=torch.bfloat16, device=dev)
+        self.fa = torch.empty(self.n, 4096, dtype=torch.bfloat16, device=dev)
+        self.ba = torch.empty(self.n, 4096, dtype=torch.bfloat16, device=dev)
         self.index = {id(l): i for i, l in enumerate(lins)}
-        tab = [[l.weight.data_ptr(), self.fw[i].data_ptr(), self.bw[i].data_ptr()] for i, l in enumerate(lins)]
+        tab = [[l.weight.data_ptr(), self.fw[i].data_ptr(), self.bw[i].data_ptr(), self.fa[i].data_ptr(),
+                self.ba[i].data_ptr()] for i, l in enumerate(lins)]
         self.table = torch.tensor(tab, dtype=torch.int64, device=dev)
         self.version = None
 
@@ -132,7 +158,7 @@ class ModelPack:
     def mat(self, lin):
         i = self.index[id(lin)]
         return Mat(self.fw[i].data_ptr(), self.bw[i].data_ptr(), lin.bias.data_ptr(), _gptr(lin.weight),
-                   _gptr(lin.bias))
+                   _gptr(lin.bias), self.fa[i].data_ptr(), self.ba[i].data_ptr())
 
     @property
     def decoder_fw(self):
@@ -188,8 +214,8 @@ def decoder_unsupported_reasons(model):
         r.append("dec_actor")
     if model.action_type not in ("Semi_Discrete", "Discrete"):
         r.append(f"action_type {model.action_type}")
-    if model.action_dim > 8:
-        r.append(f"action_dim {model.action_dim} > 8")
+    if model.action_dim > MAX_ACTION_DIM:
+        r.append(f"action_dim {model.action_dim} > {MAX_ACTION_DIM}")
     if model.action_type == "Semi_Discrete" and model.semi_index != -1:
         r.append(f"semi_index {model.semi_index} != -1")
     return r
@@ -261,7 +287,7 @@ class EncoderFused:
                 saves += [t, lse]
                 p.sv[bi] = Sv(t[0].data_ptr(), t[1].data_ptr(), lse.data_ptr(), t[2].data_ptr(), None, None, None,
                               t[3].data_ptr())
-        check(getattr(lib(), "mdl_mat_enc_fwd" + sfx)(ctypes.byref(p), m.n_block, int(save), kernels._stream()), "mat_enc_fwd")
+        check(_enc_fwd(sfx, p, None, m.n_block, save), "mat_enc_fwd")
         self.ctx = (obs, rep, v, saves, [Sv.from_buffer_copy(p.sv[i]) for i in range(m.n_block)])
         return v, rep
 
@@ -281,7 +307,7 @@ class EncoderFused:
         p.g_delta, p.g_stride, p.g_copies = m._mdl_gws if getattr(m, "_mdl_gws_active", False) else (0, 0, 0)
         if p.g_copies:
             check_grad_ptrs(p, m._mdl_gws_buf[1])
-        check(getattr(lib(), "mdl_mat_enc_bwd" + sfx)(ctypes.byref(p), m.n_block, kernels._stream()), "mat_enc_bwd")
+        check(_enc_bwd(sfx, p, None, None, m.n_block), "mat_enc_bwd")
         b = m.encoder.head[3].bias
         if b.grad is not None:
             b.grad.add_(dv.reshape(-1, dv.shape[-1]).sum(0))
@@ -471,7 +497,7 @@ def flat_range(params, flat):
         return None
     lo = end = offs[0][0]
     for o, n in offs:
-        if o != end:
+        if not end <= o < end + 16:   # contiguous up to the per-parameter padding (ops/ppo_fused.PAD)
             return None
         end = o + n
     return lo, end

@@ -33,7 +33,7 @@ class PPOArgs(ctypes.Structure):
 
 class AdamArgs(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int)] + [(k, vp) for k in ("p", "g", "m", "v", "sumsq")] + \
-               [(k, ctypes.c_float) for k in ("lr", "beta1", "beta2", "eps", "wd", "bc1", "bc2", "max_norm")] + \
+               [(k, ctypes.c_float) for k in ("lr", "beta1", "beta2", "eps", "wd", "t", "max_norm")] + \
                [("clip", ctypes.c_int)]
 
 
@@ -43,17 +43,26 @@ sig("mdl_ppo_finish", ctypes.POINTER(PPOArgs), vp)
 sig("mdl_adam", ctypes.POINTER(AdamArgs), vp)
 
 
+PAD = 16   # every parameter starts on a 64-byte boundary of the flat buffer (aligned float4 loads in the kernels)
+
+
+def padded(n: int) -> int:
+    return (n + PAD - 1) // PAD * PAD
+
+
 def flatten_params(module: torch.nn.Module) -> torch.Tensor:
+    """Move every trainable parameter into ONE flat fp32 buffer (views), each padded to 16 floats.  The padding
+    stays zero: its gradient is never written, so Adam leaves it at zero."""
     params = [p for p in module.parameters() if p.requires_grad]
-    n = sum(p.numel() for p in params)
+    n = sum(padded(p.numel()) for p in params)
     dev = params[0].device
-    flat = torch.empty(n, dtype=torch.float32, device=dev)
+    flat = torch.zeros(n, dtype=torch.float32, device=dev)
     off = 0
     for p in params:
         k = p.numel()
         flat[off:off + k].copy_(p.data.reshape(-1).float())
         p.data = flat[off:off + k].view_as(p)
-        off += k
+        off += padded(k)
     module._mdl_flat_params = flat
     return flat
 
@@ -67,19 +76,35 @@ def flat_params_of(module):
     for p in params:   # views still in place (load_state_dict copies into them)
         if p.data_ptr() != flat[off:].data_ptr():
             return None
-        off += p.numel()
+        off += padded(p.numel())
     return flat
 
 
+def param_offsets(module):
+    """[(param, offset)] of the flat layout (same for the flat parameters and the flat gradients)."""
+    out, off = [], 0
+    for p in module.parameters():
+        if p.requires_grad:
+            out.append((p, off))
+            off += padded(p.numel())
+    return out
+
+
 class FlatAdam:
+    """Adam + clip over the flat buffers.  The step counter used for the bias corrections is the number of APPLIED
+    steps (attempted ``t`` minus the device-side count of skipped non-finite steps), like ``torch.optim.Adam``.
+    ``state_dict`` is torch.optim.Adam's per-parameter format, so a fused-path checkpoint resumes on the eager
+    path (and vice versa)."""
+
     def __init__(self, flat_params: torch.Tensor, flat_grads: torch.Tensor, lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
-                 weight_decay=0.0, max_grad_norm=None):
+                 weight_decay=0.0, max_grad_norm=None, layout=None):
         self.p, self.g = flat_params, flat_grads
         self.m = torch.zeros_like(flat_params)
         self.v = torch.zeros_like(flat_params)
         self.scratch = torch.zeros(3, dtype=torch.float32, device=flat_params.device)   # sumsq, norm, skipped
         self.param_groups = [{"lr": lr, "betas": betas, "eps": eps, "weight_decay": weight_decay}]
         self.max_grad_norm = max_grad_norm
+        self.layout = layout   # [(param, flat offset)] (ops/ppo_fused.param_offsets)
         self.t = 0
 
     @property
@@ -98,27 +123,48 @@ class FlatAdam:
         self.t += 1
         b1, b2 = g["betas"]
         a = AdamArgs(n=self.p.numel(), p=P(self.p), g=P(self.g), m=P(self.m), v=P(self.v), sumsq=P(self.scratch),
-                     lr=g["lr"], beta1=b1, beta2=b2, eps=g["eps"], wd=g["weight_decay"], bc1=1 - b1 ** self.t,
-                     bc2=1 - b2 ** self.t, max_norm=float(self.max_grad_norm or 0.0),
-                     clip=int(self.max_grad_norm is not None))
+                     lr=g["lr"], beta1=b1, beta2=b2, eps=g["eps"], wd=g["weight_decay"], t=float(self.t),
+                     max_norm=float(self.max_grad_norm or 0.0), clip=int(self.max_grad_norm is not None))
         check(lib().mdl_adam(ctypes.byref(a), _stream()), "adam")
 
+    def applied_steps(self) -> int:
+        return self.t - int(round(float(self.scratch[2])))
+
     def state_dict(self):
-        return {"m": self.m, "v": self.v, "t": self.t, "param_groups": self.param_groups}
+        grp = {k: v for k, v in self.param_groups[0].items()}
+        grp.update(amsgrad=False, maximize=False, foreach=None, capturable=False, differentiable=False, fused=None)
+        if self.layout is None:
+            raise RuntimeError("FlatAdam.state_dict needs the parameter layout")
+        step = float(self.applied_steps())
+        state = {}
+        for i, (p, off) in enumerate(self.layout):
+            n = p.numel()
+            state[i] = {"step": torch.tensor(step), "exp_avg": self.m[off:off + n].view_as(p).detach().clone(),
+                        "exp_avg_sq": self.v[off:off + n].view_as(p).detach().clone()}
+        grp["params"] = list(range(len(self.layout)))
+        return {"state": state, "param_groups": [grp]}
 
     def load_state_dict(self, sd):
-        if "m" not in sd:   # a torch.optim.Adam state (per-parameter exp_avg / exp_avg_sq)
-            st = sd.get("state", {})
-            if st:
-                self.m.copy_(torch.cat([st[i]["exp_avg"].reshape(-1) for i in sorted(st)]))
-                self.v.copy_(torch.cat([st[i]["exp_avg_sq"].reshape(-1) for i in sorted(st)]))
-                self.t = int(float(st[min(st)]["step"]))
-            self.param_groups[0]["lr"] = sd["param_groups"][0]["lr"]
+        if "m" in sd:   # round-1 flat format (unpadded layout): only usable if the sizes still agree
+            if sd["m"].numel() == self.m.numel():
+                self.m.copy_(sd["m"])
+                self.v.copy_(sd["v"])
+            self.t = int(sd["t"])
+            self.param_groups[0].update({k: v for k, v in sd["param_groups"][0].items() if k != "params"})
             return
-        self.m.copy_(sd["m"])
-        self.v.copy_(sd["v"])
-        self.t = int(sd["t"])
-        self.param_groups[0].update({k: v for k, v in sd["param_groups"][0].items() if k != "params"})
+        st = sd.get("state", {})
+        if st:
+            if self.layout is None or len(self.layout) != len(st):
+                raise RuntimeError("optimizer state does not match the model's parameters")
+            self.m.zero_()
+            self.v.zero_()
+            for i, (p, off) in enumerate(self.layout):
+                n = p.numel()
+                self.m[off:off + n].copy_(st[i]["exp_avg"].reshape(-1).to(self.m.device))
+                self.v[off:off + n].copy_(st[i]["exp_avg_sq"].reshape(-1).to(self.v.device))
+            self.t = int(float(st[min(st)]["step"]))
+            self.scratch[2] = 0.0
+        self.param_groups[0]["lr"] = sd["param_groups"][0]["lr"]
 
 
 class PPOLossFused:

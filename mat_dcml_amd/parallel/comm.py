@@ -119,9 +119,12 @@ class Comm:
 class FlatGrads:
     """All ``.grad`` tensors as views of one flat buffer (zero_grad must use ``set_to_none=False``)."""
 
+    PAD = 16   # same per-parameter padding as the flat parameter buffer (ops/ppo_fused.flatten_params)
+
     def __init__(self, params):
         self.params = [p for p in params if p.requires_grad]
-        n = sum(p.numel() for p in self.params)
+        pad = lambda k: (k + self.PAD - 1) // self.PAD * self.PAD  # noqa: E731
+        n = sum(pad(p.numel()) for p in self.params)
         dev = self.params[0].device
         self.buf = torch.zeros(n, dtype=torch.float32, device=dev)
         self.views = []
@@ -132,7 +135,7 @@ class FlatGrads:
                 v.copy_(p.grad)
             p.grad = v
             self.views.append(v)
-            off += p.numel()
+            off += pad(p.numel())
         self._ids = {id(p) for p in self.params}
 
     def owns(self, params):
