@@ -65,6 +65,8 @@ class MATTrainer:
         self.params = [p for p in policy.transformer.parameters() if p.requires_grad]
         self.poison = False          # fault injection: non-finite gradients this iteration
         self.skipped = torch.zeros((), device=self.device)
+        self._vn_pre = None          # (Σ, Σ², n) of the current minibatch's returns when precomputed per epoch
+        self.collectives = 0         # statistics / gradient collectives issued (DP accounting, tests)
         self.fused = self._setup_fused(args)
 
     def _setup_fused(self, args):
@@ -113,7 +115,7 @@ class MATTrainer:
     def cal_value_loss(self, values, value_preds_batch, return_batch, active_masks_batch):
         clipped = value_preds_batch + (values - value_preds_batch).clamp(-self.clip_param, self.clip_param)
         if self.value_normalizer is not None:
-            self.value_normalizer.update(return_batch)
+            self.value_normalizer.update(return_batch, presummed=self._vn_pre)
             target = self.value_normalizer.normalize(return_batch)
         else:
             target = return_batch
@@ -154,6 +156,7 @@ class MATTrainer:
                 p.grad.fill_(float("nan"))
         if self.comm is not None and self.comm.world_size > 1:
             self.comm.all_reduce_grads_(self.params)
+            self.collectives += 1
         if flat is not None:
             grad_norm = flat.buf.norm()
             if self._use_max_grad_norm:   # clip_grad_norm_ semantics: scale = max / (norm + 1e-6), capped at 1
@@ -169,14 +172,7 @@ class MATTrainer:
         mat_fused.bump_version(pol.transformer)
         return value_loss.detach(), grad_norm.detach(), policy_loss.detach(), entropy.detach(), imp.detach().mean()
 
-    def _dec_grad_range(self, m):
-        """Flat-gradient element range of the decoder parameters (None if not contiguous)."""
-        if not hasattr(self, "_dec_range"):
-            from ..ops import mat_train
-            self._dec_range = mat_train.flat_range(list(m.decoder.parameters()), self.comm._flat.buf)
-        return self._dec_range
-
-    def ppo_update_fused(self, mb):
+    def ppo_update_fused(self, mb, pre_stats=None):
         from ..ops import mat_train
         pol = self.policy
         m = pol.transformer
@@ -185,48 +181,63 @@ class MATTrainer:
         logp, ent = dec.forward(rep, mb["actions"], mb["ava"], save=True)
         buf = self.comm._flat.buf
         buf.zero_()
-        dv, dlp, dent = self.loss_fused.run(v, logp, ent, mb, self.comm)
+        dv, dlp, dent = self.loss_fused.run(v, logp, ent, mb, self.comm, pre_stats=pre_stats)
         m._mdl_gws_active = hasattr(m, "_mdl_gws")   # weight-gradient atomics into the 8-copy workspace
         drep = dec.backward(dlp, dent)
-        # data parallel: the decoder's gradient all-reduce (RCCL, on the process group's stream) runs under the
-        # encoder backward; the rest of the buffer is reduced after it
-        rng = self._dec_grad_range(m) if self.comm.world_size > 1 and not self.poison else None
-        work = None
-        if rng is not None:
-            mat_train.reduce_grad_workspace(m, *rng)
-            work = self.comm.all_reduce_sum_async(buf[rng[0]:rng[1]])
         enc.backward(drep, dv)
         m._mdl_gws_active = False
-        if rng is None:
-            mat_train.reduce_grad_workspace(m)
-        else:
-            mat_train.reduce_grad_workspace(m, 0, rng[0])
-            mat_train.reduce_grad_workspace(m, rng[1])
+        mat_train.reduce_grad_workspace(m)
         dec.ctx = None
         enc.ctx = None
         if self.poison:
             buf[:1].fill_(float("nan"))   # the fused Adam kernel skips non-finite steps
         if self.comm.world_size > 1:
-            if work is None:
-                self.comm.all_reduce_grads_(self.params)
-            else:
-                for a, b in ((0, rng[0]), (rng[1], buf.numel())):
-                    if b > a:
-                        self.comm.all_reduce_sum_(buf[a:b])
-                work.wait()
-                buf.mul_(1.0 / self.comm.world_size)
+            # ONE all-reduce of the whole 0.6 MB flat gradient per minibatch: at this size RCCL over xGMI is
+            # latency-bound, so splitting it to overlap the decoder slice with the encoder backward only added a
+            # collective (round-1 variant)
+            self.comm.all_reduce_sum_(buf)
+            buf.mul_(1.0 / self.comm.world_size)
+            self.collectives += 1
         pol.optimizer.step()
         mat_fused.bump_version(m)
         return pol.optimizer.grad_norm
 
     # ------------------------------------------------------------------------------------------------
-    def _advantages(self, buffer):
-        adv = buffer.advantages
-        active = buffer.active_masks[:-1]
-        sums = rl_ops.masked_sums(adv, active)
-        if self.comm is not None and self.comm.world_size > 1:
-            self.comm.all_reduce_sum_(sums)
-        return rl_ops.normalize_from_sums(adv, sums)
+    def _epoch_stats(self, buffer, idx_list, native):
+        """Advantage moments (masked Σ, Σ², n) and, under data parallelism with a value normaliser, every
+        minibatch's return moments of this epoch — ONE all-reduce per epoch (the reference's per-minibatch
+        ValueNorm update order is kept: minibatch m updates with its own, now global, moments).
+        Returns (adv_sums fp64[3], per-minibatch stats fp32 [n_mb, 2·n_obj + 2] or None)."""
+        act = buffer.active_masks[:-1]
+        adv_sums = kernels.masked_sums(buffer.advantages, act) if native else rl_ops.masked_sums(buffer.advantages, act)
+        dp = self.comm is not None and self.comm.world_size > 1
+        if not dp:
+            return adv_sums, None
+        mbs = None
+        if self.value_normalizer is not None:
+            ret_f, am_f = buffer.flat("returns"), buffer.flat("active_masks")
+            if native:
+                mbs = kernels.mb_stats(ret_f, am_f, torch.cat(idx_list), len(idx_list))
+            else:
+                rows = []
+                for idx in idx_list:
+                    r = ret_f[idx].double().reshape(-1, ret_f.shape[-1])
+                    rows.append(torch.cat([r.sum(0), (r * r).sum(0),
+                                           torch.tensor([float(r.shape[0])], dtype=torch.float64, device=r.device),
+                                           am_f[idx].double().sum().reshape(1)]))
+                mbs = torch.stack(rows)
+            K = mbs.shape[1]
+            packed = torch.cat([adv_sums, mbs[:, :K - 1].reshape(-1)])
+        else:
+            packed = adv_sums
+        self.comm.all_reduce_sum_(packed)
+        self.collectives += 1
+        adv_sums = packed[:3]
+        if mbs is None:
+            return adv_sums, None
+        # global (Σ ret, Σ ret², n); the active count stays local (losses are local means, gradients are averaged)
+        pre = torch.cat([packed[3:].view(len(idx_list), K - 1), mbs[:, K - 1:]], 1).float().contiguous()
+        return adv_sums, pre
 
     def train(self, buffer):
         pol = self.policy
@@ -241,6 +252,7 @@ class MATTrainer:
         lp_f = buffer.flat("action_log_probs")
         vp_f = buffer.flat("value_preds")
         am_f = buffer.flat("active_masks")
+        n_obj = buffer.returns.shape[-1]
         # HIP path: advantage statistics by a fixed-order fp64 reduction kernel, and each minibatch gathered by ONE
         # launch that also standardises the advantages of the rows it reads (no full normalised copy)
         native = self.fused and kernels.use_hip(obs_f)
@@ -248,16 +260,15 @@ class MATTrainer:
             if epoch == 0 or self.recompute_gae_every_epoch:
                 next_values = pol.get_values(None, buffer.obs[-1], buffer.available_actions[-1])
                 buffer.compute_returns(next_values, self.value_normalizer)
-                if native:
-                    sums = kernels.masked_sums(buffer.advantages, buffer.active_masks[:-1])
-                    if self.comm is not None and self.comm.world_size > 1:
-                        self.comm.all_reduce_sum_(sums)
-                    adv_f = buffer.flat("advantages")
-                else:
-                    adv = self._advantages(buffer)
-                    adv_f = adv.reshape(T * E, *adv.shape[2:])
-                ret_f = buffer.flat("returns")
-            for idx in buffer.minibatch_indices(self.num_mini_batch, self.generator):
+            ret_f = buffer.flat("returns")
+            idx_list = buffer.minibatch_indices(self.num_mini_batch, self.generator)
+            sums, pre = self._epoch_stats(buffer, idx_list, native)
+            if native:
+                adv_f = buffer.flat("advantages")
+            else:
+                adv = rl_ops.normalize_from_sums(buffer.advantages, sums)
+                adv_f = adv.reshape(T * E, *adv.shape[2:])
+            for m, idx in enumerate(idx_list):
                 src = {"obs": obs_f, "actions": act_f, "ava": ava_f, "old_logp": lp_f, "value_preds": vp_f,
                        "returns": ret_f, "active": am_f, "adv": adv_f}
                 if native:
@@ -265,9 +276,11 @@ class MATTrainer:
                 else:
                     mb = {k: v[idx] for k, v in src.items()}
                 if self.fused:
-                    acc[3:5] += self.ppo_update_fused(mb)
+                    acc[3:5] += self.ppo_update_fused(mb, None if pre is None else pre[m])
                     continue
+                self._vn_pre = None if pre is None else (pre[m, :n_obj], pre[m, n_obj:2 * n_obj], pre[m, 2 * n_obj])
                 vl, gn, pl, ent, ratio = self.ppo_update(mb)
+                self._vn_pre = None
                 acc += torch.stack([vl, pl, ent, gn, gn, ratio]).float()
         if self.fused:   # loss scalars accumulated on device by the loss kernel: [policy, value, entropy, ratio]
             o = self.loss_fused.out

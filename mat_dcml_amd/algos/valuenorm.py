@@ -36,7 +36,19 @@ class ValueNorm(nn.Module):
         return mean, var
 
     @torch.no_grad()
-    def update(self, x: torch.Tensor):
+    def update(self, x: torch.Tensor, presummed=None):
+        """``presummed`` = (Σx, Σx², n) already reduced over the (global) batch — the data-parallel trainer computes
+        every minibatch's moments of an epoch up front and all-reduces them in one message (MATTrainer.train)."""
+        if presummed is not None:
+            s, sq, n = presummed
+            s, sq = s.float().view_as(self.running_mean), sq.float().view_as(self.running_mean)
+            n = n.float() if torch.is_tensor(n) else float(n)
+            mean, sq_mean = s / n, sq / n
+            w = self.beta ** n if self.per_element_update else self.beta
+            self.running_mean.mul_(w).add_(mean * (1.0 - w))
+            self.running_mean_sq.mul_(w).add_(sq_mean * (1.0 - w))
+            self.debiasing_term.mul_(w).add_(1.0 * (1.0 - w))
+            return
         # the reference flattens (batch, agents, 1) minibatches to (batch*agents, 1) before updating
         x = x.float().reshape(-1, self.running_mean.numel())
         n = x.shape[0]

@@ -33,52 +33,70 @@ __device__ __forceinline__ CT dec_embed_pre_ct(const DecP& p, int rt, int& tokid
 }
 
 // ------------------------------------------------------------------------------------------ cross attention
+// cross-attention projections: q = W_q rep (from global f32), k / v = W_k x1, W_v x1 (x1 = xr, or the saved x1 when
+// xr is null) -> QB / KB / VB; x1 optionally saved (forward) or staged into XB (backward, X of dW_k / dW_v)
+__device__ __forceinline__ void cross_proj(const Mat* m, const CT* xr, const bf16_t* sv_x1_in, const float* rep,
+                                           bf16_t* sv_x1_out, const Ctx& c) {
+  const int lane = c.lane;
+  CTr xp[MAXRT], rp[MAXRT];
+#pragma unroll
+  for (int k = 0; k < MAXRT; ++k) {
+    const int rt = c.wave + 4 * k;
+    if (rt < c.NT) {
+      rp[k] = ct_pack(ld_gf(rep, c.tok0, rt, c.NR, lane));
+      xp[k] = xr ? ct_pack(xr[k]) : ld_g(sv_x1_in, c.tok0, rt, c.NR, lane);
+      if (sv_x1_out) st_g(sv_x1_out, c.tok0, rt, c.NR, xp[k], lane);
+      if (!xr) st_lds(c.XB, rt, xp[k], tok_ok(rt, c), lane);
+    }
+  }
+#pragma unroll
+  for (int mi = 0; mi < 3; ++mi) {
+    AFr W;
+    loadA(W, m[4 + mi].fa, lane);
+    const CT b = ld_vec(m[4 + mi].b, lane);
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) {
+        CT t = b;
+        mm(t, W, mi == 0 ? rp[k] : xp[k]);
+        st_lds(mi == 0 ? c.QB : mi == 1 ? c.KB : c.VB, rt, ct_pack(t), tok_ok(rt, c), lane);
+      }
+    }
+  }
+}
+
 // x <- LN(rep + proj(attn(q = W_q rep, k = W_k x, v = W_v x)))   (ma_transformer.py:114)
 template <bool SAVE>
 __device__ __forceinline__ void cross_attn_fwd_ct(const Mat* m, const LNp& ln, CT* xr, const float* rep, bf16_t* sv_x1,
                                                   bf16_t* sv_a, float* sv_lse, const Ctx& c) {
   const int lane = c.lane;
-  {
-    AFr Wq, Wk, Wv;
-    loadA(Wq, m[4].fa, lane);
-    loadA(Wk, m[5].fa, lane);
-    loadA(Wv, m[6].fa, lane);
-    const CT bq = ld_vec(m[4].b, lane), bk = ld_vec(m[5].b, lane), bv = ld_vec(m[6].b, lane);
-#pragma unroll
-    for (int k = 0; k < MAXRT; ++k) {
-      const int rt = c.wave + 4 * k;
-      if (rt < c.NT) {
-        const bool ok = tok_ok(rt, c);
-        const CTr x = ct_pack(xr[k]);
-        if (SAVE) st_g(sv_x1, c.tok0, rt, c.NR, x, lane);
-        const CTr r = ct_pack(ld_gf(rep, c.tok0, rt, c.NR, lane));
-        CT q = bq, kk = bk, v = bv;
-        mm(q, Wq, r);
-        mm(kk, Wk, x);
-        mm(v, Wv, x);
-        st_lds(c.QB, rt, ct_pack(q), ok, lane);
-        st_lds(c.KB, rt, ct_pack(kk), ok, lane);
-        st_lds(c.VB, rt, ct_pack(v), ok, lane);
-      }
-    }
-  }
+  cross_proj(m, xr, nullptr, rep, SAVE ? sv_x1 : nullptr, c);
   __syncthreads();
+  CP_MARK(24);
   attn_fwd(c.QB, c.KB, c.VB, c.QB, true, SAVE ? sv_lse : nullptr, c);
   __syncthreads();
+  CP_MARK(25);
   AFr Wp;
   loadA(Wp, m[7].fa, lane);
   const CT bp = ld_vec(m[7].b, lane), gam = ld_vec(ln.g, lane), bet = ld_vec(ln.b, lane);
+  CT rp[MAXRT];
+#pragma unroll
+  for (int k = 0; k < MAXRT; ++k) {
+    const int rt = c.wave + 4 * k;
+    if (rt < c.NT) rp[k] = ld_gf(rep, c.tok0, rt, c.NR, lane);
+  }
 #pragma unroll
   for (int k = 0; k < MAXRT; ++k) {
     const int rt = c.wave + 4 * k;
     if (rt < c.NT) {
       const CTr a = ld_lds(c.QB, rt, lane);
       if (SAVE) st_g(sv_a, c.tok0, rt, c.NR, a, lane);
-      CT t = ct_add(bp, ld_gf(rep, c.tok0, rt, c.NR, lane)), xh;
+      CT t = ct_add(bp, rp[k]), xh;
       mm(t, Wp, a);
       ln_fwd_ct(t, xh, xr[k], gam, bet);
     }
-  }
+  }  CP_MARK(26);
 }
 
 // backward: dx (w.r.t. the sublayer output) -> d x1 (returned in dx); d rep accumulated into global drep
@@ -99,14 +117,17 @@ __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, C
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
       const int rt = c.wave + 4 * k;
-      if (rt < c.NT) as[k] = ld_g(sv_a, c.tok0, rt, c.NR, lane);
+      if (rt < c.NT) {
+        as[k] = ld_g(sv_a, c.tok0, rt, c.NR, lane);
+        dres[k] = ld_gf(rep, c.tok0, rt, c.NR, lane);   // rep (the residual input) parked in dres until used
+      }
     }
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
       const int rt = c.wave + 4 * k;
       if (rt < c.NT) {
         const bool ok = tok_ok(rt, c);
-        CT s = ct_add(bp, ld_gf(rep, c.tok0, rt, c.NR, lane)), xh, yy, ds;
+        CT s = ct_add(bp, dres[k]), xh, yy, ds;
         mm(s, Wpf, as[k]);
         const float rs = ln_fwd_ct(s, xh, yy, gam, bet);
         ln_bwd_ct(dx[k], xh, rs, gam, ok, ds, dlg, dlb);
@@ -124,66 +145,60 @@ __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, C
     flush_vec(dlb, c.g(ln.db), lane);
   }
   __syncthreads();
+  CP_MARK(4);
   wgrad64(c.DQ, c.XB, m[7], c);
   __syncthreads();
+  CP_MARK(5);
+  cross_proj(m, nullptr, sv_x1, rep, nullptr, c);
+  load_lse(sv_lse, c);
+  __syncthreads();
+  CP_MARK(6);
+  attn_bwd_q(c.QB, c.KB, c.VB, c.DA, c.DQ, true, c);
+  __syncthreads();
+  CP_MARK(7);
+  attn_bwd_kv(c.QB, c.KB, c.VB, c.DA, true, c);
+  __syncthreads();
+  CP_MARK(8);
   {
-    AFr Wq, Wk, Wv;
-    loadA(Wq, m[4].fa, lane);
-    loadA(Wk, m[5].fa, lane);
-    loadA(Wv, m[6].fa, lane);
-    const CT bq = ld_vec(m[4].b, lane), bk = ld_vec(m[5].b, lane), bv = ld_vec(m[6].b, lane);
+    CTr rq[MAXRT];
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {   // q input (rep) into QB for dW_q
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) rq[k] = ct_pack(ld_gf(rep, c.tok0, rt, c.NR, lane));
+    }
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
       const int rt = c.wave + 4 * k;
-      if (rt < c.NT) {
-        const bool ok = tok_ok(rt, c);
-        const CTr x1 = ld_g(sv_x1, c.tok0, rt, c.NR, lane);
-        const CTr r = ct_pack(ld_gf(rep, c.tok0, rt, c.NR, lane));
-        CT q = bq, kk = bk, v = bv;
-        mm(q, Wq, r);
-        mm(kk, Wk, x1);
-        mm(v, Wv, x1);
-        st_lds(c.QB, rt, ct_pack(q), ok, lane);
-        st_lds(c.KB, rt, ct_pack(kk), ok, lane);
-        st_lds(c.VB, rt, ct_pack(v), ok, lane);
-        st_lds(c.XB, rt, x1, ok, lane);   // X of dWk / dWv
-      }
+      if (rt < c.NT) st_lds(c.QB, rt, rq[k], tok_ok(rt, c), lane);
     }
   }
-  load_lse(sv_lse, c);
   __syncthreads();
-  attn_bwd_q(c.QB, c.KB, c.VB, c.DA, c.DQ, true, c);
-  __syncthreads();
-  attn_bwd_kv(c.QB, c.KB, c.VB, c.DA, true, c);
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < MAXRT; ++k) {   // q input (rep) into QB for dW_q
-    const int rt = c.wave + 4 * k;
-    if (rt < c.NT) st_lds(c.QB, rt, ct_pack(ld_gf(rep, c.tok0, rt, c.NR, lane)), tok_ok(rt, c), lane);
-  }
-  __syncthreads();
+  CP_MARK(9);
   wgrad64(c.DQ, c.QB, m[4], c);
   wgrad64(c.KB, c.XB, m[5], c);
   wgrad64(c.VB, c.XB, m[6], c);
+  CP_MARK(18);
+#pragma unroll
+  for (int k = 0; k < MAXRT; ++k) {
+    const int rt = c.wave + 4 * k;
+    if (rt < c.NT) ct_zero(dx[k]);
+  }
+  proj3_bwd(m, 4, c.DQ, c.KB, c.VB, dres, dx, c);
   {
-    AFr Wq, Wk, Wv;
-    loadA(Wq, m[4].ba, lane);
-    loadA(Wk, m[5].ba, lane);
-    loadA(Wv, m[6].ba, lane);
+    CT cur[MAXRT];
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {   // d rep read-modify-write (each row owned by exactly one wave of one workgroup)
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) cur[k] = ld_gf(drep, c.tok0, rt, c.NR, lane);
+    }
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
       const int rt = c.wave + 4 * k;
-      if (rt < c.NT) {
-        mm(dres[k], Wq, ld_lds(c.DQ, rt, lane));
-        ct_zero(dx[k]);
-        mm(dx[k], Wk, ld_lds(c.KB, rt, lane));
-        mm(dx[k], Wv, ld_lds(c.VB, rt, lane));
-        // d rep read-modify-write (each row owned by exactly one wave of one workgroup)
-        st_gf(drep, c.tok0, rt, c.NR, ct_add(ld_gf(drep, c.tok0, rt, c.NR, lane), dres[k]), lane);
-      }
+      if (rt < c.NT) st_gf(drep, c.tok0, rt, c.NR, ct_add(cur[k], dres[k]), lane);
     }
   }
   __syncthreads();
+  CP_MARK(10);
 }
 
 // ------------------------------------------------------------------------------------------ action head
@@ -458,18 +473,21 @@ __device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c)
     if (lane == 0 && p.d_log_std && p.n_disc < p.L) atomicAdd(c.g(p.d_log_std) + (p.A - 1), t);
   }
   __syncthreads();
+  CP_MARK(1);
   wgrad_g(c.DA, c.XB, c.NRP, c.g(p.d_wh2), 64, p.A, 64, c.g(p.d_bh2), c.wave, lane);
   wgrad64(c.DQ, c.KB, p.h1, c);
   __syncthreads();
+  CP_MARK(19);
 }
 
 // ============================================================================================== forward
-template <int NB, bool SAVE>
+template <int NB, bool SAVE, int MA>
 __device__ __forceinline__ void dec_fwd_tile(const DecP& p, char* smem, int seq0, int nseq) {
   const Ctx c = make_ctx(p, smem, seq0, nseq);
   if (c.nseq <= 0) return;
-  zero_lds(smem, mat_train_lds_bytes(p.NRP, p.SQ, p.L), c.tid);
+  zero_lds(smem, ct_fwd_lds_bytes(p.NRP), c.tid);
   __syncthreads();
+  CP_MARK(0);
   const int lane = c.lane;
   CT xr[MAXRT];
   {
@@ -494,35 +512,30 @@ __device__ __forceinline__ void dec_fwd_tile(const DecP& p, char* smem, int seq0
     cross_attn_fwd_ct<SAVE>(B.m, B.ln[1], xr, p.rep, p.sv[b].x1, p.sv[b].a2, p.sv[b].lse2, cc);
     mlp_fwd_ct<SAVE>(B.m[8], B.m[9], B.ln[2], xr, p.sv[b].x2, p.sv[b].h, cc);
   }
-  const int MA = (p.A + 15) >> 4;
-  if (MA == 1) head_fwd_ct<1>(p, xr, SAVE, c);
-  else if (MA == 2) head_fwd_ct<2>(p, xr, SAVE, c);
-  else if (MA == 3) head_fwd_ct<3>(p, xr, SAVE, c);
-  else head_fwd_ct<4>(p, xr, SAVE, c);
+  head_fwd_ct<MA>(p, xr, SAVE, c);
+  CP_MARK(27);
 }
 
-template <int NB, bool SAVE>
-__global__ __launch_bounds__(256, WGPC) void mat_dec_fwd_ct(DecP p) {
+// MA = logit tiles of the action head: 1 (A <= 16: DCML, MPE) or 4 (A <= 64: SMAC's 36 actions)
+template <int NB, bool SAVE, int MA>
+__global__ __launch_bounds__(256, FWD_WGPC) void mat_dec_fwd_ct(DecP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  FOR_TILES(p, (dec_fwd_tile<NB, SAVE>(p, smem, s0, ns)));
+  CP_BEGIN();
+  FOR_TILES(p, (dec_fwd_tile<NB, SAVE, MA>(p, smem, s0, ns)));
+  CP_END();
 }
 
 // ============================================================================================== backward
-template <int NB>
+template <int NB, int MA>
 __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0, int nseq) {
   const Ctx c = make_ctx(p, smem, seq0, nseq);
   if (c.nseq <= 0) return;
   zero_lds(smem, mat_train_lds_bytes(p.NRP, p.SQ, p.L), c.tid);
   __syncthreads();
+  CP_MARK(0);
   const int lane = c.lane;
   CT dx[MAXRT];
-  {
-    const int MA = (p.A + 15) >> 4;
-    if (MA == 1) head_bwd_ct<1>(p, dx, c);
-    else if (MA == 2) head_bwd_ct<2>(p, dx, c);
-    else if (MA == 3) head_bwd_ct<3>(p, dx, c);
-    else head_bwd_ct<4>(p, dx, c);
-  }
+  head_bwd_ct<MA>(p, dx, c);
 #pragma unroll 1
   for (int bb = NB - 1; bb >= 0; --bb) {
     const Blk& B = p.blk[bb];
@@ -571,28 +584,50 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
         atomicAdd(c.g(p.d_wa) + col * (p.A + 1) + t, EMB[i]);
       }
   }
+  CP_MARK(30);
 }
 
-template <int NB>
+template <int NB, int MA>
 __global__ __launch_bounds__(256, WGPC) void mat_dec_bwd_ct(DecP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  FOR_TILES(p, (dec_bwd_tile<NB>(p, smem, s0, ns)));
+  CP_BEGIN();
+  FOR_TILES(p, (dec_bwd_tile<NB, MA>(p, smem, s0, ns)));
+  CP_END();
 }
 
 }  // namespace
 
+template <int MA>
+static int dec_fwd_ct(const DecP* p, int NB, int save, hipStream_t st) {
+  if (NB == 1) return save ? launch_ct(mat_dec_fwd_ct<1, true, MA>, p, true, st) : launch_ct(mat_dec_fwd_ct<1, false, MA>, p, true, st);
+  if (NB == 2) return save ? launch_ct(mat_dec_fwd_ct<2, true, MA>, p, true, st) : launch_ct(mat_dec_fwd_ct<2, false, MA>, p, true, st);
+  if (NB == 3) return save ? launch_ct(mat_dec_fwd_ct<3, true, MA>, p, true, st) : launch_ct(mat_dec_fwd_ct<3, false, MA>, p, true, st);
+  return -3;
+}
+template <int MA>
+static int dec_bwd_ct(const DecP* p, int NB, hipStream_t st) {
+  if (NB == 1) return launch_ct(mat_dec_bwd_ct<1, MA>, p, false, st);
+  if (NB == 2) return launch_ct(mat_dec_bwd_ct<2, MA>, p, false, st);
+  if (NB == 3) return launch_ct(mat_dec_bwd_ct<3, MA>, p, false, st);
+  return -3;
+}
+
 MDL_API int mdl_mat_dec_fwd_ct(const DecP* p, int NB, int save, hipStream_t st) {
   if (p->A > 64 || p->A < 1) return -1;
-  if (NB == 1) return save ? launch(mat_dec_fwd_ct<1, true>, p, st) : launch(mat_dec_fwd_ct<1, false>, p, st);
-  if (NB == 2) return save ? launch(mat_dec_fwd_ct<2, true>, p, st) : launch(mat_dec_fwd_ct<2, false>, p, st);
-  if (NB == 3) return save ? launch(mat_dec_fwd_ct<3, true>, p, st) : launch(mat_dec_fwd_ct<3, false>, p, st);
-  return -3;
+  return p->A <= 16 ? dec_fwd_ct<1>(p, NB, save, st) : dec_fwd_ct<4>(p, NB, save, st);
 }
 
 MDL_API int mdl_mat_dec_bwd_ct(const DecP* p, int NB, hipStream_t st) {
   if (p->A > 64 || p->A < 1 || 2 * p->NRP * 128 < (p->A + 1) * 256) return -1;
-  if (NB == 1) return launch(mat_dec_bwd_ct<1>, p, st);
-  if (NB == 2) return launch(mat_dec_bwd_ct<2>, p, st);
-  if (NB == 3) return launch(mat_dec_bwd_ct<3>, p, st);
-  return -3;
+  return p->A <= 16 ? dec_bwd_ct<1>(p, NB, st) : dec_bwd_ct<4>(p, NB, st);
 }
+
+#ifdef MDL_CT_PROF
+MDL_API int mdl_ctprof_dec(unsigned long long* out, int reset) {
+  if (reset) {
+    unsigned long long z[64] = {0};
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_ctprof), z, sizeof(z));
+  }
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ctprof), sizeof(unsigned long long) * 64, 0, hipMemcpyDeviceToHost);
+}
+#endif

@@ -94,8 +94,9 @@ template <int NB, bool SAVE>
 __device__ __forceinline__ void enc_fwd_tile(const EncP& p, const EncX& ex, char* smem, int seq0, int nseq) {
   const Ctx c = make_ctx(p, smem, seq0, nseq);
   if (c.nseq <= 0) return;
-  zero_lds(smem, mat_train_lds_bytes(p.NRP, p.SQ, p.L), c.tid);
+  zero_lds(smem, ct_fwd_lds_bytes(p.NRP), c.tid);
   __syncthreads();
+  CP_MARK(0);
   const int lane = c.lane, g = lane >> 4;
   CT xr[MAXRT];
   {
@@ -113,6 +114,7 @@ __device__ __forceinline__ void enc_fwd_tile(const EncP& p, const EncX& ex, char
       }
     }
   }
+  CP_MARK(28);
 #pragma unroll 1
   for (int b = 0; b < NB; ++b) {
     const Blk& B = p.blk[b];
@@ -155,12 +157,15 @@ __device__ __forceinline__ void enc_fwd_tile(const EncP& p, const EncX& ex, char
       }
     }
   }
+  CP_MARK(27);
 }
 
 template <int NB, bool SAVE>
-__global__ __launch_bounds__(256, WGPC) void mat_enc_fwd_ct(EncP p, EncX ex) {
+__global__ __launch_bounds__(256, FWD_WGPC) void mat_enc_fwd_ct(EncP p, EncX ex) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  CP_BEGIN();
   FOR_TILES(p, (enc_fwd_tile<NB, SAVE>(p, ex, smem, s0, ns)));
+  CP_END();
 }
 
 // ============================================================================================== backward
@@ -170,6 +175,7 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
   if (c.nseq <= 0) return;
   zero_lds(smem, mat_train_lds_bytes(p.NRP, p.SQ, p.L), c.tid);
   __syncthreads();
+  CP_MARK(0);
   const int lane = c.lane;
   CT dx[MAXRT];
   // ---------------- value head backward (+ incoming d rep from the decoder)
@@ -186,6 +192,12 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
     const CT w0 = ld_vec(p.wh2, lane);
     CT w1;
     if (p.n_obj > 1) w1 = ld_vec(p.wh2 + 64, lane); else ct_zero(w1);
+    CT reps[MAXRT];
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {   // every tile's encoder output requested up front (one latency, not three)
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) reps[k] = ld_gf(p.rep, c.tok0, rt, c.NR, lane);
+    }
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
       const int rt = c.wave + 4 * k;
@@ -194,7 +206,7 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
         const size_t tok = (size_t)(c.tok0 + (ok ? rt * 16 + (lane & 15) : 0));
         const float dv0 = ok ? p.dv[tok * p.n_obj] : 0.f;
         const float dv1 = (ok && p.n_obj > 1) ? p.dv[tok * p.n_obj + 1] : 0.f;
-        const CTr r = ct_pack(ld_gf(p.rep, c.tok0, rt, c.NR, lane));
+        const CTr r = ct_pack(reps[k]);
         CT hh = bh;
         mm(hh, Hf, r);
         CT gl = hh, xh, n, dn, dg;
@@ -216,7 +228,7 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
         const CTr dgr = ct_pack(dg);
         st_lds(c.DQ, rt, dgr, ok, lane);   // dY of W_h1
         st_lds(c.XB, rt, r, ok, lane);     // X of W_h1
-        CT t = ld_gf(p.drep, c.tok0, rt, c.NR, lane);
+        CT t = ld_gf(p.drep, c.tok0, rt, c.NR, lane);   // issued before the LN/GELU work of this tile
         mm(t, Hb, dgr);
         dx[k] = t;
       }
@@ -228,6 +240,7 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
     __syncthreads();
     wgrad64(c.DQ, c.XB, p.h1, c);
     __syncthreads();
+    CP_MARK(1);
   }
   // ---------------- blocks in reverse
 #pragma unroll 1
@@ -313,26 +326,15 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
       wgrad_g(c.DA, c.XB, c.NRP, c.g(p.d_we), p.od, 64, p.od, nullptr, c.wave, lane);
     }
   }
+  CP_MARK(30);
 }
 
 template <int NB>
 __global__ __launch_bounds__(256, WGPC) void mat_enc_bwd_ct(EncP p, EncX ex) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  CP_BEGIN();
   FOR_TILES(p, (enc_bwd_tile<NB>(p, ex, smem, s0, ns)));
-}
-
-template <typename K>
-int launch_x(K kern, const EncP* p, const EncX& ex, hipStream_t st) {
-  if (p->SQ <= 0 || p->NRP <= 0 || (p->SQ * p->L + 15) / 16 > 4 * MAXRT) return -4;
-  const size_t lds = mat_train_lds_bytes(p->NRP, p->SQ, p->L);
-  if (lds > LDS_BUDGET) return -2;
-  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (e != hipSuccess) return (int)e;
-  const int tiles = (p->Bs + p->SQ - 1) / p->SQ;
-  const int grid = tiles < n_cus() * WGPC ? tiles : n_cus() * WGPC;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, *p, ex);
-  MDL_CHECK_LAUNCH();
-  return 0;
+  CP_END();
 }
 
 }  // namespace
@@ -356,17 +358,27 @@ MDL_API int mdl_mat_train_geometry_ct(int L) {
 MDL_API int mdl_mat_enc_fwd_ct(const EncP* p, const float* pre_in, int NB, int save, hipStream_t st) {
   if ((!pre_in && (p->od > 16 || p->od < 1)) || p->n_obj > 2 || p->n_obj < 1) return -1;
   const EncX ex{pre_in, nullptr};
-  if (NB == 1) return save ? launch_x(mat_enc_fwd_ct<1, true>, p, ex, st) : launch_x(mat_enc_fwd_ct<1, false>, p, ex, st);
-  if (NB == 2) return save ? launch_x(mat_enc_fwd_ct<2, true>, p, ex, st) : launch_x(mat_enc_fwd_ct<2, false>, p, ex, st);
-  if (NB == 3) return save ? launch_x(mat_enc_fwd_ct<3, true>, p, ex, st) : launch_x(mat_enc_fwd_ct<3, false>, p, ex, st);
+  if (NB == 1) return save ? launch_ct(mat_enc_fwd_ct<1, true>, p, true, st, ex) : launch_ct(mat_enc_fwd_ct<1, false>, p, true, st, ex);
+  if (NB == 2) return save ? launch_ct(mat_enc_fwd_ct<2, true>, p, true, st, ex) : launch_ct(mat_enc_fwd_ct<2, false>, p, true, st, ex);
+  if (NB == 3) return save ? launch_ct(mat_enc_fwd_ct<3, true>, p, true, st, ex) : launch_ct(mat_enc_fwd_ct<3, false>, p, true, st, ex);
   return -3;
 }
 
 MDL_API int mdl_mat_enc_bwd_ct(const EncP* p, const float* pre_in, float* dpre_out, int NB, hipStream_t st) {
   if ((!pre_in && (p->od > 16 || p->od < 1)) || p->n_obj > 2 || p->n_obj < 1 || (pre_in && !dpre_out)) return -1;
   const EncX ex{pre_in, dpre_out};
-  if (NB == 1) return launch_x(mat_enc_bwd_ct<1>, p, ex, st);
-  if (NB == 2) return launch_x(mat_enc_bwd_ct<2>, p, ex, st);
-  if (NB == 3) return launch_x(mat_enc_bwd_ct<3>, p, ex, st);
+  if (NB == 1) return launch_ct(mat_enc_bwd_ct<1>, p, false, st, ex);
+  if (NB == 2) return launch_ct(mat_enc_bwd_ct<2>, p, false, st, ex);
+  if (NB == 3) return launch_ct(mat_enc_bwd_ct<3>, p, false, st, ex);
   return -3;
 }
+
+#ifdef MDL_CT_PROF
+MDL_API int mdl_ctprof_enc(unsigned long long* out, int reset) {
+  if (reset) {
+    unsigned long long z[64] = {0};
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_ctprof), z, sizeof(z));
+  }
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ctprof), sizeof(unsigned long long) * 64, 0, hipMemcpyDeviceToHost);
+}
+#endif

@@ -25,6 +25,42 @@
 
 namespace {
 
+// Phase profiler (-DMDL_CT_PROF): thread 0 of EVERY workgroup accumulates s_memtime cycles between marks (placed
+// after workgroup barriers, so a phase = the slowest wave's span) in LDS and adds them to g_ctprof once per launch
+// (no global traffic inside the kernel: the round-1 marks' read-modify-writes distorted the vmcnt waits).
+#ifdef MDL_CT_PROF
+__device__ unsigned long long g_ctprof[64];
+__shared__ unsigned long long cp_acc[64];
+#define CP_BEGIN() do { if (threadIdx.x < 64) cp_acc[threadIdx.x] = 0; __syncthreads(); \
+  if (threadIdx.x == 0) cp_acc[63] = __builtin_amdgcn_s_memtime(); } while (0)
+#define CP_MARK(k) do { if (threadIdx.x == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+  cp_acc[k] += t_ - cp_acc[63]; cp_acc[63] = t_; } } while (0)
+#define CP_END() do { __syncthreads(); if (threadIdx.x < 63) atomicAdd(&g_ctprof[threadIdx.x], cp_acc[threadIdx.x]); } while (0)
+#else
+#define CP_BEGIN() do { } while (0)
+#define CP_MARK(k) do { } while (0)
+#define CP_END() do { } while (0)
+#endif
+
+// Forward kernels keep only Q / K / V in LDS (3 of the 6 token-major buffers): 74 KB at 192 rows, so TWO
+// workgroups fit per CU (8 waves, 2 per SIMD: one workgroup's load / barrier stalls overlap the other's compute).
+constexpr int FWD_WGPC = 2;
+__host__ __device__ inline size_t ct_fwd_lds_bytes(int NRP) { return (size_t)NRP * 64 * 2 * 3; }
+
+template <typename K, typename PT, typename... X>
+static int launch_ct(K kern, const PT* p, bool fwd, hipStream_t st, X... extra) {
+  if (p->SQ <= 0 || p->NRP <= 0 || (p->SQ * p->L + 15) / 16 > 4 * MAXRT) return -4;   // geometry not valid here
+  const size_t lds = fwd ? ct_fwd_lds_bytes(p->NRP) : mat_train_lds_bytes(p->NRP, p->SQ, p->L);
+  if (lds > (fwd ? LDS_BUDGET / FWD_WGPC : LDS_BUDGET)) return -2;
+  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return (int)e;
+  const int tiles = (p->Bs + p->SQ - 1) / p->SQ;
+  const int cap = n_cus() * (fwd ? FWD_WGPC : 1);
+  hipLaunchKernelGGL(kern, dim3(tiles < cap ? tiles : cap), dim3(256), lds, st, *p, extra...);
+  MDL_CHECK_LAUNCH();
+  return 0;
+}
+
 struct CT { f32x4 v[4]; };          // v[mt][r] = feature 16mt + 4g + r of token (lane & 15) of a 16-token tile
 struct CTr { uint2 q[4]; };         // the same as packed bf16: q[mt] = features 16mt+4g .. +3
 struct AFr { bf16x8 f[4][2]; };     // A fragments of a 64x64 weight (rows 16mt + lane&15, k-step s, perm k order)
@@ -296,6 +332,43 @@ __device__ __forceinline__ void wgrad64(const bf16_t* Y, const bf16_t* X, const 
   wgrad_g(Y, X, c.NRP, c.g(m.dW), 64, 64, 64, c.g(m.db), c.wave, c.lane);
 }
 
+// q / k / v projections of the packed tiles xp (one weight matrix live at a time) -> QB / KB / VB; m0 = index of
+// the query matrix (0: self attention; the cross attention has its own q input)
+__device__ __forceinline__ void proj3(const Mat* m, int m0, const CTr* xp, const Ctx& c) {
+  bf16_t* outs[3] = {c.QB, c.KB, c.VB};
+#pragma unroll
+  for (int mi = 0; mi < 3; ++mi) {
+    AFr W;
+    loadA(W, m[m0 + mi].fa, c.lane);
+    const CT b = ld_vec(m[m0 + mi].b, c.lane);
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) {
+        CT t = b;
+        mm(t, W, xp[k]);
+        st_lds(outs[mi], rt, ct_pack(t), tok_ok(rt, c), c.lane);
+      }
+    }
+  }
+}
+
+// dx[k] (+)= Σ_i W_iᵀ · (tile k of LDS buffer src_i) for the three projection matrices m[m0 .. m0+2]
+__device__ __forceinline__ void proj3_bwd(const Mat* m, int m0, const bf16_t* s0, const bf16_t* s1, const bf16_t* s2,
+                                          CT* d0, CT* d12, const Ctx& c) {
+  const bf16_t* srcs[3] = {s0, s1, s2};
+#pragma unroll
+  for (int mi = 0; mi < 3; ++mi) {
+    AFr W;
+    loadA(W, m[m0 + mi].ba, c.lane);
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + 4 * k;
+      if (rt < c.NT) mm(mi == 0 ? d0[k] : d12[k], W, ld_lds(srcs[mi], rt, c.lane));
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------ sublayers (forward)
 // self attention: x <- LN(x + proj(attn(q(x), k(x), v(x))))   (ma_transformer.py:89-92,112)
 template <bool SAVE>
@@ -303,31 +376,22 @@ __device__ __forceinline__ void self_attn_fwd_ct(const Mat* m, const LNp& ln, CT
                                                  bf16_t* sv_a, float* sv_lse, const Ctx& c) {
   const int lane = c.lane;
   {
-    AFr Wq, Wk, Wv;
-    loadA(Wq, m[0].fa, lane);
-    loadA(Wk, m[1].fa, lane);
-    loadA(Wv, m[2].fa, lane);
-    const CT bq = ld_vec(m[0].b, lane), bk = ld_vec(m[1].b, lane), bv = ld_vec(m[2].b, lane);
+    CTr xp[MAXRT];
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
       const int rt = c.wave + 4 * k;
       if (rt < c.NT) {
-        const bool ok = tok_ok(rt, c);
-        const CTr x = ct_pack(xr[k]);
-        if (SAVE) st_g(sv_xin, c.tok0, rt, c.NR, x, lane);
-        CT q = bq, kk = bk, v = bv;
-        mm(q, Wq, x);
-        mm(kk, Wk, x);
-        mm(v, Wv, x);
-        st_lds(c.QB, rt, ct_pack(q), ok, lane);
-        st_lds(c.KB, rt, ct_pack(kk), ok, lane);
-        st_lds(c.VB, rt, ct_pack(v), ok, lane);
+        xp[k] = ct_pack(xr[k]);
+        if (SAVE) st_g(sv_xin, c.tok0, rt, c.NR, xp[k], lane);
       }
     }
+    proj3(m, 0, xp, c);
   }
   __syncthreads();
+  CP_MARK(20);
   attn_fwd(c.QB, c.KB, c.VB, c.QB, causal, SAVE ? sv_lse : nullptr, c);
   __syncthreads();
+  CP_MARK(21);
   AFr Wp;
   loadA(Wp, m[3].fa, lane);
   const CT bp = ld_vec(m[3].b, lane), gam = ld_vec(ln.g, lane), bet = ld_vec(ln.b, lane);
@@ -341,7 +405,7 @@ __device__ __forceinline__ void self_attn_fwd_ct(const Mat* m, const LNp& ln, CT
       mm(t, Wp, a);
       ln_fwd_ct(t, xh, xr[k], gam, bet);
     }
-  }
+  }  CP_MARK(22);
 }
 
 // MLP: x <- LN(x + W2 GELU(W1 x + b1) + b2)   (ma_transformer.py:84-86,91-92)
@@ -368,6 +432,7 @@ __device__ __forceinline__ void mlp_fwd_ct(const Mat& m1, const Mat& m2, const L
       ln_fwd_ct(mo, xh, xr[k], gam, bet);
     }
   }
+  CP_MARK(23);
 }
 
 // ------------------------------------------------------------------------------------------ sublayers (backward)
@@ -427,9 +492,11 @@ __device__ __forceinline__ void mlp_bwd_ct(const Mat& m1, const Mat& m2, const L
   flush_vec(dlg, c.g(ln.dg), lane);
   flush_vec(dlb, c.g(ln.db), lane);
   __syncthreads();
+  CP_MARK(2);
   wgrad64(c.DA, c.XB, m2, c);
   wgrad64(c.KB, c.QB, m1, c);
   __syncthreads();
+  CP_MARK(3);
 }
 
 // recompute + store q / k / v of the saved input, attention backward, weight gradients; returns through dx (+=) the
@@ -479,55 +546,32 @@ __device__ __forceinline__ void self_attn_bwd_ct(const Mat* m, const LNp& ln, CT
     flush_vec(dlb, c.g(ln.db), lane);
   }
   __syncthreads();
+  CP_MARK(11);
   wgrad64(c.DQ, c.XB, m[3], c);
   __syncthreads();
-  {
-    AFr Wq, Wk, Wv;
-    loadA(Wq, m[0].fa, lane);
-    loadA(Wk, m[1].fa, lane);
-    loadA(Wv, m[2].fa, lane);
-    const CT bq = ld_vec(m[0].b, lane), bk = ld_vec(m[1].b, lane), bv = ld_vec(m[2].b, lane);
+  CP_MARK(12);
+  proj3(m, 0, xin, c);
 #pragma unroll
-    for (int k = 0; k < MAXRT; ++k) {
-      const int rt = c.wave + 4 * k;
-      if (rt < c.NT) {
-        const bool ok = tok_ok(rt, c);
-        CT q = bq, kk = bk, v = bv;
-        mm(q, Wq, xin[k]);
-        mm(kk, Wk, xin[k]);
-        mm(v, Wv, xin[k]);
-        st_lds(c.QB, rt, ct_pack(q), ok, lane);
-        st_lds(c.KB, rt, ct_pack(kk), ok, lane);
-        st_lds(c.VB, rt, ct_pack(v), ok, lane);
-        st_lds(c.XB, rt, xin[k], ok, lane);   // X of dWq / dWk / dWv
-      }
-    }
+  for (int k = 0; k < MAXRT; ++k) {
+    const int rt = c.wave + 4 * k;
+    if (rt < c.NT) st_lds(c.XB, rt, xin[k], tok_ok(rt, c), lane);   // X of dWq / dWk / dWv
   }
   load_lse(sv_lse, c);
   __syncthreads();
+  CP_MARK(13);
   attn_bwd_q(c.QB, c.KB, c.VB, c.DA, c.DQ, causal, c);
   __syncthreads();
+  CP_MARK(14);
   attn_bwd_kv(c.QB, c.KB, c.VB, c.DA, causal, c);
   __syncthreads();
+  CP_MARK(15);
   wgrad64(c.DQ, c.XB, m[0], c);
   wgrad64(c.KB, c.XB, m[1], c);
   wgrad64(c.VB, c.XB, m[2], c);
-  {
-    AFr Wq, Wk, Wv;
-    loadA(Wq, m[0].ba, lane);
-    loadA(Wk, m[1].ba, lane);
-    loadA(Wv, m[2].ba, lane);
-#pragma unroll
-    for (int k = 0; k < MAXRT; ++k) {
-      const int rt = c.wave + 4 * k;
-      if (rt < c.NT) {
-        mm(dx[k], Wq, ld_lds(c.DQ, rt, lane));
-        mm(dx[k], Wk, ld_lds(c.KB, rt, lane));
-        mm(dx[k], Wv, ld_lds(c.VB, rt, lane));
-      }
-    }
-  }
+  CP_MARK(16);
+  proj3_bwd(m, 0, c.DQ, c.KB, c.VB, dx, dx, c);
   __syncthreads();
+  CP_MARK(17);
 }
 
 }  // namespace

@@ -143,6 +143,64 @@ MDL_API int mdl_masked_sums(const float* x, const float* mask, int n, int mdiv, 
   return 0;
 }
 
+// mb_stats: per-minibatch return statistics of one PPO epoch, computed up front so that a data-parallel epoch needs
+// ONE statistics all-reduce (with the advantage moments) instead of one per minibatch inside the loss.
+// out[m] = (Σ ret_o (n_obj), Σ ret_o² (n_obj), token count, Σ active) over the rows perm[m*mb .. (m+1)*mb), each row
+// `width` tokens.  Fixed-order two-pass fp64 reduction (bitwise repeatable, no float atomics).
+constexpr int MBS_PARTS = 32;
+constexpr int MBS_K = 6;   // 2 * n_obj + 2 for n_obj <= 2
+
+__global__ __launch_bounds__(256) void mb_stats_partial_kernel(const float* __restrict__ ret,
+                                                               const float* __restrict__ active,
+                                                               const int64_t* __restrict__ perm, int mb, int width,
+                                                               int n_obj, double* __restrict__ part) {
+  const int m = blockIdx.y, K = 2 * n_obj + 2;
+  double acc[MBS_K];
+#pragma unroll
+  for (int k = 0; k < MBS_K; ++k) acc[k] = 0.0;
+  const int total = mb * width;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += MBS_PARTS * 256) {
+    const long long row = perm[(long long)m * mb + i / width];
+    const long long tok = row * width + i % width;
+    for (int o = 0; o < n_obj; ++o) {
+      const double r = (double)ret[tok * n_obj + o];
+      acc[o] += r;
+      acc[n_obj + o] += r * r;
+    }
+    acc[2 * n_obj] += 1.0;
+    acc[2 * n_obj + 1] += (double)active[tok];
+  }
+  __shared__ double red[MBS_K][256];
+#pragma unroll
+  for (int k = 0; k < MBS_K; ++k) red[k][threadIdx.x] = acc[k];
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w)
+      for (int k = 0; k < K; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x < K) part[((size_t)m * MBS_PARTS + blockIdx.x) * K + threadIdx.x] = red[threadIdx.x][0];
+}
+
+__global__ void mb_stats_final_kernel(const double* __restrict__ part, int n_mb, int K, double* __restrict__ out) {
+  const int i = threadIdx.x;
+  if (i >= n_mb * K) return;
+  const int m = i / K, k = i % K;
+  double s = 0.0;
+  for (int p = 0; p < MBS_PARTS; ++p) s += part[((size_t)m * MBS_PARTS + p) * K + k];
+  out[i] = s;
+}
+
+MDL_API int mdl_mb_stats(const float* ret, const float* active, const int64_t* perm, int n_mb, int mb, int width,
+                         int n_obj, double* part, double* out, hipStream_t s) {
+  if (n_obj < 1 || 2 * n_obj + 2 > MBS_K || n_mb < 1 || n_mb * (2 * n_obj + 2) > 1024) return -1;
+  hipLaunchKernelGGL(mb_stats_partial_kernel, dim3(MBS_PARTS, n_mb), dim3(256), 0, s, ret, active, perm, mb, width,
+                     n_obj, part);
+  hipLaunchKernelGGL(mb_stats_final_kernel, dim3(1), dim3(1024), 0, s, part, n_mb, 2 * n_obj + 2, out);
+  MDL_CHECK_LAUNCH();
+  return 0;
+}
+
 // gather_rows: dst_k[r, :] = src_k[idx[r], :] for up to 10 row-major fp32 tensors in ONE launch (blockIdx.y = k);
 // entries flagged `norm` are standardised on the fly with the masked_sums statistics:
 // (x - mean) / (std + eps), std the population std — the normalised advantage of the reference, computed only for

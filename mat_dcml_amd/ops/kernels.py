@@ -137,6 +137,26 @@ def masked_sums(x, mask):
     return out
 
 
+sig("mdl_mb_stats", vp, vp, vp, i32, i32, i32, i32, vp, vp, vp)
+_MBS_WS = {}
+
+
+def mb_stats(ret, active, perm, n_mb):
+    """Per-minibatch (Σ ret_o, Σ ret_o², count, Σ active) of one epoch's partition ``perm`` (n_mb equal slices of
+    rows; every row = ``ret.shape[1]`` tokens) as a device fp64 [n_mb, 2·n_obj + 2]."""
+    assert ret.is_contiguous() and active.is_contiguous() and perm.dtype == torch.int64 and perm.is_contiguous()
+    n_obj = ret.shape[-1]
+    width = ret[0].numel() // n_obj
+    mb = perm.numel() // n_mb
+    K = 2 * n_obj + 2
+    ws = _MBS_WS.get(ret.device)
+    if ws is None or ws.numel() < n_mb * 32 * K:
+        ws = _MBS_WS[ret.device] = torch.empty(max(n_mb, 16) * 32 * K, dtype=torch.float64, device=ret.device)
+    out = torch.empty(n_mb, K, dtype=torch.float64, device=ret.device)
+    check(lib().mdl_mb_stats(P(ret), P(active), P(perm), n_mb, mb, width, n_obj, P(ws), P(out), _stream()), "mb_stats")
+    return out
+
+
 class GatherEnt(ctypes.Structure):
     _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("width", ctypes.c_int), ("norm", ctypes.c_int)]
 

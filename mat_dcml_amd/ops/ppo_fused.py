@@ -195,7 +195,7 @@ class PPOLossFused:
             vnm._mdl_flat = flat
         return flat
 
-    def run(self, values, logp, ent, mb, comm=None):
+    def run(self, values, logp, ent, mb, comm=None, pre_stats=None):
         """values (N, n_obj), logp / ent (N, 1) fp32 contiguous → (dv, dlogp, dent).  Losses accumulate into
         ``self.out`` = [policy, value, entropy, ratio] (caller zeroes it per log window)."""
         tr = self.tr
@@ -209,16 +209,20 @@ class PPOLossFused:
         vn = self._vn_buffer(n_obj, dev)
         ts = [t.reshape(-1).contiguous() if t.is_contiguous() else t.contiguous() for t in
               (mb["old_logp"], mb["adv"], mb["value_preds"], mb["returns"], mb["active"])]
+        stats = self.stats if pre_stats is None else pre_stats
         a = PPOArgs(n=N, n_obj=n_obj, v=P(values), logp=P(logp), ent=P(ent), old_logp=P(ts[0]), adv=P(ts[1]),
                     vpred=P(ts[2]), ret=P(ts[3]), active=P(ts[4]), dv=P(dv), dlogp=P(dlp), dent=P(dent),
-                    stats=P(self.stats), out=P(self.out), vn=P(vn), clip=tr.clip_param, coef_v=tr.value_loss_coef,
+                    stats=P(stats), out=P(self.out), vn=P(vn), clip=tr.clip_param, coef_v=tr.value_loss_coef,
                     coef_e=tr.entropy_coef, huber_delta=tr.huber_delta, beta=vnm.beta if vnm is not None else 1.0,
                     eps=vnm.epsilon if vnm is not None else 1e-5,
                     omb=(1.0 - vnm.beta) if vnm is not None else 0.0, use_huber=int(tr._use_huber_loss),
                     use_clip_v=int(tr._use_clipped_value_loss), use_vam=int(tr._use_value_active_masks),
                     use_pam=int(tr._use_policy_active_masks), use_vn=int(vnm is not None),
                     update_vn=int(vnm is not None))
-        if comm is not None and comm.world_size > 1 and vnm is not None:
+        if pre_stats is not None:   # statistics of this minibatch precomputed (and all-reduced) for the epoch
+            assert pre_stats.dtype == torch.float32 and pre_stats.numel() == 2 * n_obj + 2 and pre_stats.is_contiguous()
+            check(lib().mdl_ppo_finish(ctypes.byref(a), _stream()), "ppo_finish")
+        elif comm is not None and comm.world_size > 1 and vnm is not None:
             check(lib().mdl_ppo_reduce(ctypes.byref(a), _stream()), "ppo_reduce")
             comm.all_reduce_sum_(self.stats[: 2 * n_obj + 1])
             check(lib().mdl_ppo_finish(ctypes.byref(a), _stream()), "ppo_finish")

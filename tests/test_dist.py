@@ -159,3 +159,92 @@ def test_dp_ranks_share_weights_but_not_exploration_noise():
     out = spawn(_rng_case)
     assert out[0][0] == out[1][0]
     assert out[0][1] != out[1][1]
+
+
+# ------------------------------------------------------------------------------------------ DP at 2 / 4 / 8 ranks
+E_TOT, T_SYN, W_SYN = 8, 4, 4
+
+
+def _synthetic_trainer(comm, E, env_off):
+    """A MAT trainer + buffer over envs [env_off, env_off + E) of a fixed synthetic rollout (same data whatever the
+    rank count)."""
+    from mat_dcml_amd.algos.buffer import RolloutBuffer
+    from mat_dcml_amd.algos.mat_trainer import MATTrainer
+    from mat_dcml_amd.algos.policy import TransformerPolicy
+    from mat_dcml_amd.config import get_config, parse_args
+    from mat_dcml_amd.envs.dcml.spaces import dcml_action_spaces
+    args = parse_args(["--env_name", "DCML", "--n_workers", str(W_SYN), "--ppo_epoch", "3", "--num_mini_batch", "1",
+                       "--use_valuenorm", "--lr", "1e-3"], get_config(), warn=False)
+    A = W_SYN + 1
+    torch.manual_seed(0)
+    pol = TransformerPolicy(args, [7], [W_SYN + 2], dcml_action_spaces(W_SYN)[0], A)
+    comm.attach_flat_grads(pol.transformer.parameters())
+    tr = MATTrainer(args, pol, A, comm=comm)
+    buf = RolloutBuffer(T_SYN, E, A, 7, W_SYN + 2, 2)
+    g = torch.Generator().manual_seed(123)
+    full = {"obs": torch.rand(T_SYN + 1, E_TOT, A, 7, generator=g),
+            "actions": (torch.rand(T_SYN, E_TOT, A, 1, generator=g) < 0.5).float(),
+            "action_log_probs": -torch.rand(T_SYN, E_TOT, A, 1, generator=g),
+            "value_preds": torch.randn(T_SYN + 1, E_TOT, A, 1, generator=g),
+            "rewards": torch.randn(T_SYN, E_TOT, A, 1, generator=g) * 5}
+    for k, v in full.items():
+        getattr(buf, k).copy_(v[:, env_off:env_off + E])
+    return tr, buf, pol
+
+
+def _dp_equiv_case(comm):
+    E = E_TOT // comm.world_size
+    tr, buf, pol = _synthetic_trainer(comm, E, comm.rank * E)
+    tr.prep_training()
+    tr.train(buf)
+    flat = torch.cat([p.detach().reshape(-1) for p in pol.transformer.parameters()])
+    vn = [t.clone() for t in tr.value_normalizer.running_mean_var()]
+    return flat.numpy(), [t.numpy() for t in vn], tr.collectives   # numpy: tensors would travel by shared fd
+
+
+def _single_reference():
+    from mat_dcml_amd.parallel.comm import Comm
+    tr, buf, pol = _synthetic_trainer(Comm(), E_TOT, 0)
+    tr.prep_training()
+    tr.train(buf)
+    return torch.cat([p.detach().reshape(-1) for p in pol.transformer.parameters()]), \
+        [t.clone() for t in tr.value_normalizer.running_mean_var()]
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_dp_equals_single_process_large_batch(world):
+    """N ranks with 1/N of the envs each == one process with all of them: parameters identical across ranks and
+    within 1e-5 of the single-process update (full-batch minibatches, so the partition does not matter); one
+    statistics all-reduce per epoch + one gradient all-reduce per minibatch."""
+    torch.set_num_threads(1)
+    ref, ref_vn = _single_reference()
+    out = spawn(_dp_equiv_case, world=world)
+    for r in range(1, world):
+        assert (out[r][0] == out[0][0]).all()
+    err = (torch.from_numpy(out[0][0]) - ref).abs().max().item()
+    assert err < 1e-5, err
+    for a, b in zip(out[0][1], ref_vn):
+        assert torch.allclose(torch.from_numpy(a), b, rtol=1e-5, atol=1e-6)
+    ppo_epoch, n_mb = 3, 1
+    assert all(o[2] == ppo_epoch * (n_mb + 1) for o in out.values()), [o[2] for o in out.values()]
+
+
+def _runner_case_world(comm):
+    from mat_dcml_amd.config import get_config, parse_args
+    from mat_dcml_amd.runner.dcml_runner import DCMLRunner
+    args = parse_args(["--n_workers", "4", "--n_rollout_threads", "2", "--episode_length", "3", "--ppo_epoch", "2",
+                       "--num_mini_batch", "2", "--use_valuenorm", "--env_name", "DCML"], get_config(), warn=False)
+    r = DCMLRunner({"all_args": args, "device": comm.device, "run_dir": None, "comm": comm})
+    r.warmup()
+    r.train_iteration()
+    flat = torch.cat([p.detach().reshape(-1) for p in r.policy.transformer.parameters()])
+    return float(flat.double().sum()), float(flat.double().pow(2).sum()), r.trainer.collectives, \
+        [float(t) for t in r.trainer.value_normalizer.running_mean_var()]
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_dp_runner_ranks_stay_in_sync_at_4_and_8(world):
+    out = spawn(_runner_case_world, world=world)
+    for r in range(1, world):
+        assert out[r][0] == out[0][0] and out[r][1] == out[0][1] and out[r][3] == out[0][3]
+    assert out[0][2] == 2 * (2 + 1)   # 2 epochs x (1 statistics + 2 gradient all-reduces)

@@ -111,3 +111,18 @@ def test_masked_sums_and_gather_match_torch(gpu):
     assert torch.equal(out["obs"], obs[idx]) and torch.equal(out["actions"], act[idx])
     norm = rl_ops.normalize_from_sums(adv, ref).reshape(T * E, A, 1)[idx]
     torch.testing.assert_close(out["adv"], norm, rtol=1e-6, atol=1e-6)
+
+
+def test_mb_stats_matches_torch(gpu):
+    """Per-minibatch return moments of one epoch (DP statistics precompute) vs torch on the gathered rows."""
+    g = torch.Generator(device=gpu).manual_seed(5)
+    N, A, K = 400, 33, 2
+    ret = torch.randn(N, A, K, device=gpu, generator=g) * 7
+    act = (torch.rand(N, A, 1, device=gpu, generator=g) > 0.1).float()
+    perm = torch.randperm(N, device=gpu, generator=g)
+    out = kernels.mb_stats(ret, act, perm, 4)
+    for m, idx in enumerate(perm.view(4, -1)):
+        r = ret[idx].double().reshape(-1, K)
+        ref = torch.cat([r.sum(0), (r * r).sum(0), torch.tensor([float(r.shape[0])], device=gpu, dtype=torch.float64),
+                         act[idx].double().sum().reshape(1)])
+        assert torch.allclose(out[m], ref, rtol=1e-10, atol=1e-8), (m, out[m], ref)
