@@ -4,7 +4,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_train.py tests/test_gpu_ppo.py tests/test_gpu_rl_ops.py -x -v -s --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/ct_tests.log 2>&1; rc=$?
+timeout -k 10 300 python -u -m pytest tests/test_gpu_train.py tests/test_gpu_ppo.py tests/test_gpu_rl_ops.py tests/test_dist.py -x -v -s --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/ct_tests.log 2>&1; rc=$?
 grep -E "PASSED|FAILED|Error|error|assert" gpurun_out/ct_tests.log | head -40; tail -3 gpurun_out/ct_tests.log
 [ $rc -ne 0 ] && exit 1
 timeout -k 10 200 python -u bench.py --steps 5 --warmup 2 --no_eval > gpurun_out/bench_ct.log 2>&1 || { tail -20 gpurun_out/bench_ct.log; exit 2; }
