@@ -1,0 +1,251 @@
+// Observation embedding for wide observations (SMAC 27m_vs_30m: obs_dim 1288) on MFMA — the part of the encoder's
+// obs_encoder (ma_transformer.py:133-134: LayerNorm(obs_dim) -> Linear(obs_dim, 64) -> GELU) that the fused encoder
+// kernels (mat_enc_ct.hip, `pre_in`) cannot hold in a lane.  Output: pre = W_e · LN_obs(x) + b_e, [tok][64] f32.
+//
+// One pass over x (the only large operand: 5 KB per token) by folding the LayerNorm into the GEMM:
+//   LN_obs(x)_k = (x_k - mu) r g_k + b_k  =>  pre_f = r (W' x)_f - r mu c1_f + c0_f,
+//   W' = W_e diag(g) (bf16, packed per optimizer step), c1_f = Σ_k W'_fk (of the rounded W'), c0_f = W_e b + b_e,
+// with mu / r from the same pass (Σx, Σx² per token).  x enters the MFMA as a hi/lo bf16 pair (≈16 significant
+// bits) so the r·mu·c1 cancellation keeps fp32-like accuracy.
+//
+// Backward (no gradient w.r.t. the data): with P_tf = dpre_tf r_t,
+//   M = Pᵀ x (64 x od, token reduction on MFMA),  u_f = Σ_t P_tf mu_t,  db_f = Σ_t dpre_tf,
+//   dW_fk = g_k (M_fk - u_f) + b_k db_f,   dg_k = Σ_f W_fk (M_fk - u_f),   db_obs_k = Σ_f W_fk db_f,   db_e = db.
+#include "mat_train_common.h"
+
+namespace {
+
+constexpr int OE_TOK = 64;   // tokens per forward workgroup (4 waves x 16)
+
+struct OEArgs {
+  int N, od, KS;               // tokens, obs dim, k-steps of 32 (ceil(od / 32))
+  const float* x;              // [N][od]
+  const float* we;             // [64][od] W_e
+  const float* be;             // [64]
+  const float* g;              // [od] LN_obs weight
+  const float* b;              // [od] LN_obs bias
+  bf16_t* wpack;               // [KS][4][64 lanes][8] W' A fragments (natural k order)
+  float* c01;                  // [2][64] c1, c0
+  float* pre;                  // [N][64]
+  float* stat;                 // [N][2] mu, rstd
+  // backward
+  const float* dpre;           // [N][64]
+  float* M;                    // [64][od] workspace (zeroed by the host)
+  float* ud;                   // [2][64] u, db workspace (zeroed by the host)
+  float *d_we, *d_be, *d_g, *d_b;
+};
+
+// W' = W_e diag(g) as bf16 A fragments + c1 (from the rounded values) / c0.  One block per output feature f.
+__global__ __launch_bounds__(256) void obs_embed_pack_kernel(OEArgs a) {
+  const int f = blockIdx.x;
+  float s1 = 0.f, s0 = 0.f;
+  for (int k = threadIdx.x; k < a.KS * 32; k += 256) {
+    const bool in = k < a.od;
+    const float w = in ? a.we[(size_t)f * a.od + k] : 0.f;
+    const uint16_t wb = f2bf(in ? w * a.g[k] : 0.f);
+    s1 += bf2f(wb);
+    s0 += in ? w * a.b[k] : 0.f;
+    // fragment position: k-step s = k / 32, lane = 16 (k%32 / 8) + f%16, j = k % 8, mt = f / 16
+    const int s = k >> 5, kk = k & 31, lane = 16 * (kk >> 3) + (f & 15), j = kk & 7, mt = f >> 4;
+    a.wpack[(((size_t)s * 4 + mt) * 64 + lane) * 8 + j] = wb;
+  }
+  __shared__ float red[2][256];
+  red[0][threadIdx.x] = s1;
+  red[1][threadIdx.x] = s0;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + w];
+      red[1][threadIdx.x] += red[1][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    a.c01[f] = red[0][0];
+    a.c01[64 + f] = red[1][0] + a.be[f];
+  }
+}
+
+// forward: wave w of the block owns tokens t0 + 16w .. +15 (token on lane & 15, features 16mt + 4g + r in registers)
+__global__ __launch_bounds__(256) void obs_embed_fwd_kernel(OEArgs a) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  const int tok = blockIdx.x * OE_TOK + wave * 16 + c;
+  const bool ok = tok < a.N;
+  const float* xr = a.x + (size_t)(ok ? tok : 0) * a.od;
+  f32x4 acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  float sx = 0.f, sxx = 0.f;
+  const bool vec4 = (a.od & 3) == 0;
+  for (int s = 0; s < a.KS; ++s) {
+    const int k0 = 32 * s + 8 * g;
+    float v[8];
+    if (vec4 && k0 + 8 <= a.od) {
+      const float4 p = *(const float4*)(xr + k0), q = *(const float4*)(xr + k0 + 4);
+      v[0] = p.x; v[1] = p.y; v[2] = p.z; v[3] = p.w; v[4] = q.x; v[5] = q.y; v[6] = q.z; v[7] = q.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = k0 + j < a.od ? xr[k0 + j] : 0.f;
+    }
+    bf16x8 hi, lo;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float xv = ok ? v[j] : 0.f;
+      sx += xv;
+      sxx += xv * xv;
+      const uint16_t h = f2bf(xv);
+      hi[j] = (short)h;
+      lo[j] = (short)f2bf(xv - bf2f(h));
+    }
+    const bf16_t* wp = a.wpack + ((size_t)s * 4 * 64 + lane) * 8;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const bf16x8 w = *(const bf16x8*)(wp + (size_t)mt * 64 * 8);
+      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, hi, acc[mt], 0, 0, 0);
+      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, lo, acc[mt], 0, 0, 0);
+    }
+  }
+  sx = cross_row_sum(sx);
+  sxx = cross_row_sum(sxx);
+  const float mu = sx / (float)a.od;
+  const float var = fmaxf(sxx / (float)a.od - mu * mu, 0.f);
+  const float r = rsqrtf(var + 1e-5f);
+  if (ok) {
+    float* out = a.pre + (size_t)tok * 64 + 4 * g;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      f32x4 y;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int f = 16 * mt + 4 * g + q;
+        y[q] = r * acc[mt][q] - r * mu * a.c01[f] + a.c01[64 + f];
+      }
+      *(f32x4*)(out + 16 * mt) = y;
+    }
+    if (g == 0) {
+      a.stat[2 * (size_t)tok] = mu;
+      a.stat[2 * (size_t)tok + 1] = r;
+    }
+  }
+}
+
+// backward step 1: M += Pᵀ x over a token range, for one 64-column block of x.  Token-major swizzled bf16 LDS tiles
+// of 32 tokens (P, x hi, x lo); wave w owns output rows f in [16w, 16w+16); 4 column tiles of 16.
+constexpr int OEB_SPLIT = 16;   // token ranges per column block
+__global__ __launch_bounds__(256) void obs_embed_bwd_m_kernel(OEArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16_t Pt[32 * 64], Xh[32 * 64], Xl[32 * 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c16 = lane & 15, g = lane >> 4;
+  const int col0 = blockIdx.x * 64;
+  const int t_lo = (int)((long long)a.N * blockIdx.y / OEB_SPLIT), t_hi = (int)((long long)a.N * (blockIdx.y + 1) / OEB_SPLIT);
+  RT acc;
+  rt_zero(acc);
+  for (int t0 = t_lo; t0 < t_hi; t0 += 32) {
+    // stage: 32 tokens x 64 values of P = dpre * r and of x (hi / lo); thread -> (row, 8-column chunk)
+    {
+      const int row = threadIdx.x >> 3, lc = threadIdx.x & 7;
+      const int t = t0 + row;
+      const bool ok = t < t_hi;
+      float pv[8], xv[8];
+      const float rr = ok ? a.stat[2 * (size_t)t + 1] : 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        pv[j] = ok ? a.dpre[(size_t)t * 64 + 8 * lc + j] * rr : 0.f;
+        const int k = col0 + 8 * lc + j;
+        xv[j] = (ok && k < a.od) ? a.x[(size_t)t * a.od + k] : 0.f;
+      }
+      uint4 up, uh, ul;
+      uint32_t* p32 = (uint32_t*)&up;
+      uint32_t* h32 = (uint32_t*)&uh;
+      uint32_t* l32 = (uint32_t*)&ul;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        p32[j] = (uint32_t)f2bf(pv[2 * j]) | ((uint32_t)f2bf(pv[2 * j + 1]) << 16);
+        const uint16_t h0 = f2bf(xv[2 * j]), h1 = f2bf(xv[2 * j + 1]);
+        h32[j] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+        l32[j] = (uint32_t)f2bf(xv[2 * j] - bf2f(h0)) | ((uint32_t)f2bf(xv[2 * j + 1] - bf2f(h1)) << 16);
+      }
+      const int o = (row << 6) + ((lc ^ ((row >> 1) & 7)) << 3);
+      *(uint4*)(Pt + o) = up;
+      *(uint4*)(Xh + o) = uh;
+      *(uint4*)(Xl + o) = ul;
+    }
+    __syncthreads();
+    const bf16x8 pa = ld_frag_T(Pt, 0, 16 * wave, lane);
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      acc.v[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, ld_frag_T(Xh, 0, 16 * ct, lane), acc.v[ct], 0, 0, 0);
+      acc.v[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, ld_frag_T(Xl, 0, 16 * ct, lane), acc.v[ct], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int f = 16 * wave + 4 * g + r, k = col0 + 16 * ct + c16;
+      if (k < a.od) atomicAdd(a.M + (size_t)f * a.od + k, acc.v[ct][r]);
+    }
+}
+
+// backward step 1b: u_f = Σ_t dpre_tf r_t mu_t and db_f = Σ_t dpre_tf (thread = (token lane, feature))
+__global__ __launch_bounds__(256) void obs_embed_bwd_u_kernel(OEArgs a) {
+  const int f = threadIdx.x & 63, tl = threadIdx.x >> 6;
+  float u = 0.f, d = 0.f;
+  for (int t = blockIdx.x * 4 + tl; t < a.N; t += gridDim.x * 4) {
+    const float dp = a.dpre[(size_t)t * 64 + f];
+    u += dp * a.stat[2 * (size_t)t + 1] * a.stat[2 * (size_t)t];
+    d += dp;
+  }
+  __shared__ float su[4][64], sd[4][64];
+  su[tl][f] = u;
+  sd[tl][f] = d;
+  __syncthreads();
+  if (tl == 0) {
+    atomicAdd(a.ud + f, su[0][f] + su[1][f] + su[2][f] + su[3][f]);
+    atomicAdd(a.ud + 64 + f, sd[0][f] + sd[1][f] + sd[2][f] + sd[3][f]);
+  }
+}
+
+// backward step 2: parameter gradients from M, u, db (one thread per obs dim k; d_be by the first 64 threads)
+__global__ __launch_bounds__(256) void obs_embed_bwd_fin_kernel(OEArgs a) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x < 64 && a.d_be) atomicAdd(a.d_be + threadIdx.x, a.ud[64 + threadIdx.x]);
+  if (k >= a.od) return;
+  const float gk = a.g[k], bk = a.b[k];
+  float dg = 0.f, dbo = 0.f;
+  for (int f = 0; f < 64; ++f) {
+    const float m = a.M[(size_t)f * a.od + k] - a.ud[f], db = a.ud[64 + f], w = a.we[(size_t)f * a.od + k];
+    if (a.d_we) atomicAdd(a.d_we + (size_t)f * a.od + k, gk * m + bk * db);
+    dg += w * m;
+    dbo += w * db;
+  }
+  if (a.d_g) atomicAdd(a.d_g + k, dg);
+  if (a.d_b) atomicAdd(a.d_b + k, dbo);
+}
+
+}  // namespace
+
+MDL_API int mdl_obs_embed_pack(const OEArgs* a, hipStream_t st) {
+  if (a->od < 1 || a->KS * 32 < a->od) return -1;
+  hipLaunchKernelGGL(obs_embed_pack_kernel, dim3(64), dim3(256), 0, st, *a);
+  MDL_CHECK_LAUNCH();
+  return 0;
+}
+
+MDL_API int mdl_obs_embed_fwd(const OEArgs* a, hipStream_t st) {
+  if (a->N <= 0) return 0;
+  hipLaunchKernelGGL(obs_embed_fwd_kernel, dim3((a->N + OE_TOK - 1) / OE_TOK), dim3(256), 0, st, *a);
+  MDL_CHECK_LAUNCH();
+  return 0;
+}
+
+MDL_API int mdl_obs_embed_bwd(const OEArgs* a, hipStream_t st) {
+  if (a->N <= 0) return 0;
+  hipMemsetAsync(a->M, 0, sizeof(float) * 64 * (size_t)a->od, st);
+  hipMemsetAsync(a->ud, 0, sizeof(float) * 128, st);
+  hipLaunchKernelGGL(obs_embed_bwd_m_kernel, dim3((a->od + 63) / 64, OEB_SPLIT), dim3(256), 0, st, *a);
+  MDL_CHECK_LAUNCH();
+  hipLaunchKernelGGL(obs_embed_bwd_u_kernel, dim3(256), dim3(256), 0, st, *a);
+  MDL_CHECK_LAUNCH();
+  hipLaunchKernelGGL(obs_embed_bwd_fin_kernel, dim3((a->od + 255) / 256), dim3(256), 0, st, *a);
+  MDL_CHECK_LAUNCH();
+  return 0;
+}

@@ -23,7 +23,7 @@ struct PPOArgs {
   const float* logp;      // (n)
   const float* ent;       // (n)
   const float* old_logp;  // (n)
-  const float* adv;       // (n)  (already normalised)
+  const float* adv;       // (n, n_obj)  (already normalised)
   const float* vpred;     // (n, n_obj) old value predictions
   const float* ret;       // (n, n_obj) returns
   const float* active;    // (n)
@@ -105,16 +105,20 @@ __global__ __launch_bounds__(256) void ppo_grad_kernel(PPOArgs a) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
     const float act = a.active[i];
     // policy: -min(r A, clip(r) A)
+    // multi-objective MAT (momat / dmomat): one advantage per objective, the surrogate summed over objectives
+    // (mat_trainer.py:129-139 on (B, A, n_obj) advantages: min(...).sum(-1))
     const float imp = __expf(a.logp[i] - a.old_logp[i]);
-    const float ad = a.adv[i];
-    const float s1 = imp * ad;
     const float ic = fminf(fmaxf(imp, 1.f - a.clip), 1.f + a.clip);
-    const float s2 = ic * ad;
     const float wp = a.use_pam ? act * inv_pa : inv_pa;
-    float dm;
-    if (s1 <= s2) dm = imp * ad;
-    else dm = (imp >= 1.f - a.clip && imp <= 1.f + a.clip) ? imp * ad : 0.f;  // clamp passes grad inclusively
-    pl -= fminf(s1, s2) * wp;
+    float dm = 0.f, sm_ = 0.f;
+    for (int o = 0; o < a.n_obj; ++o) {
+      const float ad = a.adv[(size_t)i * a.n_obj + o];
+      const float s1 = imp * ad, s2 = ic * ad;
+      if (s1 <= s2) dm += imp * ad;
+      else dm += (imp >= 1.f - a.clip && imp <= 1.f + a.clip) ? imp * ad : 0.f;  // clamp passes grad inclusively
+      sm_ += fminf(s1, s2);
+    }
+    pl -= sm_ * wp;
     a.dlogp[i] = -wp * dm;
     // entropy bonus
     a.dent[i] = -a.coef_e * wp;

@@ -77,6 +77,60 @@ sig("mdl_mat_enc_bwd_ct", ctypes.POINTER(EncP), VP, VP, ctypes.c_int, VP)
 sig("mdl_mat_dec_fwd_ct", ctypes.POINTER(DecP), ctypes.c_int, ctypes.c_int, VP)
 sig("mdl_mat_dec_bwd_ct", ctypes.POINTER(DecP), ctypes.c_int, VP)
 sig("mdl_grad_reduce", VP, VP, ctypes.c_int, ctypes.c_longlong, ctypes.c_int, VP)
+
+
+class OEArgs(ctypes.Structure):   # csrc/obs_embed.hip
+    _fields_ = [(n, ctypes.c_int) for n in ("N", "od", "KS")] + \
+               [(n, VP) for n in ("x", "we", "be", "g", "b", "wpack", "c01", "pre", "stat", "dpre", "M", "ud", "d_we",
+                                  "d_be", "d_g", "d_b")]
+
+
+sig("mdl_obs_embed_pack", ctypes.POINTER(OEArgs), VP)
+sig("mdl_obs_embed_fwd", ctypes.POINTER(OEArgs), VP)
+sig("mdl_obs_embed_bwd", ctypes.POINTER(OEArgs), VP)
+MAX_FUSED_OBS = 16      # obs_dim embedded inside the fused encoder; wider observations use csrc/obs_embed.hip
+
+
+class ObsEmbed:
+    """LN(obs_dim) -> Linear(obs_dim, 64) pre-activation on MFMA for wide observations (SMAC), with the LayerNorm
+    folded into the GEMM (csrc/obs_embed.hip); its W' pack is refreshed once per optimizer step."""
+
+    def __init__(self, model):
+        enc = model.encoder
+        self.model = model
+        self.ln, self.lin = enc.obs_encoder[0], enc.obs_encoder[1]
+        self.od = enc.obs_dim
+        self.KS = (self.od + 31) // 32
+        dev = self.lin.weight.device
+        self.wpack = torch.empty(self.KS * 4 * 64 * 8, dtype=torch.bfloat16, device=dev)
+        self.c01 = torch.empty(128, device=dev)
+        self.M = torch.empty(64 * self.od, device=dev)
+        self.ud = torch.empty(128, device=dev)
+        self.version = None
+
+    def _args(self, N=0, x=None, pre=None, stat=None, dpre=None):
+        return OEArgs(N=N, od=self.od, KS=self.KS, x=_ptr(x), we=self.lin.weight.data_ptr(), be=self.lin.bias.data_ptr(),
+                      g=self.ln.weight.data_ptr(), b=self.ln.bias.data_ptr(), wpack=self.wpack.data_ptr(),
+                      c01=self.c01.data_ptr(), pre=_ptr(pre), stat=_ptr(stat), dpre=_ptr(dpre), M=self.M.data_ptr(),
+                      ud=self.ud.data_ptr(), d_we=_gptr(self.lin.weight), d_be=_gptr(self.lin.bias),
+                      d_g=_gptr(self.ln.weight), d_b=_gptr(self.ln.bias))
+
+    def forward(self, obs2d):
+        ver = getattr(self.model, "_mdl_version", 0)
+        if ver != self.version:
+            a = self._args()
+            check(lib().mdl_obs_embed_pack(ctypes.byref(a), kernels._stream()), "obs_embed_pack")
+            self.version = ver
+        N = obs2d.shape[0]
+        pre = torch.empty(N, 64, device=obs2d.device)
+        stat = torch.empty(N, 2, device=obs2d.device)
+        a = self._args(N, obs2d, pre, stat)
+        check(lib().mdl_obs_embed_fwd(ctypes.byref(a), kernels._stream()), "obs_embed_fwd")
+        return pre, stat
+
+    def backward(self, obs2d, stat, dpre):
+        a = self._args(obs2d.shape[0], obs2d, None, stat, dpre)
+        check(lib().mdl_obs_embed_bwd(ctypes.byref(a), kernels._stream()), "obs_embed_bwd")
 sig("mdl_pack_weights", VP, ctypes.c_int, VP)
 
 MAX_ACTION_DIM = 64 if TRAIN_KERNELS == "ct" else 8
@@ -200,8 +254,8 @@ def encoder_unsupported_reasons(model):
     r = _common_reasons(model)
     if enc.encode_state:
         r.append("encode_state")
-    if enc.obs_dim > 16:
-        r.append(f"obs_dim {enc.obs_dim} > 16")
+    if enc.obs_dim > MAX_FUSED_OBS and TRAIN_KERNELS != "ct":
+        r.append(f"obs_dim {enc.obs_dim} > {MAX_FUSED_OBS} (round-1 kernels)")
     if model.n_objective > 2:
         r.append(f"n_objective {model.n_objective} > 2")
     return r
@@ -274,6 +328,11 @@ class EncoderFused:
         SQ, NRP, sfx = geometry(L)
         n_tok = B * L
         obs = obs.float().contiguous()
+        pre = stat = None
+        if od > MAX_FUSED_OBS:   # wide observations: embedding pre-activation from the obs-embedding kernel
+            if getattr(self, "emb", None) is None:
+                self.emb = ObsEmbed(m)
+            pre, stat = self.emb.forward(obs.view(n_tok, od))
         rep = torch.empty(B, L, 64, device=dev)
         v = torch.empty(B, L, m.n_objective, device=dev)
         p = self.p
@@ -287,13 +346,13 @@ class EncoderFused:
                 saves += [t, lse]
                 p.sv[bi] = Sv(t[0].data_ptr(), t[1].data_ptr(), lse.data_ptr(), t[2].data_ptr(), None, None, None,
                               t[3].data_ptr())
-        check(_enc_fwd(sfx, p, None, m.n_block, save), "mat_enc_fwd")
-        self.ctx = (obs, rep, v, saves, [Sv.from_buffer_copy(p.sv[i]) for i in range(m.n_block)])
+        check(_enc_fwd(sfx, p, _ptr(pre), m.n_block, save), "mat_enc_fwd")
+        self.ctx = (obs, rep, v, saves, [Sv.from_buffer_copy(p.sv[i]) for i in range(m.n_block)], pre, stat)
         return v, rep
 
     def backward(self, drep, dv):
         m = self.model
-        obs, rep, v, saves, svs = self.ctx
+        obs, rep, v, saves, svs, pre, stat = self.ctx
         self._build()
         p = self.p
         drep = drep.float().contiguous()
@@ -307,7 +366,10 @@ class EncoderFused:
         p.g_delta, p.g_stride, p.g_copies = m._mdl_gws if getattr(m, "_mdl_gws_active", False) else (0, 0, 0)
         if p.g_copies:
             check_grad_ptrs(p, m._mdl_gws_buf[1])
-        check(_enc_bwd(sfx, p, None, None, m.n_block), "mat_enc_bwd")
+        dpre = torch.empty_like(pre) if pre is not None else None
+        check(_enc_bwd(sfx, p, _ptr(pre), _ptr(dpre), m.n_block), "mat_enc_bwd")
+        if pre is not None:
+            self.emb.backward(obs.view(-1, od), stat, dpre)
         b = m.encoder.head[3].bias
         if b.grad is not None:
             b.grad.add_(dv.reshape(-1, dv.shape[-1]).sum(0))

@@ -17,8 +17,8 @@ def train_unsupported_reasons(model) -> list:
     """Why the fused training step (fused fwd/bwd + PPO loss + Adam) cannot run this model, device aside."""
     from . import mat_train
     r = mat_train.encoder_unsupported_reasons(model) + mat_train.decoder_unsupported_reasons(model)
-    if getattr(model, "n_objective", 1) != 1:
-        r.append(f"n_objective {model.n_objective} (fused PPO loss is single-objective)")
+    if getattr(model, "n_objective", 1) > 2:
+        r.append(f"n_objective {model.n_objective} > 2")
     return list(dict.fromkeys(r))
 
 

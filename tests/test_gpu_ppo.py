@@ -85,14 +85,17 @@ def test_flat_adam_matches_torch_adam_with_clipping(gpu):
         assert torch.allclose(flat_p, p_ref.detach(), atol=1e-6, rtol=1e-5), (flat_p - p_ref).abs().max()
 
 
-def test_fused_trainer_step_matches_autograd_step(gpu):
-    """One PPO minibatch: fused loss + FlatAdam vs autograd loss + torch Adam (same fused fwd/bwd kernels)."""
+@pytest.mark.parametrize("n_obj", [1, 2])
+def test_fused_trainer_step_matches_autograd_step(gpu, n_obj):
+    """One PPO minibatch: fused loss + FlatAdam vs autograd loss + torch Adam (same fused fwd/bwd kernels); n_obj = 2
+    is the multi-objective MAT (vector value head, per-objective ValueNorm and advantages)."""
     from mat_dcml_amd.algos.mat_trainer import MATTrainer
     from mat_dcml_amd.algos.policy import TransformerPolicy
     from mat_dcml_amd.config import get_config, parse_args
     from mat_dcml_amd.envs.dcml.spaces import dcml_action_spaces
     from mat_dcml_amd.parallel.comm import Comm
-    args = parse_args(["--n_workers", "8", "--lr", "5e-4", "--use_valuenorm", "--use_value_active_masks"],
+    args = parse_args(["--n_workers", "8", "--lr", "5e-4", "--use_valuenorm", "--use_value_active_masks",
+                       "--n_objective", str(n_obj)] + (["--algorithm_name", "momat"] if n_obj == 2 else []),
                       get_config(), warn=False)
     res = []
     g = torch.Generator(device=gpu).manual_seed(3)
@@ -113,7 +116,7 @@ def test_fused_trainer_step_matches_autograd_step(gpu):
             pol.optimizer = torch.optim.Adam(pol.transformer.parameters(), lr=5e-4, eps=1e-5)
         with torch.no_grad():
             v0, lp0, _ = pol.evaluate_actions(None, obs, actions, ava)
-        mb = {"obs": obs, "actions": actions, "ava": ava, "old_logp": lp0 + 0.05, "adv": torch.randn(B, A, 1, device=gpu, generator=torch.Generator(device=gpu).manual_seed(5)),
+        mb = {"obs": obs, "actions": actions, "ava": ava, "old_logp": lp0 + 0.05, "adv": torch.randn(B, A, n_obj, device=gpu, generator=torch.Generator(device=gpu).manual_seed(5)),
               "value_preds": v0, "returns": v0 + 1.0, "active": torch.ones(B, A, 1, device=gpu)}
         before = [p.detach().clone() for p in pol.transformer.parameters()]
         if fused:

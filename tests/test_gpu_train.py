@@ -120,3 +120,61 @@ def test_full_mat_fused_grads(gpu, L, B):
             bad.append((n, round(e, 4), round(rel(refb[n], r), 4)))
         print(f"{n:45s} err {e:.4f} yardstick {rel(refb[n], r):.4f} |ref| {r.norm().item():.4e}")
     assert not bad, bad
+
+
+def make_discrete(L, A, od, dev, seed=0, scale=0.2):
+    torch.manual_seed(seed)
+    m = MultiAgentTransformer(L, od, A, L, 2, 64, 2, action_type="Discrete").to(dev)
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if "ln" in n or "head.2" in n or "obs_encoder.0" in n:
+                p.copy_((1.0 + 0.1 * torch.randn(p.shape, generator=g)).to(dev) if n.endswith("weight")
+                        else (0.1 * torch.randn(p.shape, generator=g)).to(dev))
+            else:
+                p.copy_((torch.randn(p.shape, generator=g) * scale / (1.0 if p.shape[-1] < 100 else 4.0)).to(dev))
+    return m
+
+
+@pytest.mark.parametrize("L,B,A,od", [(27, 24, 36, 1288), (10, 30, 12, 40)])
+def test_full_mat_fused_grads_wide_obs_discrete(gpu, L, B, A, od):
+    """SMAC shape (27m_vs_30m: 27 agents, obs 1288 through the obs-embedding kernels, Discrete(36) heads on the MFMA
+    head path) — every parameter gradient vs fp32 autograd with the bf16-autocast yardstick."""
+    m = make_discrete(L, A, od, gpu, seed=4)
+    g = torch.Generator(device=gpu).manual_seed(6)
+    obs = torch.rand(B, L, od, device=gpu, generator=g) * (torch.rand(B, L, od, device=gpu, generator=g) < 0.3)
+    ava = (torch.rand(B, L, A, device=gpu, generator=g) < 0.7).float()
+    ava[..., 0] = 1
+    probs = ava / ava.sum(-1, keepdim=True)
+    actions = torch.multinomial(probs.view(-1, A), 1, generator=g).view(B, L, 1).float()
+    w1, w2, w3 = (torch.randn(B, L, 1, device=gpu, generator=g) for _ in range(3))
+    m.zero_grad()
+    lp_r, v_r, ent_r = m(None, obs, actions, ava)
+    ((lp_r * w1).sum() + (v_r * w2).sum() + (ent_r * w3).sum()).backward()
+    ref = {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
+    m.zero_grad()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        lp_b, v_b, ent_b = m(None, obs, actions, ava)
+        ((lp_b.float() * w1).sum() + (v_b.float() * w2).sum() + (ent_b.float() * w3).sum()).backward()
+    refb = {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
+    for p_ in m.parameters():
+        p_.grad = torch.zeros_like(p_)
+    tol = lambda a, b: max(3e-2, 2.5 * rel(a.float(), b))  # noqa: E731
+    v_k, lp_k, ent_k = mat_train.evaluate_actions(m, obs, actions, ava)
+    assert rel(lp_k, lp_r) < tol(lp_b, lp_r), (rel(lp_k, lp_r), rel(lp_b.float(), lp_r))
+    assert rel(v_k, v_r) < tol(v_b, v_r) and rel(ent_k, ent_r) < tol(ent_b, ent_r)
+    ((lp_k * w1).sum() + (v_k * w2).sum() + (ent_k * w3).sum()).backward()
+    torch.cuda.synchronize()
+    bad = []
+    params = dict(m.named_parameters())
+    for n, r in ref.items():
+        gg = params[n].grad
+        if "key.bias" in n:
+            e = (gg - r).abs().max().item() / (ref[n.replace("key.bias", "key.weight")].abs().max().item() + 1e-6)
+            lim = 8e-2
+        else:
+            e = rel(gg, r)
+            lim = max(6e-2, 2.5 * rel(refb[n], r))
+        if e > lim:
+            bad.append((n, round(e, 4), round(rel(refb[n], r), 4)))
+    assert not bad, bad

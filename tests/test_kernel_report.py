@@ -29,7 +29,6 @@ def test_dcml_config_takes_every_hip_path():
     assert g == {"encoder": [], "decode": [], "train": []}, g
 
 
-@pytest.mark.xfail(strict=True, reason="obs_dim 1288 embedding kernel not wired yet")
 def test_smac_config_gates():
     _need_lib()
     from mat_dcml_amd.envs.smac.synthetic import SyntheticSMACEnv
@@ -42,7 +41,6 @@ def test_smac_config_gates():
     assert g["train"] == [], g
 
 
-@pytest.mark.xfail(strict=True, reason="vector value head in the fused PPO loss not wired yet")
 def test_momat_config_gates():
     _need_lib()
     from mat_dcml_amd.ops.paths import gate_reasons
