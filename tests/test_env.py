@@ -122,3 +122,70 @@ def test_shannon_links():
     ref.reset()
     _, _, _, _, d_ref, _, _ = ref.step(act)
     assert float(delay.mean()) <= float(d_ref.mean()) + 1e-6
+
+
+# ------------------------------------------------------------------------------------------ policy-driven parity
+def _policy_actions(rng, ava, policy):
+    """(A, 1) action vector for one env from the availability rows (ava[:, 1] = worker available)."""
+    W = ava.shape[0] - 1
+    av = ava[:W, 1] > 0
+    if policy == "bernoulli":
+        sel = (rng.random(W) < 0.5) & av
+        ratio = rng.random()
+    elif policy == "all_half":
+        sel, ratio = av.copy(), 0.5
+    else:   # "none": N == 0 -> the standalone branch
+        sel, ratio = np.zeros(W, dtype=bool), rng.random()
+    return np.concatenate([sel.astype(np.float64), [ratio]]).reshape(-1, 1)
+
+
+def _ref_policy_run(tmp_path, policy, n_steps):
+    ro.install_stubs()
+    import random
+    random.seed(21)
+    np.random.seed(21)
+    rng = np.random.default_rng(7)
+    with ro.ref_cwd(tmp_path):
+        from DCML_BID_FIRST_MA_ENV_SingleProcess import Env
+        env = Env()
+        _, _, ava = env.reset()
+        d, p, r = [], [], []
+        for _ in range(n_steps):
+            _, _, rew, _, info, ava = env.step(_policy_actions(rng, np.asarray(ava), policy))
+            d.append(info[0]["delay"])
+            p.append(info[0]["payment"])
+            r.append(float(np.asarray(rew).reshape(-1)[0]))
+    return np.array(d), np.array(p), np.array(r)
+
+
+def _our_policy_run(policy, n_steps, envs=64, W=100):
+    env = DeviceDCMLEnv(envs, DCMLConfig(n_workers=W), seed=9)
+    _, _, ava = env.reset()
+    rng = np.random.default_rng(8)
+    d, p, r = [], [], []
+    for _ in range(n_steps):
+        a = np.stack([_policy_actions(rng, ava[e].numpy(), policy)[:, 0] for e in range(envs)])
+        _, _, rew, _, delay, pay, ava = env.step(torch.from_numpy(a).float())
+        d.append(delay.numpy())
+        p.append(pay.numpy())
+        r.append(rew.numpy())
+    return (np.concatenate(d).astype(np.float64), np.concatenate(p).astype(np.float64),
+            np.concatenate(r).astype(np.float64))
+
+
+@pytest.mark.skipif(not ro.available(), reason="reference not mounted")
+@pytest.mark.parametrize("policy", ["bernoulli", "all_half", "none"])
+def test_policy_driven_distribution_matches_reference(tmp_path, policy):
+    """parity under policy-driven selections at 100 workers — random Bernoulli selections with a
+    U(0, 1) ratio (K = ceil(N ratio), clamps), every available worker at ratio 0.5, and N = 0 (the standalone
+    worker-0 branch with its 1.5x reward penalty): delay, payment and reward distributions (KS) and means."""
+    from scipy.stats import ks_2samp
+    rd, rp, rr = _ref_policy_run(tmp_path, policy, 6000)
+    od, op, orr = _our_policy_run(policy, 150)
+    for name, a, b in (("delay", rd, od), ("payment", rp, op), ("reward", rr, orr)):
+        pv = ks_2samp(a, b).pvalue
+        gap = abs(a.mean() - b.mean()) / abs(a.mean())
+        # delays are heavy-tailed (Bernoulli p90 ~ 6x the median): at 6000 reference samples a 5 % mean gap is only
+        # ~2 standard errors, so a larger gap must also be statistically significant (|z| >= 3) to fail
+        z = abs(a.mean() - b.mean()) / np.sqrt(a.var() / len(a) + b.var() / len(b))
+        assert pv > 1e-3 and (gap < 0.05 or z < 3.0), (policy, name, pv, gap, z, a.mean(), b.mean())
