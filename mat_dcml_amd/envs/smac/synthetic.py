@@ -122,7 +122,7 @@ class SyntheticSMACEnv:
         step = dirs[(a - 2).clamp(0, 3)] * MOVE * mv.unsqueeze(-1)
         self.apos = (self.apos + step).clamp(0.0, MAP_SIZE)
         # ally attacks
-        d_ae = torch.cdist(self.apos, self.epos)                                   # (E, A, N)
+        d_ae = (self.apos[:, :, None] - self.epos[:, None]).norm(dim=-1)           # (E, A, N) (no GEMM path)
         tgt = (a - N_NO_ATTACK).clamp(0, N - 1)
         att = (a >= N_NO_ATTACK) & alive
         in_rng = torch.gather(d_ae, 2, tgt.unsqueeze(-1)).squeeze(-1) <= SHOOT
