@@ -18,13 +18,28 @@ __device__ __forceinline__ int dec_token_ct(const DecP& p, int tok, int i) {
   return 1 + a;
 }
 
-// x0 pre-activation = W_a · onehot(token) — a column gather of W_a [64][A+1]
+// x0 pre-activation = W_a · onehot(token) — a column gather of W_a [64][A+1]; continuous action type:
+// W_a · a_prev + b_a with a_prev the previous agent's action vector (zero for row 0)
 __device__ __forceinline__ CT dec_embed_pre_ct(const DecP& p, int rt, int& tokid, const Ctx& c) {
   const int lane = c.lane, g = lane >> 4;
   const int row = rt * 16 + (lane & 15);
   const bool ok = row < c.NR;
-  tokid = ok ? dec_token_ct(p, c.tok0 + row, row % c.L) : 0;
   CT pre;
+  if (p.cont) {
+    tokid = -1;
+    const bool first = !ok || row % c.L == 0;
+    const float* prev = p.act + (size_t)(c.tok0 + (first ? 0 : row - 1)) * p.A;
+    pre = ld_vec(p.ba, lane);
+    for (int k = 0; k < p.A; ++k) {
+      const float x = first ? 0.f : prev[k];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pre.v[mt][r] += p.wa[(16 * mt + 4 * g + r) * p.A + k] * x;
+    }
+    return pre;
+  }
+  tokid = ok ? dec_token_ct(p, c.tok0 + row, row % c.L) : 0;
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
@@ -324,8 +339,8 @@ __device__ __forceinline__ void head_fwd_ct(const DecP& p, const CT* xr, bool sa
       const int row = rt * 16 + (lane & 15);
       const bool ok = row < c.NR;
       const size_t tok = (size_t)(c.tok0 + (ok ? row : 0));
-      const unsigned am = slot_mask<MA>(p, tok, lane);
-      const float actf = p.act[tok];
+      const unsigned am = p.cont ? 0u : slot_mask<MA>(p, tok, lane);
+      const float actf = p.cont ? 0.f : p.act[tok];
       const CTr x = ct_pack(xr[k]);
       if (save) st_g(p.sv_head, c.tok0, rt, c.NR, x, lane);
       CT hh = bh, xh, n;
@@ -334,6 +349,20 @@ __device__ __forceinline__ void head_fwd_ct(const DecP& p, const CT* xr, bool sa
       ln_fwd_ct(hh, xh, n, gam, bet);
       f32x4 L[MA];
       head_logits_ct<MA>(p, W, n, L, lane);
+      if (p.cont) {   // per-dimension Normal(mean, std): this lane's dims a = 16ma + 4g + r
+#pragma unroll
+        for (int ma = 0; ma < MA; ++ma)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int a = 16 * ma + 4 * g + r;
+            if (ok && a < p.A) {
+              const float sd = p.stdv[a], z = (p.act[tok * p.A + a] - L[ma][r]) / sd;
+              p.logp[tok * p.A + a] = -0.5f * z * z - __logf(sd) - HALF_LOG_2PI;
+              p.ent[tok * p.A + a] = 0.5f + HALF_LOG_2PI + __logf(sd);
+            }
+          }
+        continue;
+      }
       const bool disc = (row % c.L) < p.n_disc;
       const int act = min(max((int)actf, 0), p.A - 1);
       const HeadStat st = head_stats<MA>(p, L, am, act, disc, lane);
@@ -362,6 +391,9 @@ __device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c)
   ct_zero(dlg);
   ct_zero(dlb);
   float dls = 0.f;
+  f32x4 dlsv[MA];   // continuous: per-dimension log_std partials of this lane's slots
+#pragma unroll
+  for (int ma = 0; ma < MA; ++ma) dlsv[ma] = f32x4{0.f, 0.f, 0.f, 0.f};
   {
     HeadW<MA> W;
     head_w<MA>(p, W, lane);
@@ -391,9 +423,9 @@ __device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c)
         const int row = rt * 16 + (lane & 15);
         const bool ok = row < c.NR;
         const size_t tok = (size_t)(c.tok0 + (ok ? row : 0));
-        const unsigned am = slot_mask<MA>(p, tok, lane);
-        const float actf = p.act[tok];
-        const float dlp = ok ? p.dlogp[tok] : 0.f, den = ok ? p.dent[tok] : 0.f;
+        const unsigned am = p.cont ? 0u : slot_mask<MA>(p, tok, lane);
+        const float actf = p.cont ? 0.f : p.act[tok];
+        const float dlp = (ok && !p.cont) ? p.dlogp[tok] : 0.f, den = (ok && !p.cont) ? p.dent[tok] : 0.f;
         const CTr x = ld_g(p.sv_head, c.tok0, rt, c.NR, lane);
         CT hh = bh;
         mm(hh, Hf, x);
@@ -402,14 +434,29 @@ __device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c)
         const float rs = ln_fwd_ct(gl, xh, n, gam, bet);
         f32x4 L[MA];
         head_logits_ct<MA>(p, W, n, L, lane);
-        const bool disc = (row % c.L) < p.n_disc;
+        const bool disc = !p.cont && (row % c.L) < p.n_disc;
         const int act = min(max((int)actf, 0), p.A - 1);
-        const HeadStat st = head_stats<MA>(p, L, am, act, disc, lane);
+        const HeadStat st = p.cont ? HeadStat{0.f, 0.f, 0.f, 0.f} : head_stats<MA>(p, L, am, act, disc, lane);
         // d loss / d logits of this lane's slots
         f32x4 Z[2 * SB];
 #pragma unroll
         for (int ma = 0; ma < 2 * SB; ++ma) Z[ma] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (disc) {
+        if (p.cont) {   // per-dimension Normal heads: d log p / d mean, and the log_std partials of this lane's dims
+#pragma unroll
+          for (int ma = 0; ma < MA; ++ma)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int a = 16 * ma + 4 * g + r;
+              if (ok && a < p.A) {
+                const float sd = p.stdv[a], diff = p.act[tok * p.A + a] - L[ma][r];
+                const float dl = p.dlogp[tok * p.A + a], de = p.dent[tok * p.A + a];
+                Z[ma][r] = dl * diff / (sd * sd);
+                const float dsd = dl * (diff * diff / (sd * sd * sd) - 1.f / sd) + de / sd;
+                const float sg = 1.f / (1.f + __expf(-p.log_std[a]));
+                dlsv[ma][r] += dsd * 0.5f * sg * (1.f - sg);
+              }
+            }
+        } else if (disc) {
 #pragma unroll
           for (int ma = 0; ma < MA; ++ma)
 #pragma unroll
@@ -468,7 +515,16 @@ __device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c)
   }
   flush_vec(dlg, c.g(p.lnh.dg), lane);
   flush_vec(dlb, c.g(p.lnh.db), lane);
-  {
+  if (p.cont) {
+#pragma unroll
+    for (int ma = 0; ma < MA; ++ma)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float t = group_sum<16>(dlsv[ma][r]);
+        const int a = 16 * ma + 4 * g + r;
+        if ((lane & 15) == 0 && a < p.A && p.d_log_std) atomicAdd(c.g(p.d_log_std) + a, t);
+      }
+  } else {
     const float t = wave_sum(dls);
     if (lane == 0 && p.d_log_std && p.n_disc < p.L) atomicAdd(c.g(p.d_log_std) + (p.A - 1), t);
   }
@@ -566,7 +622,21 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
         gelu_ct(e);
         const float rs = ln_fwd_ct(e, xh, yy, gam, bet);
         ln_bwd_ct(dx[k], xh, rs, gam, ok, de, dlg, dlb);
-        if (ok) {
+        if (ok && p.cont) {   // EMB[k][f] += d pre_f * a_prev_k (k < A), EMB[A][f] += d pre_f (bias)
+          const int row = rt * 16 + (lane & 15);
+          const bool first = row % c.L == 0;
+          const float* prev = p.act + (size_t)(c.tok0 + (first ? 0 : row - 1)) * p.A;
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float dp = de.v[mt][r] * gelu_erf_grad(pre.v[mt][r]);
+              const int f = 16 * mt + 4 * g + r;
+              atomicAdd(EMB + p.A * 64 + f, dp);
+              if (!first)
+                for (int kk = 0; kk < p.A; ++kk) atomicAdd(EMB + kk * 64 + f, dp * prev[kk]);
+            }
+        } else if (ok) {
 #pragma unroll
           for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
@@ -578,7 +648,13 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
     flush_vec(dlg, c.g(p.d_lnd_g), lane);
     flush_vec(dlb, c.g(p.d_lnd_b), lane);
     __syncthreads();
-    if (p.d_wa)
+    if (p.cont) {   // W_a [64][A] and b_a
+      for (int i = c.tid; i < (p.A + 1) * 64; i += 256) {
+        const int t = i / 64, col = i % 64;
+        if (t < p.A) { if (p.d_wa) atomicAdd(c.g(p.d_wa) + col * p.A + t, EMB[i]); }
+        else if (p.d_ba) atomicAdd(c.g(p.d_ba) + col, EMB[i]);
+      }
+    } else if (p.d_wa)
       for (int i = c.tid; i < (p.A + 1) * 64; i += 256) {
         const int t = i / 64, col = i % 64;
         atomicAdd(c.g(p.d_wa) + col * (p.A + 1) + t, EMB[i]);

@@ -106,6 +106,11 @@ struct DecP {
   bf16_t* sv_head;       // [tok][64] head input (last block output)
   long long g_delta, g_stride;
   int g_copies;
+  // continuous action type (MA-MuJoCo, transformer_act.py:192-232): act / logp / ent / dlogp / dent are
+  // [tok][A], the action embedding is Linear(A, 64) with bias (wa = [64][A], ba = [64]) on the previous agent's action
+  int cont;
+  const float* ba;
+  float* d_ba;
 };
 
 struct Ctx {

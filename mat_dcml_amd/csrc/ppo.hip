@@ -34,6 +34,7 @@ struct PPOArgs {
   float* vn;        // ValueNorm: running_mean[n_obj], running_mean_sq[n_obj], debiasing_term
   float clip, coef_v, coef_e, huber_delta, beta, eps, omb;   // omb = 1 - beta computed in double on the host
   int use_huber, use_clip_v, use_vam, use_pam, use_vn, update_vn;
+  int n_lp;         // log-prob / entropy entries per token (continuous action type: one per action dimension)
 };
 
 #define MAXOBJ 2
@@ -107,23 +108,29 @@ __global__ __launch_bounds__(256) void ppo_grad_kernel(PPOArgs a) {
     // policy: -min(r A, clip(r) A)
     // multi-objective MAT (momat / dmomat): one advantage per objective, the surrogate summed over objectives
     // (mat_trainer.py:129-139 on (B, A, n_obj) advantages: min(...).sum(-1))
-    const float imp = __expf(a.logp[i] - a.old_logp[i]);
-    const float ic = fminf(fmaxf(imp, 1.f - a.clip), 1.f + a.clip);
+    // continuous action type: one ratio per action dimension, the surrogate summed over dimensions; the entropy is
+    // the mean over every (token, dimension) entry (transformer_policy.py:212-215 with (B, L, A) entropies)
     const float wp = a.use_pam ? act * inv_pa : inv_pa;
-    float dm = 0.f, sm_ = 0.f;
-    for (int o = 0; o < a.n_obj; ++o) {
-      const float ad = a.adv[(size_t)i * a.n_obj + o];
-      const float s1 = imp * ad, s2 = ic * ad;
-      if (s1 <= s2) dm += imp * ad;
-      else dm += (imp >= 1.f - a.clip && imp <= 1.f + a.clip) ? imp * ad : 0.f;  // clamp passes grad inclusively
-      sm_ += fminf(s1, s2);
+    const float inv_lp = 1.f / (float)a.n_lp;
+    for (int k = 0; k < a.n_lp; ++k) {
+      const size_t q = (size_t)i * a.n_lp + k;
+      const float imp = __expf(a.logp[q] - a.old_logp[q]);
+      const float ic = fminf(fmaxf(imp, 1.f - a.clip), 1.f + a.clip);
+      float dm = 0.f, sm_ = 0.f;
+      for (int o = 0; o < a.n_obj; ++o) {
+        const float ad = a.adv[(size_t)i * a.n_obj + o];
+        const float s1 = imp * ad, s2 = ic * ad;
+        if (s1 <= s2) dm += imp * ad;
+        else dm += (imp >= 1.f - a.clip && imp <= 1.f + a.clip) ? imp * ad : 0.f;  // clamp passes grad inclusively
+        sm_ += fminf(s1, s2);
+      }
+      pl -= sm_ * wp;
+      a.dlogp[q] = -wp * dm;
+      // entropy bonus
+      a.dent[q] = -a.coef_e * wp * inv_lp;
+      el += a.ent[q] * wp * inv_lp;
+      rl += imp * inv_lp;
     }
-    pl -= sm_ * wp;
-    a.dlogp[i] = -wp * dm;
-    // entropy bonus
-    a.dent[i] = -a.coef_e * wp;
-    el += a.ent[i] * wp;
-    rl += imp;
     // value
     const float wv = a.use_vam ? act * inv_va : inv_va;
     for (int o = 0; o < a.n_obj; ++o) {

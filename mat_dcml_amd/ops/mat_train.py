@@ -53,7 +53,8 @@ class DecP(ctypes.Structure):
                [(n, VP) for n in ("wh2", "bh2", "d_wh2", "d_bh2", "stdv", "log_std", "d_log_std", "rep", "logp",
                                   "ent")] + \
                [("sv", Sv * 3)] + [(n, VP) for n in ("dlogp", "dent", "drep", "sv_head")] + \
-               [("g_delta", ctypes.c_longlong), ("g_stride", ctypes.c_longlong), ("g_copies", ctypes.c_int)]
+               [("g_delta", ctypes.c_longlong), ("g_stride", ctypes.c_longlong), ("g_copies", ctypes.c_int)] + \
+               [("cont", ctypes.c_int), ("ba", VP), ("d_ba", VP)]
 
 
 # builds of the training kernels, by name suffix (csrc/mat_train_common.h MDL_VARIANT_SUFFIX).  Only the base build
@@ -266,7 +267,8 @@ def decoder_unsupported_reasons(model):
     r = _common_reasons(model)
     if dec.dec_actor:
         r.append("dec_actor")
-    if model.action_type not in ("Semi_Discrete", "Discrete"):
+    ok_types = ("Semi_Discrete", "Discrete") + (("Continuous", "Continous") if TRAIN_KERNELS == "ct" else ())
+    if model.action_type not in ok_types:
         r.append(f"action_type {model.action_type}")
     if model.action_dim > MAX_ACTION_DIM:
         r.append(f"action_dim {model.action_dim} > {MAX_ACTION_DIM}")
@@ -391,6 +393,9 @@ class DecoderFused:
         dec = m.decoder
         p = DecP()
         p.wa, p.d_wa = dec.action_encoder[0].weight.data_ptr(), _gptr(dec.action_encoder[0].weight)
+        self.cont = m.action_type in ("Continuous", "Continous")
+        if self.cont:   # Linear(A, 64) with bias on the previous agent's action vector
+            p.cont, p.ba, p.d_ba = 1, dec.action_encoder[0].bias.data_ptr(), _gptr(dec.action_encoder[0].bias)
         p.lnd_g, p.lnd_b, p.d_lnd_g, p.d_lnd_b = dec.ln.weight.data_ptr(), dec.ln.bias.data_ptr(), \
             _gptr(dec.ln.weight), _gptr(dec.ln.bias)
         for bi, blk in enumerate(dec.blocks):
@@ -415,7 +420,11 @@ class DecoderFused:
 
     def _n_disc(self, L):
         m = self.model
-        return L if m.action_type == "Discrete" else L + m.semi_index
+        if m.action_type == "Discrete":
+            return L
+        if m.action_type in ("Continuous", "Continous"):
+            return 0
+        return L + m.semi_index
 
     def _geom(self, B, L):
         SQ, NRP, sfx = geometry(L)
@@ -434,10 +443,11 @@ class DecoderFused:
         dev = rep.device
         n_tok = B * L
         rep = rep.float().contiguous()
-        act = actions.reshape(B, L).float().contiguous()
-        ava_c = ava.float().contiguous() if ava is not None else None
-        logp = torch.empty(B, L, 1, device=dev)
-        ent = torch.empty(B, L, 1, device=dev)
+        nlp = m.action_dim if self.cont else 1   # continuous: per-dimension actions / log-probs / entropies
+        act = actions.reshape(B, L, nlp).float().contiguous()
+        ava_c = ava.float().contiguous() if (ava is not None and not self.cont) else None
+        logp = torch.empty(B, L, nlp, device=dev)
+        ent = torch.empty(B, L, nlp, device=dev)
         sfx = self._geom(B, L)
         p = self.p
         p.act, p.ava, p.rep, p.logp, p.ent = act.data_ptr(), _ptr(ava_c), rep.data_ptr(), logp.data_ptr(), ent.data_ptr()
@@ -461,7 +471,7 @@ class DecoderFused:
         m = self.model
         rep, act, ava_c, logp, ent, saves, svs, head = self.ctx
         self._build()
-        B, L = act.shape
+        B, L = act.shape[:2]
         sfx = self._geom(B, L)
         p = self.p
         dlogp = dlogp.reshape(-1).float().contiguous()

@@ -28,7 +28,8 @@ class PPOArgs(ctypes.Structure):
                [(k, vp) for k in ("v", "logp", "ent", "old_logp", "adv", "vpred", "ret", "active", "dv", "dlogp",
                                   "dent", "stats", "out", "vn")] + \
                [(k, ctypes.c_float) for k in ("clip", "coef_v", "coef_e", "huber_delta", "beta", "eps", "omb")] + \
-               [(k, ctypes.c_int) for k in ("use_huber", "use_clip_v", "use_vam", "use_pam", "use_vn", "update_vn")]
+               [(k, ctypes.c_int) for k in ("use_huber", "use_clip_v", "use_vam", "use_pam", "use_vn", "update_vn",
+                                            "n_lp")]
 
 
 class AdamArgs(ctypes.Structure):
@@ -200,9 +201,10 @@ class PPOLossFused:
         ``self.out`` = [policy, value, entropy, ratio] (caller zeroes it per log window)."""
         tr = self.tr
         n_obj = values.shape[-1]
-        N = logp.numel()
+        N = values.numel() // n_obj           # tokens
+        n_lp = logp.numel() // N              # log-prob entries per token (continuous: action dims)
         dev = values.device
-        if self._g is None or self._g[0].shape != values.shape or self._g[1].numel() != N:
+        if self._g is None or self._g[0].shape != values.shape or self._g[1].shape != logp.shape:
             self._g = (torch.empty_like(values), torch.empty_like(logp), torch.empty_like(ent))
         dv, dlp, dent = self._g
         vnm = tr.value_normalizer
@@ -218,7 +220,7 @@ class PPOLossFused:
                     omb=(1.0 - vnm.beta) if vnm is not None else 0.0, use_huber=int(tr._use_huber_loss),
                     use_clip_v=int(tr._use_clipped_value_loss), use_vam=int(tr._use_value_active_masks),
                     use_pam=int(tr._use_policy_active_masks), use_vn=int(vnm is not None),
-                    update_vn=int(vnm is not None))
+                    update_vn=int(vnm is not None), n_lp=n_lp)
         if pre_stats is not None:   # statistics of this minibatch precomputed (and all-reduced) for the epoch
             assert pre_stats.dtype == torch.float32 and pre_stats.numel() == 2 * n_obj + 2 and pre_stats.is_contiguous()
             check(lib().mdl_ppo_finish(ctypes.byref(a), _stream()), "ppo_finish")

@@ -178,3 +178,75 @@ def test_full_mat_fused_grads_wide_obs_discrete(gpu, L, B, A, od):
         if e > lim:
             bad.append((n, round(e, 4), round(rel(refb[n], r), 4)))
     assert not bad, bad
+
+
+@pytest.mark.parametrize("L,B,A", [(6, 50, 3), (17, 20, 1)])
+def test_full_mat_fused_grads_continuous(gpu, L, B, A):
+    """MA-MuJoCo shape (Continuous action type, transformer_act.py:192-232): per-dimension Normal log-probs /
+    entropies, the continuous action embedding Linear(A, 64) and log_std — every parameter gradient vs fp32 autograd."""
+    torch.manual_seed(3)
+    od = 11
+    m = MultiAgentTransformer(L, od, A, L, 2, 64, 2, action_type="Continuous").to(gpu)
+    g0 = torch.Generator().manual_seed(3)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if "ln" in n or "head.2" in n or "obs_encoder.0" in n:
+                p.copy_((1.0 + 0.1 * torch.randn(p.shape, generator=g0)).to(gpu) if n.endswith("weight")
+                        else (0.1 * torch.randn(p.shape, generator=g0)).to(gpu))
+            elif n.endswith("log_std"):
+                p.copy_((0.3 * torch.randn(p.shape, generator=g0)).to(gpu))
+            else:
+                p.copy_((torch.randn(p.shape, generator=g0) * 0.2).to(gpu))
+    g = torch.Generator(device=gpu).manual_seed(7)
+    obs = torch.rand(B, L, od, device=gpu, generator=g)
+    actions = torch.randn(B, L, A, device=gpu, generator=g) * 0.5
+    w1, w3 = torch.randn(B, L, A, device=gpu, generator=g), torch.randn(B, L, A, device=gpu, generator=g)
+    w2 = torch.randn(B, L, 1, device=gpu, generator=g)
+    m.zero_grad()
+    lp_r, v_r, ent_r = m(None, obs, actions, None)
+    ((lp_r * w1).sum() + (v_r * w2).sum() + (ent_r * w3).sum()).backward()
+    ref = {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
+    m.zero_grad()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        lp_b, v_b, ent_b = m(None, obs, actions, None)
+        ((lp_b.float() * w1).sum() + (v_b.float() * w2).sum() + (ent_b.float() * w3).sum()).backward()
+    refb = {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
+    for p_ in m.parameters():
+        p_.grad = torch.zeros_like(p_)
+    tol = lambda a, b: max(3e-2, 2.5 * rel(a.float(), b))  # noqa: E731
+    v_k, lp_k, ent_k = mat_train.evaluate_actions(m, obs, actions, None)
+    assert lp_k.shape == lp_r.shape and ent_k.shape == ent_r.shape
+    assert rel(lp_k, lp_r) < tol(lp_b, lp_r), (rel(lp_k, lp_r), rel(lp_b.float(), lp_r))
+    assert rel(v_k, v_r) < tol(v_b, v_r) and rel(ent_k, ent_r) < tol(ent_b, ent_r)
+    ((lp_k * w1).sum() + (v_k * w2).sum() + (ent_k * w3).sum()).backward()
+    torch.cuda.synchronize()
+    bad = []
+    params = dict(m.named_parameters())
+    for n, r in ref.items():
+        gg = params[n].grad
+        if "key.bias" in n:
+            e = (gg - r).abs().max().item() / (ref[n.replace("key.bias", "key.weight")].abs().max().item() + 1e-6)
+            lim = 8e-2
+        else:
+            e = rel(gg, r)
+            lim = max(6e-2, 2.5 * rel(refb[n], r))
+        if e > lim:
+            bad.append((n, round(e, 4), round(rel(refb[n], r), 4)))
+    assert not bad, bad
+
+
+def test_mujoco_runner_uses_fused_trainer(gpu):
+    """MA-MuJoCo (HalfCheetah 6x1 surrogate) trains through the fused HIP trainer (no eager GEMMs in the update)."""
+    from mat_dcml_amd.config import _MUJOCO_FLAGS, get_config, parse_args
+    from mat_dcml_amd.ops.paths import kernel_report
+    from mat_dcml_amd.runner.mujoco_runner import MujocoRunner
+    args = parse_args(["--env_name", "mujoco", "--scenario", "HalfCheetah-v2", "--agent_conf", "6x1", "--agent_obsk", "0",
+                       "--n_rollout_threads", "8", "--episode_length", "10", "--ppo_epoch", "2", "--num_mini_batch", "2"],
+                      get_config(), extra=_MUJOCO_FLAGS, warn=False)
+    r = MujocoRunner({"all_args": args, "device": gpu, "run_dir": None})
+    assert r.trainer.fused, r.trainer.fused_reason
+    r.warmup()
+    infos = r.train_iteration()
+    torch.cuda.synchronize()
+    assert all(torch.isfinite(torch.as_tensor(float(v))) for v in infos.values())
+    assert kernel_report(r)["train"].startswith("hip:")
