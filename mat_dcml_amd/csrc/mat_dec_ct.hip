@@ -86,11 +86,12 @@ template <bool SAVE>
 __device__ __forceinline__ void cross_attn_fwd_ct(const Mat* m, const LNp& ln, CT* xr, const float* rep, bf16_t* sv_x1,
                                                   bf16_t* sv_a, float* sv_lse, const Ctx& c) {
   const int lane = c.lane;
+  __syncthreads();   // every wave done reading the self-attention's K / V
   cross_proj(m, xr, nullptr, rep, SAVE ? sv_x1 : nullptr, c);
   __syncthreads();
   CP_MARK(24);
-  attn_fwd(c.QB, c.KB, c.VB, c.QB, true, SAVE ? sv_lse : nullptr, c);
-  __syncthreads();
+  CT O[MAXRT];
+  attn_fwd_ct(c.QB, c.KB, c.VB, true, SAVE ? sv_lse : nullptr, O, c);
   CP_MARK(25);
   AFr Wp;
   loadA(Wp, m[7].fa, lane);
@@ -105,7 +106,7 @@ __device__ __forceinline__ void cross_attn_fwd_ct(const Mat* m, const LNp& ln, C
   for (int k = 0; k < MAXRT; ++k) {
     const int rt = c.wave + 4 * k;
     if (rt < c.NT) {
-      const CTr a = ld_lds(c.QB, rt, lane);
+      const CTr a = ct_pack(O[k]);
       if (SAVE) st_g(sv_a, c.tok0, rt, c.NR, a, lane);
       CT t = ct_add(bp, rp[k]), xh;
       mm(t, Wp, a);
@@ -168,10 +169,10 @@ __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, C
   load_lse(sv_lse, c);
   __syncthreads();
   CP_MARK(6);
-  attn_bwd_q(c.QB, c.KB, c.VB, c.DA, c.DQ, true, c);
+  attn_bwd_q_ct(c.QB, c.KB, c.VB, c.DA, c.DQ, true, c);
   __syncthreads();
   CP_MARK(7);
-  attn_bwd_kv(c.QB, c.KB, c.VB, c.DA, true, c);
+  attn_bwd_kv_ct(c.QB, c.KB, c.VB, c.DA, true, c);
   __syncthreads();
   CP_MARK(8);
   {

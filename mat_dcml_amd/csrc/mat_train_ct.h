@@ -369,6 +369,204 @@ __device__ __forceinline__ void proj3_bwd(const Mat* m, int m0, const bf16_t* s0
   }
 }
 
+// ------------------------------------------------------------------------------------------ attention (CT)
+// Sequence-block-diagonal attention over the workgroup's packed rows, per (16-row tile, head), keys / queries visited
+// in 32-row chunks.  Round-1 MFMA attention (mat_train_common.h) with the operands turned around so that every
+// product's output lands in the token-on-lane layout:
+//  * scores: Sᵀ = K·Qᵀ (round 1): lane (g, c) holds S[query c][keys kb + 8g + j] — already the B operand (k = keys,
+//    n = query) of Oᵀ = Vᵀ·Pᵀ, whose A operand Vᵀ comes from ds_read_b64_tr_b16 of the token-major V;
+//  * so O (and dQ, dK, dV in the backward) come out as CT tiles — O feeds the output projection from registers;
+//  * forward: ONE pass with an online max (round 1 took two: max/sum, then P·V), scores in log2 units so that
+//    p = exp2(s - m) is a subtract + v_exp; P and dS enter their MFMAs as hi/lo bf16 pairs (dS rows sum to zero and
+//    feed bias gradients; a single-bf16 P left the cross-attention query-bias gradient at 2.6x the bf16 yardstick);
+//  * log-sum-exp is saved in log2 units ([tok][2], consumed only by these kernels).
+constexpr float ATT_L2 = 0.17677669529663687f * 1.4426950408889634f;   // 1/sqrt(32) * log2(e)
+
+struct QSpan { int qs, qe; };   // keys [qs, qe) visible to a query (empty for padded rows)
+__device__ __forceinline__ QSpan qspan(int q, bool causal, const Ctx& c) {
+  QSpan s;
+  s.qs = (q / c.L) * c.L;
+  s.qe = q >= c.NR ? s.qs : (causal ? q + 1 : min(s.qs + c.L, c.NR));
+  return s;
+}
+
+// scores of one chunk for this lane's query, log2 units, invisible keys -inf
+__device__ __forceinline__ void chunk_scores(const bf16_t* K, int kb, int h, const bf16x8& qB, const QSpan& qs,
+                                             float* sc, int lane) {
+  score_chunk_T(K, kb, h, qB, sc, lane);
+  const int base = kb + 8 * (lane >> 4);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sc[j] = (base + j >= qs.qs && base + j < qs.qe) ? sc[j] * ATT_L2 : -INFINITY;
+}
+
+__device__ __forceinline__ bf16x8 pack8v(const float* x) {
+  return mk8(pk2(x[0], x[1]), pk2(x[2], x[3]), pk2(x[4], x[5]), pk2(x[6], x[7]));
+}
+__device__ __forceinline__ void split8v(const float* x, bf16x8& hi, bf16x8& lo) {
+  uint32_t h[4], l[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    h[i] = pk2(x[2 * i], x[2 * i + 1]);
+    l[i] = pk2(x[2 * i] - blo(h[i]), x[2 * i + 1] - bhi(h[i]));
+  }
+  hi = mk8(h[0], h[1], h[2], h[3]);
+  lo = mk8(l[0], l[1], l[2], l[3]);
+}
+
+// forward: O (CT, the wave's query tiles rt = wave + 4k, both heads) = softmax(scale Q Kᵀ) V
+__device__ __forceinline__ void attn_fwd_ct(const bf16_t* Q, const bf16_t* K, const bf16_t* V, bool causal, float* lse_g,
+                                            CT* O, const Ctx& c) {
+  const int lane = c.lane, g = lane >> 4, c16 = lane & 15;
+#pragma unroll
+  for (int k = 0; k < MAXRT; ++k) {
+    const int rt = c.wave + 4 * k;
+    if (rt < c.NT) {
+      const int q = rt * 16 + c16;
+      const QSpan qs = qspan(q, causal, c);
+      const SeqSpan sp = tile_span(rt, c, causal);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const bf16x8 qB = lda_tm(Q, q, 4 * h + g);
+        float m = -INFINITY, l = 0.f;
+        f32x4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
+        for (int kb = sp.lo; kb < sp.hi; kb += 32) {
+          float sc[8];
+          chunk_scores(K, kb, h, qB, qs, sc, lane);
+          float cm = sc[0];
+#pragma unroll
+          for (int j = 1; j < 8; ++j) cm = fmaxf(cm, sc[j]);
+          const float nm = fmaxf(m, cross_row_max(cm));
+          const float mr = nm == -INFINITY ? 0.f : nm;
+          const float alpha = exp2f(m - mr);
+          float ps = 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            sc[j] = exp2f(sc[j] - mr);
+            ps += sc[j];
+          }
+          l = l * alpha + ps;
+          o0 *= alpha;
+          o1 *= alpha;
+          bf16x8 ph, pl;
+          split8v(sc, ph, pl);
+          const bf16x8 va = ld_frag_T(V, kb, 32 * h, lane), vb = ld_frag_T(V, kb, 32 * h + 16, lane);
+          o0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, ph, o0, 0, 0, 0);
+          o0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pl, o0, 0, 0, 0);
+          o1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vb, ph, o1, 0, 0, 0);
+          o1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vb, pl, o1, 0, 0, 0);
+          m = nm;
+        }
+        l = cross_row_sum(l);
+        const float il = l > 0.f ? 1.f / l : 0.f;
+        O[k].v[2 * h] = o0 * il;
+        O[k].v[2 * h + 1] = o1 * il;
+        if (lse_g && g == 0 && q < c.NR) lse_g[(size_t)(c.tok0 + q) * 2 + h] = l > 0.f ? m + __log2f(l) : 0.f;
+      }
+    }
+  }
+}
+
+// CT pieces mt0, mt0+1 (features 16mt0 .. 16mt0+31 = one head) of row tile rt -> token-major LDS
+__device__ __forceinline__ void st_lds_head(bf16_t* buf, int rt, int h, f32x4 a, f32x4 b, bool ok, int lane) {
+  const int g = lane >> 4, row = rt * 16 + (lane & 15);
+  const uint2 ua = ok ? make_uint2(pk2(a[0], a[1]), pk2(a[2], a[3])) : make_uint2(0u, 0u);
+  const uint2 ub = ok ? make_uint2(pk2(b[0], b[1]), pk2(b[2], b[3])) : make_uint2(0u, 0u);
+  *(uint2*)(buf + tmo(row, 32 * h + 4 * g)) = ua;
+  *(uint2*)(buf + tmo(row, 32 * h + 16 + 4 * g)) = ub;
+}
+
+// backward, by (query tile, head) item: delta_q = Σ_k P dP (-> DEL), dQ = scale Σ_k dS K (-> DQ, token-major);
+// LSE in log2 units.  Items are dealt round robin (a runtime loop: the per-wave tile loop of the forward blew up
+// the backward kernels' code and register pressure).
+__device__ __forceinline__ void attn_bwd_q_ct(const bf16_t* Q, const bf16_t* K, const bf16_t* V, const bf16_t* DA,
+                                              bf16_t* DQ, bool causal, const Ctx& c) {
+  const int lane = c.lane, g = lane >> 4, c16 = lane & 15;
+  for (int item = c.wave; item < 2 * c.NT; item += 4) {
+    const int rt = item >> 1, h = item & 1;
+    const int q = rt * 16 + c16;
+    const QSpan qs = qspan(q, causal, c);
+    const SeqSpan sp = tile_span(rt, c, causal);
+    const bf16x8 qB = lda_tm(Q, q, 4 * h + g), dB = lda_tm(DA, q, 4 * h + g);
+    const float lse = c.LSE[h * c.NRP + q];
+    float delta = 0.f;
+    for (int kb = sp.lo; kb < sp.hi; kb += 32) {
+      float sc[8], dp[8];
+      chunk_scores(K, kb, h, qB, qs, sc, lane);
+      score_chunk_T(V, kb, h, dB, dp, lane);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) delta += exp2f(sc[j] - lse) * dp[j];
+    }
+    delta = cross_row_sum(delta);
+    f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
+    for (int kb = sp.lo; kb < sp.hi; kb += 32) {
+      float sc[8], dp[8];
+      chunk_scores(K, kb, h, qB, qs, sc, lane);
+      score_chunk_T(V, kb, h, dB, dp, lane);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sc[j] = exp2f(sc[j] - lse) * (dp[j] - delta);
+      bf16x8 dsh, dsl;
+      split8v(sc, dsh, dsl);
+      const bf16x8 k0 = ld_frag_T(K, kb, 32 * h, lane), k1 = ld_frag_T(K, kb, 32 * h + 16, lane);
+      d0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, dsh, d0, 0, 0, 0);
+      d0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, dsl, d0, 0, 0, 0);
+      d1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, dsh, d1, 0, 0, 0);
+      d1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, dsl, d1, 0, 0, 0);
+    }
+    st_lds_head(DQ, rt, h, d0 * ATT_SCALE, d1 * ATT_SCALE, q < c.NR, lane);
+    if (g == 0) c.DEL[h * c.NRP + q] = q < c.NR ? delta : 0.f;
+  }
+}
+
+// backward, by (key tile, head) item: dV = Pᵀ dO, dK = scale dSᵀ Q, written over the item's own K / V head columns
+__device__ __forceinline__ void attn_bwd_kv_ct(const bf16_t* Q, bf16_t* K, bf16_t* V, const bf16_t* DA, bool causal,
+                                               const Ctx& c) {
+  const int lane = c.lane, g = lane >> 4, c16 = lane & 15;
+  for (int item = c.wave; item < 2 * c.NT; item += 4) {
+    const int rt = item >> 1, h = item & 1;
+    const int kk = rt * 16 + c16;
+    const bool kv = kk < c.NR;
+    const int ks = (kk / c.L) * c.L, ke = min(ks + c.L, c.NR);
+    const int qlo = causal ? kk : ks;
+    SeqSpan sp = tile_span(rt, c, false);
+    if (causal) sp.lo = (rt * 16) & ~31;
+    const bf16x8 kB = lda_tm(K, kk, 4 * h + g), vB = lda_tm(V, kk, 4 * h + g);
+    f32x4 k0a = {0.f, 0.f, 0.f, 0.f}, k1a = {0.f, 0.f, 0.f, 0.f}, v0a = {0.f, 0.f, 0.f, 0.f}, v1a = {0.f, 0.f, 0.f, 0.f};
+    for (int qb = sp.lo; qb < sp.hi; qb += 32) {
+      float sc[8], dp[8];
+      score_chunk_T(Q, qb, h, kB, sc, lane);    // sc[j] = S[query qb + 8g + j][key kk]
+      score_chunk_T(DA, qb, h, vB, dp, lane);   // dp[j] = dP[query][key kk]
+      const float4* lp = (const float4*)(c.LSE + h * c.NRP + qb + 8 * g);
+      const float4* dl = (const float4*)(c.DEL + h * c.NRP + qb + 8 * g);
+      const float4 l0 = lp[0], l1 = lp[1], e0 = dl[0], e1 = dl[1];
+      const float lsev[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+      const float delv[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+      float pv[8], ds[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int qq = qb + 8 * g + j;
+        const bool ok = kv && qq >= qlo && qq < ke;
+        pv[j] = ok ? exp2f(sc[j] * ATT_L2 - lsev[j]) : 0.f;
+        ds[j] = pv[j] * (dp[j] - delv[j]);
+      }
+      bf16x8 ph, pl, dsh, dsl;
+      split8v(pv, ph, pl);
+      split8v(ds, dsh, dsl);
+      const bf16x8 o0 = ld_frag_T(DA, qb, 32 * h, lane), o1 = ld_frag_T(DA, qb, 32 * h + 16, lane);
+      v0a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(o0, ph, v0a, 0, 0, 0);
+      v0a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(o0, pl, v0a, 0, 0, 0);
+      v1a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(o1, ph, v1a, 0, 0, 0);
+      v1a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(o1, pl, v1a, 0, 0, 0);
+      const bf16x8 q0 = ld_frag_T(Q, qb, 32 * h, lane), q1 = ld_frag_T(Q, qb, 32 * h + 16, lane);
+      k0a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(q0, dsh, k0a, 0, 0, 0);
+      k0a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(q0, dsl, k0a, 0, 0, 0);
+      k1a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(q1, dsh, k1a, 0, 0, 0);
+      k1a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(q1, dsl, k1a, 0, 0, 0);
+    }
+    st_lds_head(K, rt, h, k0a * ATT_SCALE, k1a * ATT_SCALE, kv, lane);
+    st_lds_head(V, rt, h, v0a, v1a, kv, lane);
+  }
+}
+
 // ------------------------------------------------------------------------------------------ sublayers (forward)
 // self attention: x <- LN(x + proj(attn(q(x), k(x), v(x))))   (ma_transformer.py:89-92,112)
 template <bool SAVE>
@@ -385,12 +583,13 @@ __device__ __forceinline__ void self_attn_fwd_ct(const Mat* m, const LNp& ln, CT
         if (SAVE) st_g(sv_xin, c.tok0, rt, c.NR, xp[k], lane);
       }
     }
+    __syncthreads();   // every wave done reading the previous attention's K / V (no barrier after an attention)
     proj3(m, 0, xp, c);
   }
   __syncthreads();
   CP_MARK(20);
-  attn_fwd(c.QB, c.KB, c.VB, c.QB, causal, SAVE ? sv_lse : nullptr, c);
-  __syncthreads();
+  CT O[MAXRT];
+  attn_fwd_ct(c.QB, c.KB, c.VB, causal, SAVE ? sv_lse : nullptr, O, c);
   CP_MARK(21);
   AFr Wp;
   loadA(Wp, m[3].fa, lane);
@@ -399,7 +598,7 @@ __device__ __forceinline__ void self_attn_fwd_ct(const Mat* m, const LNp& ln, CT
   for (int k = 0; k < MAXRT; ++k) {
     const int rt = c.wave + 4 * k;
     if (rt < c.NT) {
-      const CTr a = ld_lds(c.QB, rt, lane);
+      const CTr a = ct_pack(O[k]);
       if (SAVE) st_g(sv_a, c.tok0, rt, c.NR, a, lane);
       CT t = ct_add(bp, xr[k]), xh;
       mm(t, Wp, a);
@@ -559,10 +758,10 @@ __device__ __forceinline__ void self_attn_bwd_ct(const Mat* m, const LNp& ln, CT
   load_lse(sv_lse, c);
   __syncthreads();
   CP_MARK(13);
-  attn_bwd_q(c.QB, c.KB, c.VB, c.DA, c.DQ, causal, c);
+  attn_bwd_q_ct(c.QB, c.KB, c.VB, c.DA, c.DQ, causal, c);
   __syncthreads();
   CP_MARK(14);
-  attn_bwd_kv(c.QB, c.KB, c.VB, c.DA, causal, c);
+  attn_bwd_kv_ct(c.QB, c.KB, c.VB, c.DA, causal, c);
   __syncthreads();
   CP_MARK(15);
   wgrad64(c.DQ, c.XB, m[0], c);
