@@ -20,12 +20,13 @@ __device__ __forceinline__ int dec_token_ct(const DecP& p, int tok, int i) {
 
 // x0 pre-activation = W_a · onehot(token) — a column gather of W_a [64][A+1]; continuous action type:
 // W_a · a_prev + b_a with a_prev the previous agent's action vector (zero for row 0)
+template <bool CONT>
 __device__ __forceinline__ CT dec_embed_pre_ct(const DecP& p, int rt, int& tokid, const Ctx& c) {
   const int lane = c.lane, g = lane >> 4;
   const int row = rt * 16 + (lane & 15);
   const bool ok = row < c.NR;
   CT pre;
-  if (p.cont) {
+  if (CONT) {
     tokid = -1;
     const bool first = !ok || row % c.L == 0;
     const float* prev = p.act + (size_t)(c.tok0 + (first ? 0 : row - 1)) * p.A;
@@ -56,7 +57,7 @@ __device__ __forceinline__ void cross_proj(const Mat* m, const CT* xr, const bf1
   CTr xp[MAXRT], rp[MAXRT];
 #pragma unroll
   for (int k = 0; k < MAXRT; ++k) {
-    const int rt = c.wave + 4 * k;
+    const int rt = c.wave + NW * k;
     if (rt < c.NT) {
       rp[k] = ct_pack(ld_gf(rep, c.tok0, rt, c.NR, lane));
       xp[k] = xr ? ct_pack(xr[k]) : ld_g(sv_x1_in, c.tok0, rt, c.NR, lane);
@@ -71,7 +72,7 @@ __device__ __forceinline__ void cross_proj(const Mat* m, const CT* xr, const bf1
     const CT b = ld_vec(m[4 + mi].b, lane);
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
-      const int rt = c.wave + 4 * k;
+      const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         CT t = b;
         mm(t, W, mi == 0 ? rp[k] : xp[k]);
@@ -99,12 +100,12 @@ __device__ __forceinline__ void cross_attn_fwd_ct(const Mat* m, const LNp& ln, C
   CT rp[MAXRT];
 #pragma unroll
   for (int k = 0; k < MAXRT; ++k) {
-    const int rt = c.wave + 4 * k;
+    const int rt = c.wave + NW * k;
     if (rt < c.NT) rp[k] = ld_gf(rep, c.tok0, rt, c.NR, lane);
   }
 #pragma unroll
   for (int k = 0; k < MAXRT; ++k) {
-    const int rt = c.wave + 4 * k;
+    const int rt = c.wave + NW * k;
     if (rt < c.NT) {
       const CTr a = ct_pack(O[k]);
       if (SAVE) st_g(sv_a, c.tok0, rt, c.NR, a, lane);
@@ -125,40 +126,50 @@ __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, C
     CT dlg, dlb;
     ct_zero(dlg);
     ct_zero(dlb);
-    AFr Wpf, Wpb;
-    loadA(Wpf, m[7].fa, lane);
-    loadA(Wpb, m[7].ba, lane);
-    const CT bp = ld_vec(m[7].b, lane), gam = ld_vec(ln.g, lane), bet = ld_vec(ln.b, lane);
-    CTr as[MAXRT];
+    {   // pass 1 (Wp): LN backward -> ds ; DQ = dY of Wp, XB = X of Wp
+      AFr Wpf;
+      loadA(Wpf, m[7].fa, lane);
+      const CT bp = ld_vec(m[7].b, lane), gam = ld_vec(ln.g, lane), bet = ld_vec(ln.b, lane);
+      CTr as[MAXRT];
 #pragma unroll
-    for (int k = 0; k < MAXRT; ++k) {
-      const int rt = c.wave + 4 * k;
-      if (rt < c.NT) {
-        as[k] = ld_g(sv_a, c.tok0, rt, c.NR, lane);
-        dres[k] = ld_gf(rep, c.tok0, rt, c.NR, lane);   // rep (the residual input) parked in dres until used
+      for (int k = 0; k < MAXRT; ++k) {
+        const int rt = c.wave + NW * k;
+        if (rt < c.NT) {
+          as[k] = ld_g(sv_a, c.tok0, rt, c.NR, lane);
+          dres[k] = ld_gf(rep, c.tok0, rt, c.NR, lane);   // rep (the residual input) parked in dres until used
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < MAXRT; ++k) {
+        const int rt = c.wave + NW * k;
+        if (rt < c.NT) {
+          const bool ok = tok_ok(rt, c);
+          CT s = ct_add(bp, dres[k]), xh, yy, ds;
+          mm(s, Wpf, as[k]);
+          const float rs = ln_fwd_ct(s, xh, yy, gam, bet);
+          ln_bwd_ct(dx[k], xh, rs, gam, ok, ds, dlg, dlb);
+          st_lds(c.DQ, rt, ct_pack(ds), ok, lane);   // dY of Wp
+          st_lds(c.XB, rt, as[k], ok, lane);         // X of Wp
+          dres[k] = ds;                              // residual path -> d rep
+        }
+      }
+      flush_vec(dlg, c.g(ln.dg), lane);
+      flush_vec(dlb, c.g(ln.db), lane);
+    }
+    {   // pass 2 (Wpᵀ): dO = Wpᵀ ds -> DA
+      AFr Wpb;
+      loadA(Wpb, m[7].ba, lane);
+#pragma unroll
+      for (int k = 0; k < MAXRT; ++k) {
+        const int rt = c.wave + NW * k;
+        if (rt < c.NT) {
+          CT da;
+          ct_zero(da);
+          mm(da, Wpb, ld_lds(c.DQ, rt, lane));
+          st_lds(c.DA, rt, ct_pack(da), tok_ok(rt, c), lane);
+        }
       }
     }
-#pragma unroll
-    for (int k = 0; k < MAXRT; ++k) {
-      const int rt = c.wave + 4 * k;
-      if (rt < c.NT) {
-        const bool ok = tok_ok(rt, c);
-        CT s = ct_add(bp, dres[k]), xh, yy, ds;
-        mm(s, Wpf, as[k]);
-        const float rs = ln_fwd_ct(s, xh, yy, gam, bet);
-        ln_bwd_ct(dx[k], xh, rs, gam, ok, ds, dlg, dlb);
-        const CTr dsr = ct_pack(ds);
-        st_lds(c.DQ, rt, dsr, ok, lane);     // dY of Wp
-        st_lds(c.XB, rt, as[k], ok, lane);   // X of Wp
-        CT da;
-        ct_zero(da);
-        mm(da, Wpb, dsr);
-        st_lds(c.DA, rt, ct_pack(da), ok, lane);   // dO
-        dres[k] = ds;                              // residual path -> d rep
-      }
-    }
-    flush_vec(dlg, c.g(ln.dg), lane);
-    flush_vec(dlb, c.g(ln.db), lane);
   }
   __syncthreads();
   CP_MARK(4);
@@ -179,12 +190,12 @@ __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, C
     CTr rq[MAXRT];
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {   // q input (rep) into QB for dW_q
-      const int rt = c.wave + 4 * k;
+      const int rt = c.wave + NW * k;
       if (rt < c.NT) rq[k] = ct_pack(ld_gf(rep, c.tok0, rt, c.NR, lane));
     }
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
-      const int rt = c.wave + 4 * k;
+      const int rt = c.wave + NW * k;
       if (rt < c.NT) st_lds(c.QB, rt, rq[k], tok_ok(rt, c), lane);
     }
   }
@@ -196,7 +207,7 @@ __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, C
   CP_MARK(18);
 #pragma unroll
   for (int k = 0; k < MAXRT; ++k) {
-    const int rt = c.wave + 4 * k;
+    const int rt = c.wave + NW * k;
     if (rt < c.NT) ct_zero(dx[k]);
   }
   proj3_bwd(m, 4, c.DQ, c.KB, c.VB, dres, dx, c);
@@ -204,12 +215,12 @@ __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, C
     CT cur[MAXRT];
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {   // d rep read-modify-write (each row owned by exactly one wave of one workgroup)
-      const int rt = c.wave + 4 * k;
+      const int rt = c.wave + NW * k;
       if (rt < c.NT) cur[k] = ld_gf(drep, c.tok0, rt, c.NR, lane);
     }
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
-      const int rt = c.wave + 4 * k;
+      const int rt = c.wave + NW * k;
       if (rt < c.NT) st_gf(drep, c.tok0, rt, c.NR, ct_add(cur[k], dres[k]), lane);
     }
   }
@@ -325,7 +336,7 @@ __device__ __forceinline__ HeadStat head_stats(const DecP& p, const f32x4* L, un
 
 constexpr float HALF_LOG_2PI = 0.91893853320467274f;
 
-template <int MA>
+template <int MA, bool CONT>
 __device__ __forceinline__ void head_fwd_ct(const DecP& p, const CT* xr, bool save, const Ctx& c) {
   const int lane = c.lane, g = lane >> 4;
   HeadW<MA> W;
@@ -335,13 +346,13 @@ __device__ __forceinline__ void head_fwd_ct(const DecP& p, const CT* xr, bool sa
   const CT bh = ld_vec(p.h1.b, lane), gam = ld_vec(p.lnh.g, lane), bet = ld_vec(p.lnh.b, lane);
 #pragma unroll
   for (int k = 0; k < MAXRT; ++k) {
-    const int rt = c.wave + 4 * k;
+    const int rt = c.wave + NW * k;
     if (rt < c.NT) {
       const int row = rt * 16 + (lane & 15);
       const bool ok = row < c.NR;
       const size_t tok = (size_t)(c.tok0 + (ok ? row : 0));
-      const unsigned am = p.cont ? 0u : slot_mask<MA>(p, tok, lane);
-      const float actf = p.cont ? 0.f : p.act[tok];
+      const unsigned am = CONT ? 0u : slot_mask<MA>(p, tok, lane);
+      const float actf = CONT ? 0.f : p.act[tok];
       const CTr x = ct_pack(xr[k]);
       if (save) st_g(p.sv_head, c.tok0, rt, c.NR, x, lane);
       CT hh = bh, xh, n;
@@ -350,7 +361,7 @@ __device__ __forceinline__ void head_fwd_ct(const DecP& p, const CT* xr, bool sa
       ln_fwd_ct(hh, xh, n, gam, bet);
       f32x4 L[MA];
       head_logits_ct<MA>(p, W, n, L, lane);
-      if (p.cont) {   // per-dimension Normal(mean, std): this lane's dims a = 16ma + 4g + r
+      if (CONT) {   // per-dimension Normal(mean, std): this lane's dims a = 16ma + 4g + r
 #pragma unroll
         for (int ma = 0; ma < MA; ++ma)
 #pragma unroll
@@ -384,7 +395,7 @@ __device__ __forceinline__ void head_fwd_ct(const DecP& p, const CT* xr, bool sa
   }
 }
 
-template <int MA>
+template <int MA, bool CONT>
 __device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c) {
   const int lane = c.lane, g = lane >> 4;
   constexpr int SB = (MA + 1) / 2;   // k-steps over the logit axis in dn = W_h2ᵀ dz
@@ -413,36 +424,47 @@ __device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c)
             WT[mt][s][j] = (short)f2bf(w);
           }
     }
-    AFr Hf, Hb;
-    loadA(Hf, p.h1.fa, lane);
-    loadA(Hb, p.h1.ba, lane);
-    const CT bh = ld_vec(p.h1.b, lane), gam = ld_vec(p.lnh.g, lane), bet = ld_vec(p.lnh.b, lane);
+    CT hhs[MAXRT];   // head1 pre-activations (first pass: W_h1 and its bias are dead before the softmax work)
+    {
+      AFr Hf;
+      loadA(Hf, p.h1.fa, lane);
+      const CT bh = ld_vec(p.h1.b, lane);
+#pragma unroll
+      for (int k = 0; k < MAXRT; ++k) {
+        const int rt = c.wave + NW * k;
+        if (rt < c.NT) {
+          const CTr x = ld_g(p.sv_head, c.tok0, rt, c.NR, lane);
+          st_lds(c.KB, rt, x, tok_ok(rt, c), lane);   // X of W_h1
+          hhs[k] = bh;
+          mm(hhs[k], Hf, x);
+        }
+      }
+    }
+    const CT gam = ld_vec(p.lnh.g, lane), bet = ld_vec(p.lnh.b, lane);
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
-      const int rt = c.wave + 4 * k;
+      const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         const int row = rt * 16 + (lane & 15);
         const bool ok = row < c.NR;
         const size_t tok = (size_t)(c.tok0 + (ok ? row : 0));
-        const unsigned am = p.cont ? 0u : slot_mask<MA>(p, tok, lane);
-        const float actf = p.cont ? 0.f : p.act[tok];
-        const float dlp = (ok && !p.cont) ? p.dlogp[tok] : 0.f, den = (ok && !p.cont) ? p.dent[tok] : 0.f;
-        const CTr x = ld_g(p.sv_head, c.tok0, rt, c.NR, lane);
-        CT hh = bh;
-        mm(hh, Hf, x);
+        const unsigned am = CONT ? 0u : slot_mask<MA>(p, tok, lane);
+        const float actf = CONT ? 0.f : p.act[tok];
+        const float dlp = (ok && !CONT) ? p.dlogp[tok] : 0.f, den = (ok && !CONT) ? p.dent[tok] : 0.f;
+        const CT& hh = hhs[k];
         CT gl = hh, xh, n;
         gelu_ct(gl);
         const float rs = ln_fwd_ct(gl, xh, n, gam, bet);
         f32x4 L[MA];
         head_logits_ct<MA>(p, W, n, L, lane);
-        const bool disc = !p.cont && (row % c.L) < p.n_disc;
+        const bool disc = !CONT && (row % c.L) < p.n_disc;
         const int act = min(max((int)actf, 0), p.A - 1);
-        const HeadStat st = p.cont ? HeadStat{0.f, 0.f, 0.f, 0.f} : head_stats<MA>(p, L, am, act, disc, lane);
+        const HeadStat st = CONT ? HeadStat{0.f, 0.f, 0.f, 0.f} : head_stats<MA>(p, L, am, act, disc, lane);
         // d loss / d logits of this lane's slots
         f32x4 Z[2 * SB];
 #pragma unroll
         for (int ma = 0; ma < 2 * SB; ++ma) Z[ma] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (p.cont) {   // per-dimension Normal heads: d log p / d mean, and the log_std partials of this lane's dims
+        if (CONT) {   // per-dimension Normal heads: d log p / d mean, and the log_std partials of this lane's dims
 #pragma unroll
           for (int ma = 0; ma < MA; ++ma)
 #pragma unroll
@@ -506,17 +528,25 @@ __device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c)
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int q = 0; q < 4; ++q) dgg.v[i][q] = ok ? dgg.v[i][q] * gelu_erf_grad(hh.v[i][q]) : 0.f;
-        const CTr dgr = ct_pack(dgg);
-        st_lds(c.DQ, rt, dgr, ok, lane);   // dY of W_h1
-        st_lds(c.KB, rt, x, ok, lane);     // X of W_h1
+        st_lds(c.DQ, rt, ct_pack(dgg), ok, lane);   // dY of W_h1
+      }
+    }
+  }
+  {   // second pass (W_h1ᵀ): dx = W_h1ᵀ dY
+    AFr Hb;
+    loadA(Hb, p.h1.ba, lane);
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + NW * k;
+      if (rt < c.NT) {
         ct_zero(dx[k]);
-        mm(dx[k], Hb, dgr);
+        mm(dx[k], Hb, ld_lds(c.DQ, rt, lane));
       }
     }
   }
   flush_vec(dlg, c.g(p.lnh.dg), lane);
   flush_vec(dlb, c.g(p.lnh.db), lane);
-  if (p.cont) {
+  if (CONT) {
 #pragma unroll
     for (int ma = 0; ma < MA; ++ma)
 #pragma unroll
@@ -538,7 +568,7 @@ __device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c)
 }
 
 // ============================================================================================== forward
-template <int NB, bool SAVE, int MA>
+template <int NB, bool SAVE, int MA, bool CONT>
 __device__ __forceinline__ void dec_fwd_tile(const DecP& p, char* smem, int seq0, int nseq) {
   const Ctx c = make_ctx(p, smem, seq0, nseq);
   if (c.nseq <= 0) return;
@@ -551,10 +581,10 @@ __device__ __forceinline__ void dec_fwd_tile(const DecP& p, char* smem, int seq0
     const CT gam = ld_vec(p.lnd_g, lane), bet = ld_vec(p.lnd_b, lane);
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
-      const int rt = c.wave + 4 * k;
+      const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         int tk;
-        CT pre = dec_embed_pre_ct(p, rt, tk, c), xh;
+        CT pre = dec_embed_pre_ct<CONT>(p, rt, tk, c), xh;
         gelu_ct(pre);
         ln_fwd_ct(pre, xh, xr[k], gam, bet);
       }
@@ -569,21 +599,24 @@ __device__ __forceinline__ void dec_fwd_tile(const DecP& p, char* smem, int seq0
     cross_attn_fwd_ct<SAVE>(B.m, B.ln[1], xr, p.rep, p.sv[b].x1, p.sv[b].a2, p.sv[b].lse2, cc);
     mlp_fwd_ct<SAVE>(B.m[8], B.m[9], B.ln[2], xr, p.sv[b].x2, p.sv[b].h, cc);
   }
-  head_fwd_ct<MA>(p, xr, SAVE, c);
+  head_fwd_ct<MA, CONT>(p, xr, SAVE, c);
   CP_MARK(27);
 }
 
+#ifndef MDL_CT_BWD_TU
 // MA = logit tiles of the action head: 1 (A <= 16: DCML, MPE) or 4 (A <= 64: SMAC's 36 actions)
-template <int NB, bool SAVE, int MA>
-__global__ __launch_bounds__(256, FWD_WGPC) void mat_dec_fwd_ct(DecP p) {
+template <int NB, bool SAVE, int MA, bool CONT>
+__global__ __launch_bounds__(NTHR, FWD_WGPC) void mat_dec_fwd_ct(DecP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   CP_BEGIN();
-  FOR_TILES(p, (dec_fwd_tile<NB, SAVE, MA>(p, smem, s0, ns)));
+  FOR_TILES(p, (dec_fwd_tile<NB, SAVE, MA, CONT>(p, smem, s0, ns)));
   CP_END();
 }
 
+#endif  // !MDL_CT_BWD_TU
+
 // ============================================================================================== backward
-template <int NB, int MA>
+template <int NB, int MA, bool CONT>
 __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0, int nseq) {
   const Ctx c = make_ctx(p, smem, seq0, nseq);
   if (c.nseq <= 0) return;
@@ -592,7 +625,7 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
   CP_MARK(0);
   const int lane = c.lane;
   CT dx[MAXRT];
-  head_bwd_ct<MA>(p, dx, c);
+  head_bwd_ct<MA, CONT>(p, dx, c);
 #pragma unroll 1
   for (int bb = NB - 1; bb >= 0; --bb) {
     const Blk& B = p.blk[bb];
@@ -605,7 +638,7 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
   // ---------------- embedding backward: dW_a[:, token] += d pre ; LN_dec params
   {
     float* EMB = (float*)c.QB;   // [(A+1)][64] f32 accumulators (QB + KB: 2 NRP x 128 B >= 65 x 256 B)
-    for (int i = c.tid; i < (p.A + 1) * 64; i += 256) EMB[i] = 0.f;
+    for (int i = c.tid; i < (p.A + 1) * 64; i += NTHR) EMB[i] = 0.f;
     __syncthreads();
     CT dlg, dlb;
     ct_zero(dlg);
@@ -614,16 +647,16 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
     const int g = lane >> 4;
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
-      const int rt = c.wave + 4 * k;
+      const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         const bool ok = tok_ok(rt, c);
         int tk;
-        const CT pre = dec_embed_pre_ct(p, rt, tk, c);
+        const CT pre = dec_embed_pre_ct<CONT>(p, rt, tk, c);
         CT e = pre, xh, yy, de;
         gelu_ct(e);
         const float rs = ln_fwd_ct(e, xh, yy, gam, bet);
         ln_bwd_ct(dx[k], xh, rs, gam, ok, de, dlg, dlb);
-        if (ok && p.cont) {   // EMB[k][f] += d pre_f * a_prev_k (k < A), EMB[A][f] += d pre_f (bias)
+        if (ok && CONT) {   // EMB[k][f] += d pre_f * a_prev_k (k < A), EMB[A][f] += d pre_f (bias)
           const int row = rt * 16 + (lane & 15);
           const bool first = row % c.L == 0;
           const float* prev = p.act + (size_t)(c.tok0 + (first ? 0 : row - 1)) * p.A;
@@ -649,14 +682,14 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
     flush_vec(dlg, c.g(p.d_lnd_g), lane);
     flush_vec(dlb, c.g(p.d_lnd_b), lane);
     __syncthreads();
-    if (p.cont) {   // W_a [64][A] and b_a
-      for (int i = c.tid; i < (p.A + 1) * 64; i += 256) {
+    if (CONT) {   // W_a [64][A] and b_a
+      for (int i = c.tid; i < (p.A + 1) * 64; i += NTHR) {
         const int t = i / 64, col = i % 64;
         if (t < p.A) { if (p.d_wa) atomicAdd(c.g(p.d_wa) + col * p.A + t, EMB[i]); }
         else if (p.d_ba) atomicAdd(c.g(p.d_ba) + col, EMB[i]);
       }
     } else if (p.d_wa)
-      for (int i = c.tid; i < (p.A + 1) * 64; i += 256) {
+      for (int i = c.tid; i < (p.A + 1) * 64; i += NTHR) {
         const int t = i / 64, col = i % 64;
         atomicAdd(c.g(p.d_wa) + col * (p.A + 1) + t, EMB[i]);
       }
@@ -664,43 +697,52 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
   CP_MARK(30);
 }
 
-template <int NB, int MA>
-__global__ __launch_bounds__(256, WGPC) void mat_dec_bwd_ct(DecP p) {
+#ifdef MDL_CT_BWD_TU
+template <int NB, int MA, bool CONT>
+__global__ __launch_bounds__(NTHR, WGPC) void mat_dec_bwd_ct(DecP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   CP_BEGIN();
-  FOR_TILES(p, (dec_bwd_tile<NB, MA>(p, smem, s0, ns)));
+  FOR_TILES(p, (dec_bwd_tile<NB, MA, CONT>(p, smem, s0, ns)));
   CP_END();
 }
 
+#endif  // MDL_CT_BWD_TU
+
 }  // namespace
 
-template <int MA>
+#ifndef MDL_CT_BWD_TU
+template <int MA, bool CONT>
 static int dec_fwd_ct(const DecP* p, int NB, int save, hipStream_t st) {
-  if (NB == 1) return save ? launch_ct(mat_dec_fwd_ct<1, true, MA>, p, true, st) : launch_ct(mat_dec_fwd_ct<1, false, MA>, p, true, st);
-  if (NB == 2) return save ? launch_ct(mat_dec_fwd_ct<2, true, MA>, p, true, st) : launch_ct(mat_dec_fwd_ct<2, false, MA>, p, true, st);
-  if (NB == 3) return save ? launch_ct(mat_dec_fwd_ct<3, true, MA>, p, true, st) : launch_ct(mat_dec_fwd_ct<3, false, MA>, p, true, st);
+  if (NB == 1) return save ? launch_ct(mat_dec_fwd_ct<1, true, MA, CONT>, p, true, st) : launch_ct(mat_dec_fwd_ct<1, false, MA, CONT>, p, true, st);
+  if (NB == 2) return save ? launch_ct(mat_dec_fwd_ct<2, true, MA, CONT>, p, true, st) : launch_ct(mat_dec_fwd_ct<2, false, MA, CONT>, p, true, st);
+  if (NB == 3) return save ? launch_ct(mat_dec_fwd_ct<3, true, MA, CONT>, p, true, st) : launch_ct(mat_dec_fwd_ct<3, false, MA, CONT>, p, true, st);
   return -3;
 }
-template <int MA>
-static int dec_bwd_ct(const DecP* p, int NB, hipStream_t st) {
-  if (NB == 1) return launch_ct(mat_dec_bwd_ct<1, MA>, p, false, st);
-  if (NB == 2) return launch_ct(mat_dec_bwd_ct<2, MA>, p, false, st);
-  if (NB == 3) return launch_ct(mat_dec_bwd_ct<3, MA>, p, false, st);
-  return -3;
-}
-
+// MA = logit tiles of the action head (1: A <= 16, 4: A <= 64); the continuous action type is its own instantiation
+// (its Normal-head / Linear-embedding code kept out of the discrete kernels' instruction stream)
 MDL_API int mdl_mat_dec_fwd_ct(const DecP* p, int NB, int save, hipStream_t st) {
   if (p->A > 64 || p->A < 1) return -1;
-  return p->A <= 16 ? dec_fwd_ct<1>(p, NB, save, st) : dec_fwd_ct<4>(p, NB, save, st);
+  if (p->cont) return p->A <= 16 ? dec_fwd_ct<1, true>(p, NB, save, st) : dec_fwd_ct<4, true>(p, NB, save, st);
+  return p->A <= 16 ? dec_fwd_ct<1, false>(p, NB, save, st) : dec_fwd_ct<4, false>(p, NB, save, st);
+}
+#else
+template <int MA, bool CONT>
+static int dec_bwd_ct(const DecP* p, int NB, hipStream_t st) {
+  if (NB == 1) return launch_ct(mat_dec_bwd_ct<1, MA, CONT>, p, false, st);
+  if (NB == 2) return launch_ct(mat_dec_bwd_ct<2, MA, CONT>, p, false, st);
+  if (NB == 3) return launch_ct(mat_dec_bwd_ct<3, MA, CONT>, p, false, st);
+  return -3;
 }
 
 MDL_API int mdl_mat_dec_bwd_ct(const DecP* p, int NB, hipStream_t st) {
   if (p->A > 64 || p->A < 1 || 2 * p->NRP * 128 < (p->A + 1) * 256) return -1;
-  return p->A <= 16 ? dec_bwd_ct<1>(p, NB, st) : dec_bwd_ct<4>(p, NB, st);
+  if (p->cont) return p->A <= 16 ? dec_bwd_ct<1, true>(p, NB, st) : dec_bwd_ct<4, true>(p, NB, st);
+  return p->A <= 16 ? dec_bwd_ct<1, false>(p, NB, st) : dec_bwd_ct<4, false>(p, NB, st);
 }
+#endif  // MDL_CT_BWD_TU
 
 #ifdef MDL_CT_PROF
-MDL_API int mdl_ctprof_dec(unsigned long long* out, int reset) {
+MDL_API int MDL_CAT(mdl_ctprof_dec, MDL_CT_TU_SUFFIX)(unsigned long long* out, int reset) {
   if (reset) {
     unsigned long long z[64] = {0};
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_ctprof), z, sizeof(z));

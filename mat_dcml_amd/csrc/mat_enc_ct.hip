@@ -105,7 +105,7 @@ __device__ __forceinline__ void enc_fwd_tile(const EncP& p, const EncX& ex, char
     const CT gam = ld_vec(p.ln0_g, lane), bet = ld_vec(p.ln0_b, lane);
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
-      const int rt = c.wave + 4 * k;
+      const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         float oh[4], hat[4];
         CT pre = embed_pre(p, ex, rt, W, oh, hat, c), xh;
@@ -132,7 +132,7 @@ __device__ __forceinline__ void enc_fwd_tile(const EncP& p, const EncX& ex, char
   if (p.n_obj > 1) w1 = ld_vec(p.wh2 + 64, lane); else ct_zero(w1);
 #pragma unroll
   for (int k = 0; k < MAXRT; ++k) {
-    const int rt = c.wave + 4 * k;
+    const int rt = c.wave + NW * k;
     if (rt < c.NT) {
       const bool ok = tok_ok(rt, c);
       if (p.rep) st_gf(p.rep, c.tok0, rt, c.NR, xr[k], lane);
@@ -160,13 +160,16 @@ __device__ __forceinline__ void enc_fwd_tile(const EncP& p, const EncX& ex, char
   CP_MARK(27);
 }
 
+#ifndef MDL_CT_BWD_TU
 template <int NB, bool SAVE>
-__global__ __launch_bounds__(256, FWD_WGPC) void mat_enc_fwd_ct(EncP p, EncX ex) {
+__global__ __launch_bounds__(NTHR, FWD_WGPC) void mat_enc_fwd_ct(EncP p, EncX ex) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   CP_BEGIN();
   FOR_TILES(p, (enc_fwd_tile<NB, SAVE>(p, ex, smem, s0, ns)));
   CP_END();
 }
+
+#endif  // !MDL_CT_BWD_TU
 
 // ============================================================================================== backward
 template <int NB>
@@ -185,30 +188,41 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
     ct_zero(dlb);
     ct_zero(dw0);
     ct_zero(dw1);
-    AFr Hf, Hb;
-    loadA(Hf, p.h1.fa, lane);
-    loadA(Hb, p.h1.ba, lane);
-    const CT bh = ld_vec(p.h1.b, lane), gam = ld_vec(p.lnh.g, lane), bet = ld_vec(p.lnh.b, lane);
+    CT hhs[MAXRT];   // head1 pre-activations (first pass: W_h1 and its bias are dead before the LN work)
+    {
+      AFr Hf;
+      loadA(Hf, p.h1.fa, lane);
+      const CT bh = ld_vec(p.h1.b, lane);
+      CT reps[MAXRT];
+#pragma unroll
+      for (int k = 0; k < MAXRT; ++k) {   // every tile's encoder output requested up front (one latency, not three)
+        const int rt = c.wave + NW * k;
+        if (rt < c.NT) reps[k] = ld_gf(p.rep, c.tok0, rt, c.NR, lane);
+      }
+#pragma unroll
+      for (int k = 0; k < MAXRT; ++k) {
+        const int rt = c.wave + NW * k;
+        if (rt < c.NT) {
+          const CTr r = ct_pack(reps[k]);
+          st_lds(c.XB, rt, r, tok_ok(rt, c), lane);   // X of W_h1
+          hhs[k] = bh;
+          mm(hhs[k], Hf, r);
+        }
+      }
+    }
+    const CT gam = ld_vec(p.lnh.g, lane), bet = ld_vec(p.lnh.b, lane);
     const CT w0 = ld_vec(p.wh2, lane);
     CT w1;
     if (p.n_obj > 1) w1 = ld_vec(p.wh2 + 64, lane); else ct_zero(w1);
-    CT reps[MAXRT];
-#pragma unroll
-    for (int k = 0; k < MAXRT; ++k) {   // every tile's encoder output requested up front (one latency, not three)
-      const int rt = c.wave + 4 * k;
-      if (rt < c.NT) reps[k] = ld_gf(p.rep, c.tok0, rt, c.NR, lane);
-    }
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
-      const int rt = c.wave + 4 * k;
+      const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         const bool ok = tok_ok(rt, c);
         const size_t tok = (size_t)(c.tok0 + (ok ? rt * 16 + (lane & 15) : 0));
         const float dv0 = ok ? p.dv[tok * p.n_obj] : 0.f;
         const float dv1 = (ok && p.n_obj > 1) ? p.dv[tok * p.n_obj + 1] : 0.f;
-        const CTr r = ct_pack(reps[k]);
-        CT hh = bh;
-        mm(hh, Hf, r);
+        const CT& hh = hhs[k];
         CT gl = hh, xh, n, dn, dg;
         gelu_ct(gl);
         const float rs = ln_fwd_ct(gl, xh, n, gam, bet);
@@ -225,12 +239,20 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int q = 0; q < 4; ++q) dg.v[i][q] = ok ? dg.v[i][q] * gelu_erf_grad(hh.v[i][q]) : 0.f;
-        const CTr dgr = ct_pack(dg);
-        st_lds(c.DQ, rt, dgr, ok, lane);   // dY of W_h1
-        st_lds(c.XB, rt, r, ok, lane);     // X of W_h1
-        CT t = ld_gf(p.drep, c.tok0, rt, c.NR, lane);   // issued before the LN/GELU work of this tile
-        mm(t, Hb, dgr);
-        dx[k] = t;
+        st_lds(c.DQ, rt, ct_pack(dg), ok, lane);   // dY of W_h1
+      }
+    }
+    {   // second pass (W_h1ᵀ): dx = d rep (from the decoder) + W_h1ᵀ dY
+      AFr Hb;
+      loadA(Hb, p.h1.ba, lane);
+#pragma unroll
+      for (int k = 0; k < MAXRT; ++k) {
+        const int rt = c.wave + NW * k;
+        if (rt < c.NT) {
+          CT t = ld_gf(p.drep, c.tok0, rt, c.NR, lane);
+          mm(t, Hb, ld_lds(c.DQ, rt, lane));
+          dx[k] = t;
+        }
       }
     }
     flush_vec(dlg, c.g(p.lnh.dg), lane);
@@ -266,7 +288,7 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
     const CT gam = ld_vec(p.ln0_g, lane), bet = ld_vec(p.ln0_b, lane);
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
-      const int rt = c.wave + 4 * k;
+      const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         const bool ok = tok_ok(rt, c);
         float oh[4] = {0.f, 0.f, 0.f, 0.f}, hat[4] = {0.f, 0.f, 0.f, 0.f};
@@ -329,17 +351,21 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
   CP_MARK(30);
 }
 
+#ifdef MDL_CT_BWD_TU
 template <int NB>
-__global__ __launch_bounds__(256, WGPC) void mat_enc_bwd_ct(EncP p, EncX ex) {
+__global__ __launch_bounds__(NTHR, WGPC) void mat_enc_bwd_ct(EncP p, EncX ex) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   CP_BEGIN();
   FOR_TILES(p, (enc_bwd_tile<NB>(p, ex, smem, s0, ns)));
   CP_END();
 }
 
+#endif  // MDL_CT_BWD_TU
+
 }  // namespace
 
 // ============================================================================================== host API
+#ifndef MDL_CT_BWD_TU
 MDL_API int mdl_mat_train_geometry_ct(int L) {
   const int MAXROWS = 64 * MAXRT;
   int SQ = MAXROWS / L;
@@ -364,6 +390,7 @@ MDL_API int mdl_mat_enc_fwd_ct(const EncP* p, const float* pre_in, int NB, int s
   return -3;
 }
 
+#else
 MDL_API int mdl_mat_enc_bwd_ct(const EncP* p, const float* pre_in, float* dpre_out, int NB, hipStream_t st) {
   if ((!pre_in && (p->od > 16 || p->od < 1)) || p->n_obj > 2 || p->n_obj < 1 || (pre_in && !dpre_out)) return -1;
   const EncX ex{pre_in, dpre_out};
@@ -372,9 +399,10 @@ MDL_API int mdl_mat_enc_bwd_ct(const EncP* p, const float* pre_in, float* dpre_o
   if (NB == 3) return launch_ct(mat_enc_bwd_ct<3>, p, false, st, ex);
   return -3;
 }
+#endif  // MDL_CT_BWD_TU
 
 #ifdef MDL_CT_PROF
-MDL_API int mdl_ctprof_enc(unsigned long long* out, int reset) {
+MDL_API int MDL_CAT(mdl_ctprof_enc, MDL_CT_TU_SUFFIX)(unsigned long long* out, int reset) {
   if (reset) {
     unsigned long long z[64] = {0};
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_ctprof), z, sizeof(z));

@@ -47,7 +47,12 @@ __device__ unsigned long long g_tprof[32];
 #define TP_MARK(k) do { } while (0)
 #endif
 
-constexpr int MAXRT = MDL_MAXRT;  // row tiles per wave (NT <= 4 * MAXRT)
+#ifndef MDL_NW
+#define MDL_NW 4     // waves per workgroup (the round-2 backward translation units build with 8)
+#endif
+constexpr int NW = MDL_NW;
+constexpr int NTHR = 64 * NW;
+constexpr int MAXRT = MDL_MAXRT;  // row tiles per wave (NT <= NW * MAXRT; wave w owns tiles w, w + NW, ...)
 constexpr int WGPC = MDL_WGPC;
 constexpr int LDS_BUDGET = 160 * 1024 / WGPC;
 
@@ -209,7 +214,7 @@ __device__ __forceinline__ SeqSpan tile_span(int t16, const Ctx& c, bool causal_
 __device__ __forceinline__ void attn_fwd(const bf16_t* Q, const bf16_t* K, const bf16_t* V, bf16_t* O, bool causal, float* lse_g,
                                          const Ctx& c) {
   const int lane = c.lane, g = lane >> 4, c16 = lane & 15;
-  for (int item = c.wave; item < 2 * c.NT; item += 4) {
+  for (int item = c.wave; item < 2 * c.NT; item += NW) {
     const int qt = item >> 1, h = item & 1;
     const int q = qt * 16 + c16;
     const bool qv = q < c.NR;
@@ -283,7 +288,7 @@ __device__ __forceinline__ void attn_bwd_q(const bf16_t* Q, const bf16_t* K, con
   return;
 #endif
   const int lane = c.lane, g = lane >> 4, c16 = lane & 15;
-  for (int item = c.wave; item < 2 * c.NT; item += 4) {
+  for (int item = c.wave; item < 2 * c.NT; item += NW) {
     const int qt = item >> 1, h = item & 1;
     const int q = qt * 16 + c16;
     const bool qv = q < c.NR;
@@ -339,7 +344,7 @@ __device__ __forceinline__ void attn_bwd_kv(const bf16_t* Q, bf16_t* K, bf16_t* 
   return;
 #endif
   const int lane = c.lane, g = lane >> 4, c16 = lane & 15;
-  for (int item = c.wave; item < 2 * c.NT; item += 4) {
+  for (int item = c.wave; item < 2 * c.NT; item += NW) {
     const int kt = item >> 1, h = item & 1;
     const int k = kt * 16 + c16;
     const bool kv = k < c.NR;
@@ -395,7 +400,7 @@ __device__ __forceinline__ void attn_bwd_kv(const bf16_t* Q, bf16_t* K, bf16_t* 
 
 // saved per-row log-sum-exp ([tok][2] global) -> LDS [head][NRP]
 __device__ __forceinline__ void load_lse(const float* sv_lse, const Ctx& c) {
-  for (int i = c.tid; i < 2 * c.NRP; i += 256) {
+  for (int i = c.tid; i < 2 * c.NRP; i += NTHR) {
     const int h = i / c.NRP, row = i - h * c.NRP;
     c.LSE[i] = row < c.NR ? sv_lse[(size_t)(c.tok0 + row) * 2 + h] : 0.f;
   }
@@ -428,7 +433,7 @@ __device__ __forceinline__ void g2tiles(bf16_t* buf0, const bf16_t* src0, bf16_t
   uint4 v0[MAXRT][2], v1[MAXRT][2];
 #pragma unroll
   for (int k = 0; k < MAXRT; ++k) {
-    const int rt = c.wave + 4 * k;
+    const int rt = c.wave + NW * k;
 #pragma unroll
     for (int ii = 0; ii < 2; ++ii) {
       const int i = c.lane + 64 * ii, row = rt * 16 + (i >> 3), lc = i & 7;
@@ -440,7 +445,7 @@ __device__ __forceinline__ void g2tiles(bf16_t* buf0, const bf16_t* src0, bf16_t
   }
 #pragma unroll
   for (int k = 0; k < MAXRT; ++k) {
-    const int rt = c.wave + 4 * k;
+    const int rt = c.wave + NW * k;
     if (rt < c.NT) {
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii) {
@@ -470,7 +475,7 @@ __device__ __forceinline__ void gelu_rt(RT& t) {
 }
 
 __device__ __forceinline__ void zero_lds(char* smem, size_t bytes, int tid) {
-  for (size_t i = (size_t)tid * 16; i < bytes; i += 256 * 16) *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
+  for (size_t i = (size_t)tid * 16; i < bytes; i += NTHR * 16) *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
 }
 
 __device__ __forceinline__ void flush_ln(f32x4 dg, f32x4 db, const LNp& ln, const Ctx& c) {
@@ -485,7 +490,7 @@ __device__ __forceinline__ void attn_self_fwd(const Mat* m, const LNp& ln, RT* x
   const int lane = c.lane;
 #pragma unroll
   for (int k = 0; k < MAXRT; ++k) {
-    const int rt = c.wave + 4 * k;
+    const int rt = c.wave + NW * k;
     if (rt < c.NT) {
       st_tm_m(c.XB, rt, xr[k], row_mask(rt, c.NR, lane), lane);
       if (SAVE) { wave_lds_sync(); tile2g(sv_xin, c.XB, rt, c); }
@@ -499,7 +504,7 @@ __device__ __forceinline__ void attn_self_fwd(const Mat* m, const LNp& ln, RT* x
     loadB(B, m[mi].fw, lane);
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
-      const int rt = c.wave + 4 * k;
+      const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         RT t;
         gemm_rt(t, c.XB, rt, B, lane, false);
@@ -515,7 +520,7 @@ __device__ __forceinline__ void attn_self_fwd(const Mat* m, const LNp& ln, RT* x
   loadB(B, m[3].fw, lane);
 #pragma unroll
   for (int k = 0; k < MAXRT; ++k) {
-    const int rt = c.wave + 4 * k;
+    const int rt = c.wave + NW * k;
     if (rt < c.NT) {
       if (SAVE) tile2g(sv_a, c.QB, rt, c);
       RT t, xh, y;
@@ -539,7 +544,7 @@ __device__ __forceinline__ void mlp_fwd(const Mat& m1, const Mat& m2, const LNp&
   loadB(B2, m2.fw, lane);
 #pragma unroll
   for (int k = 0; k < MAXRT; ++k) {
-    const int rt = c.wave + 4 * k;
+    const int rt = c.wave + NW * k;
     if (rt < c.NT) {
       const f32x4 vm = row_mask(rt, c.NR, lane);
       st_tm_m(c.XB, rt, xr[k], vm, lane);
@@ -656,7 +661,7 @@ __device__ __forceinline__ void mlp_bwd(const Mat& m1, const Mat& m2, const LNp&
     g2tiles(c.QB, sv_x, c.XB, sv_h, c);     // QB rows = X of dW1, XB = pre-GELU h
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
-      const int rt = c.wave + 4 * k;
+      const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         const f32x4 vm = row_mask(rt, c.NR, lane);
         RT x, h, gl;
@@ -716,7 +721,7 @@ __device__ __forceinline__ void attn_self_bwd(const Mat* m, const LNp& ln, RT* d
     g2tiles(c.XB, sv_a, c.DA, sv_xin, c);  // XB = attention output (X of dWp), DA = block input
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
-      const int rt = c.wave + 4 * k;
+      const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         const f32x4 vm = row_mask(rt, c.NR, lane);
         RT a, xin;
@@ -758,7 +763,7 @@ __device__ __forceinline__ void attn_self_bwd(const Mat* m, const LNp& ln, RT* d
       loadB(B, m[mi].fw, lane);
 #pragma unroll
       for (int k = 0; k < MAXRT; ++k) {
-        const int rt = c.wave + 4 * k;
+        const int rt = c.wave + NW * k;
         if (rt < c.NT) {
           RT t;
           gemm_rt(t, c.XB, rt, B, lane, false);
@@ -788,7 +793,7 @@ __device__ __forceinline__ void attn_self_bwd(const Mat* m, const LNp& ln, RT* d
     f32x4 dbb = {0, 0, 0, 0};
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
-      const int rt = c.wave + 4 * k;
+      const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         const f32x4 vm = row_mask(rt, c.NR, lane);
         RT g, t;
@@ -867,14 +872,14 @@ static int n_cus() {
 
 template <typename K, typename PT>
 static int launch(K kern, const PT* p, hipStream_t st) {
-  if (p->SQ <= 0 || p->NRP <= 0 || (p->SQ * p->L + 15) / 16 > 4 * MAXRT) return -4;   // geometry not valid here
+  if (p->SQ <= 0 || p->NRP <= 0 || (p->SQ * p->L + 15) / 16 > NW * MAXRT) return -4;   // geometry not valid here
   const size_t lds = mat_train_lds_bytes(p->NRP, p->SQ, p->L);
   if (lds > LDS_BUDGET) return -2;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return (int)e;
   const int tiles = (p->Bs + p->SQ - 1) / p->SQ;
   const int grid = tiles < n_cus() * WGPC ? tiles : n_cus() * WGPC;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, *p);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(NTHR), lds, st, *p);
   MDL_CHECK_LAUNCH();
   return 0;
 }

@@ -23,6 +23,14 @@
 #pragma once
 #include "mat_train_common.h"
 
+// The backward kernels build in their own translation units (mat_enc_ct_bwd.hip / mat_dec_ct_bwd.hip: 8 waves per
+// workgroup); per-TU exported names (the phase-profiler readers) carry this suffix.
+#ifdef MDL_CT_BWD_TU
+#define MDL_CT_TU_SUFFIX _bwd
+#else
+#define MDL_CT_TU_SUFFIX
+#endif
+
 namespace {
 
 // Phase profiler (-DMDL_CT_PROF): thread 0 of EVERY workgroup accumulates s_memtime cycles between marks (placed
@@ -49,14 +57,14 @@ __host__ __device__ inline size_t ct_fwd_lds_bytes(int NRP) { return (size_t)NRP
 
 template <typename K, typename PT, typename... X>
 static int launch_ct(K kern, const PT* p, bool fwd, hipStream_t st, X... extra) {
-  if (p->SQ <= 0 || p->NRP <= 0 || (p->SQ * p->L + 15) / 16 > 4 * MAXRT) return -4;   // geometry not valid here
+  if (p->SQ <= 0 || p->NRP <= 0 || (p->SQ * p->L + 15) / 16 > NW * MAXRT) return -4;   // geometry not valid here
   const size_t lds = fwd ? ct_fwd_lds_bytes(p->NRP) : mat_train_lds_bytes(p->NRP, p->SQ, p->L);
   if (lds > (fwd ? LDS_BUDGET / FWD_WGPC : LDS_BUDGET)) return -2;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return (int)e;
   const int tiles = (p->Bs + p->SQ - 1) / p->SQ;
   const int cap = n_cus() * (fwd ? FWD_WGPC : 1);
-  hipLaunchKernelGGL(kern, dim3(tiles < cap ? tiles : cap), dim3(256), lds, st, *p, extra...);
+  hipLaunchKernelGGL(kern, dim3(tiles < cap ? tiles : cap), dim3(NTHR), lds, st, *p, extra...);
   MDL_CHECK_LAUNCH();
   return 0;
 }
@@ -275,56 +283,88 @@ __device__ __forceinline__ void ln_bwd_ct(const CT& dy, const CT& xh, float rstd
 
 // per-lane feature partials (summed over the tokens the lane saw) -> one atomic per feature: reduce over the 16
 // token lanes of each row (DPP), then lane (g, c) adds feature 16(c>>2) + 4g + (c&3)
+// Σ over the 16 tokens (lanes) of a row of 16 per-lane values, reduce-scattered: lane c ends with the sum of value c.
+// Four butterfly steps (row mirror, half-row mirror, xor 2, xor 1) each halve the values a lane carries — 15 DPP
+// adds instead of 16 full 16-lane reductions (64).
+__device__ __forceinline__ float row_reduce_scatter16(const float (&v)[16], int lane) {
+  const int c = lane & 15;
+  float a[8], b[4], d[2];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const bool hi = c & 8;
+    a[k] = (hi ? v[8 + k] : v[k]) + dppf<DPP_ROW_MIRROR>(hi ? v[k] : v[8 + k]);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const bool hi = c & 4;
+    b[k] = (hi ? a[4 + k] : a[k]) + dppf<DPP_ROW_HALF_MIRROR>(hi ? a[k] : a[4 + k]);
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const bool hi = c & 2;
+    d[k] = (hi ? b[2 + k] : b[k]) + dppf<DPP_XOR2>(hi ? b[k] : b[2 + k]);
+  }
+  const bool hi = c & 1;
+  return (hi ? d[1] : d[0]) + dppf<DPP_XOR1>(hi ? d[0] : d[1]);
+}
+
+// column sums of a CT accumulator (Σ over the 16 tokens of the lane row, then the 4 rows by the atomics) -> dst[64]
 __device__ __forceinline__ void flush_vec(const CT& acc, float* dst, int lane) {
   if (!dst) return;
   const int c = lane & 15, g = lane >> 4;
-  float out = 0.f;
+  float v[16];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float s = group_sum<16>(acc.v[i][r]);
-      out = (c == 4 * i + r) ? s : out;
-    }
-  atomicAdd(dst + 16 * (c >> 2) + 4 * g + (c & 3), out);
+    for (int r = 0; r < 4; ++r) v[4 * i + r] = acc.v[i][r];
+  atomicAdd(dst + 16 * (c >> 2) + 4 * g + (c & 3), row_reduce_scatter16(v, lane));
 }
 
 // ------------------------------------------------------------------------------------------ weight gradients
 // dW[n][k] (row stride ld) += Σ_t Y[t][n] X[t][k] for n < nrows, k < ncols, and db[n] += Σ_t Y[t][n], from
-// token-major swizzled LDS tiles of KP rows (KP % 32 == 0, padded rows zero).  Wave w owns dW rows [16w, 16w+16).
-// The bias gradient is one extra MFMA per k-step against a ones fragment.  fp32 atomics.
+// token-major swizzled LDS tiles of KP rows (KP % 32 == 0, padded rows zero).  Wave w owns dW rows
+// [16(w&3), 16(w&3)+16) and 16/NW of the 4 column tiles (all four at 4 waves, two at 8).  The bias gradient is one
+// extra MFMA per k-step against a ones fragment (waves of the first column group).  fp32 atomics.
 __device__ __forceinline__ void wgrad_g(const bf16_t* Y, const bf16_t* X, int KP, float* dW, int ld, int nrows, int ncols,
                                         float* db, int wave, int lane) {
-  if ((!dW && !db) || 16 * wave >= nrows) return;
-  const int g = lane >> 4, c16 = lane & 15;
+  constexpr int NCT = 16 / NW;                      // column tiles per wave
+  const int rb = wave & 3, ct0 = (wave >> 2) * NCT;
+  if (ct0 > 0) db = nullptr;
   const int nct = dW ? (ncols + 15) >> 4 : 0;
-  RT acc;
-  rt_zero(acc);
+  if ((!db && ct0 >= nct) || 16 * rb >= nrows) return;
+  const int g = lane >> 4, c16 = lane & 15;
+  f32x4 acc[NCT];
+#pragma unroll
+  for (int j = 0; j < NCT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 accb = {0.f, 0.f, 0.f, 0.f};
   const bf16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
   for (int k0 = 0; k0 < KP; k0 += 32) {
-    const bf16x8 a = ld_frag_T(Y, k0, 16 * wave, lane);
+    const bf16x8 a = ld_frag_T(Y, k0, 16 * rb, lane);
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {
-      if (ct < nct) {
-        const bf16x8 b = ld_frag_T(X, k0, 16 * ct, lane);
-        acc.v[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc.v[ct], 0, 0, 0);
+    for (int j = 0; j < NCT; ++j) {
+      if (ct0 + j < nct) {
+        const bf16x8 b = ld_frag_T(X, k0, 16 * (ct0 + j), lane);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[j], 0, 0, 0);
       }
     }
     if (db) accb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ones, accb, 0, 0, 0);
   }
   if (dW) {
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct)
+    for (int j = 0; j < NCT; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int n = 16 * wave + 4 * g + r, k = 16 * ct + c16;
-        if (ct < nct && n < nrows && k < ncols) atomicAdd(dW + n * ld + k, acc.v[ct][r]);
+        const int n = 16 * rb + 4 * g + r, k = 16 * (ct0 + j) + c16;
+#ifdef MDL_ABLATE_WGRAD_ATOMIC   // timing experiment only: plain stores instead of the fp32 atomics (wrong sums)
+        if (ct0 + j < nct && n < nrows && k < ncols) dW[n * ld + k] = acc[j][r];
+#else
+        if (ct0 + j < nct && n < nrows && k < ncols) atomicAdd(dW + n * ld + k, acc[j][r]);
+#endif
       }
   }
   if (db && c16 < 4) {
     const float v = c16 == 0 ? accb[0] : c16 == 1 ? accb[1] : c16 == 2 ? accb[2] : accb[3];
-    const int n = 16 * wave + 4 * g + c16;
+    const int n = 16 * rb + 4 * g + c16;
     if (n < nrows) atomicAdd(db + n, v);
   }
 }
@@ -343,7 +383,7 @@ __device__ __forceinline__ void proj3(const Mat* m, int m0, const CTr* xp, const
     const CT b = ld_vec(m[m0 + mi].b, c.lane);
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
-      const int rt = c.wave + 4 * k;
+      const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         CT t = b;
         mm(t, W, xp[k]);
@@ -363,7 +403,7 @@ __device__ __forceinline__ void proj3_bwd(const Mat* m, int m0, const bf16_t* s0
     loadA(W, m[m0 + mi].ba, c.lane);
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
-      const int rt = c.wave + 4 * k;
+      const int rt = c.wave + NW * k;
       if (rt < c.NT) mm(mi == 0 ? d0[k] : d12[k], W, ld_lds(srcs[mi], rt, c.lane));
     }
   }
@@ -413,13 +453,16 @@ __device__ __forceinline__ void split8v(const float* x, bf16x8& hi, bf16x8& lo) 
   lo = mk8(l[0], l[1], l[2], l[3]);
 }
 
-// forward: O (CT, the wave's query tiles rt = wave + 4k, both heads) = softmax(scale Q Kᵀ) V
+// forward: O (CT, the wave's query tiles rt = wave + NW k, both heads) = softmax(scale Q Kᵀ) V
 __device__ __forceinline__ void attn_fwd_ct(const bf16_t* Q, const bf16_t* K, const bf16_t* V, bool causal, float* lse_g,
                                             CT* O, const Ctx& c) {
+#ifdef MDL_ABLATE_ATTN
+  return;
+#endif
   const int lane = c.lane, g = lane >> 4, c16 = lane & 15;
 #pragma unroll
   for (int k = 0; k < MAXRT; ++k) {
-    const int rt = c.wave + 4 * k;
+    const int rt = c.wave + NW * k;
     if (rt < c.NT) {
       const int q = rt * 16 + c16;
       const QSpan qs = qspan(q, causal, c);
@@ -480,8 +523,11 @@ __device__ __forceinline__ void st_lds_head(bf16_t* buf, int rt, int h, f32x4 a,
 // the backward kernels' code and register pressure).
 __device__ __forceinline__ void attn_bwd_q_ct(const bf16_t* Q, const bf16_t* K, const bf16_t* V, const bf16_t* DA,
                                               bf16_t* DQ, bool causal, const Ctx& c) {
+#ifdef MDL_ABLATE_ATTN
+  return;
+#endif
   const int lane = c.lane, g = lane >> 4, c16 = lane & 15;
-  for (int item = c.wave; item < 2 * c.NT; item += 4) {
+  for (int item = c.wave; item < 2 * c.NT; item += NW) {
     const int rt = item >> 1, h = item & 1;
     const int q = rt * 16 + c16;
     const QSpan qs = qspan(q, causal, c);
@@ -520,8 +566,11 @@ __device__ __forceinline__ void attn_bwd_q_ct(const bf16_t* Q, const bf16_t* K, 
 // backward, by (key tile, head) item: dV = Pᵀ dO, dK = scale dSᵀ Q, written over the item's own K / V head columns
 __device__ __forceinline__ void attn_bwd_kv_ct(const bf16_t* Q, bf16_t* K, bf16_t* V, const bf16_t* DA, bool causal,
                                                const Ctx& c) {
+#ifdef MDL_ABLATE_ATTN
+  return;
+#endif
   const int lane = c.lane, g = lane >> 4, c16 = lane & 15;
-  for (int item = c.wave; item < 2 * c.NT; item += 4) {
+  for (int item = c.wave; item < 2 * c.NT; item += NW) {
     const int rt = item >> 1, h = item & 1;
     const int kk = rt * 16 + c16;
     const bool kv = kk < c.NR;
@@ -577,7 +626,7 @@ __device__ __forceinline__ void self_attn_fwd_ct(const Mat* m, const LNp& ln, CT
     CTr xp[MAXRT];
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
-      const int rt = c.wave + 4 * k;
+      const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         xp[k] = ct_pack(xr[k]);
         if (SAVE) st_g(sv_xin, c.tok0, rt, c.NR, xp[k], lane);
@@ -596,7 +645,7 @@ __device__ __forceinline__ void self_attn_fwd_ct(const Mat* m, const LNp& ln, CT
   const CT bp = ld_vec(m[3].b, lane), gam = ld_vec(ln.g, lane), bet = ld_vec(ln.b, lane);
 #pragma unroll
   for (int k = 0; k < MAXRT; ++k) {
-    const int rt = c.wave + 4 * k;
+    const int rt = c.wave + NW * k;
     if (rt < c.NT) {
       const CTr a = ct_pack(O[k]);
       if (SAVE) st_g(sv_a, c.tok0, rt, c.NR, a, lane);
@@ -618,7 +667,7 @@ __device__ __forceinline__ void mlp_fwd_ct(const Mat& m1, const Mat& m2, const L
   const CT b1 = ld_vec(m1.b, lane), b2 = ld_vec(m2.b, lane), gam = ld_vec(ln.g, lane), bet = ld_vec(ln.b, lane);
 #pragma unroll
   for (int k = 0; k < MAXRT; ++k) {
-    const int rt = c.wave + 4 * k;
+    const int rt = c.wave + NW * k;
     if (rt < c.NT) {
       const CTr x = ct_pack(xr[k]);
       if (SAVE) st_g(sv_x, c.tok0, rt, c.NR, x, lane);
@@ -635,22 +684,23 @@ __device__ __forceinline__ void mlp_fwd_ct(const Mat& m1, const Mat& m2, const L
 }
 
 // ------------------------------------------------------------------------------------------ sublayers (backward)
+// Backward sublayers run in passes with ONE weight matrix live at a time (the 8-wave backward keeps every wave
+// under 256 registers): each pass leaves its per-tile products in this wave's own LDS rows (read back by the same
+// lanes, so no barrier between passes) or in dx.
 __device__ __forceinline__ void mlp_bwd_ct(const Mat& m1, const Mat& m2, const LNp& ln, CT* dx, const bf16_t* sv_x,
                                            const bf16_t* sv_h, const Ctx& c) {
   const int lane = c.lane;
-  CT dlg, dlb;
-  ct_zero(dlg);
-  ct_zero(dlb);
-  {
-    AFr W2f, W2b, W1b;
+  {   // pass 1 (W2): LN backward -> ds (dx) ; DA = dY of W2, XB = X of W2 (GELU(h))
+    CT dlg, dlb;
+    ct_zero(dlg);
+    ct_zero(dlb);
+    AFr W2f;
     loadA(W2f, m2.fa, lane);
-    loadA(W2b, m2.ba, lane);
-    loadA(W1b, m1.ba, lane);
     const CT b2 = ld_vec(m2.b, lane), gam = ld_vec(ln.g, lane), bet = ld_vec(ln.b, lane);
     CTr xs[MAXRT], hs[MAXRT];
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {   // every saved-activation load of the wave issued up front
-      const int rt = c.wave + 4 * k;
+      const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         xs[k] = ld_g(sv_x, c.tok0, rt, c.NR, lane);
         hs[k] = ld_g(sv_h, c.tok0, rt, c.NR, lane);
@@ -658,38 +708,54 @@ __device__ __forceinline__ void mlp_bwd_ct(const Mat& m1, const Mat& m2, const L
     }
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
-      const int rt = c.wave + 4 * k;
+      const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         const bool ok = tok_ok(rt, c);
-        const CT h = ct_unpack(hs[k]);
-        CT gl = h;
+        CT gl = ct_unpack(hs[k]);
         gelu_ct(gl);
         const CTr glr = ct_pack(gl);
         CT mo = ct_add(b2, ct_unpack(xs[k])), xh, yy, ds;
         mm(mo, W2f, glr);
         const float rs = ln_fwd_ct(mo, xh, yy, gam, bet);
         ln_bwd_ct(dx[k], xh, rs, gam, ok, ds, dlg, dlb);
-        const CTr dsr = ct_pack(ds);
-        st_lds(c.DA, rt, dsr, ok, lane);     // dY of W2
-        st_lds(c.XB, rt, glr, ok, lane);     // X of W2
+        st_lds(c.DA, rt, ct_pack(ds), ok, lane);   // dY of W2
+        st_lds(c.XB, rt, glr, ok, lane);           // X of W2
+        st_lds(c.QB, rt, xs[k], ok, lane);         // X of W1
+        dx[k] = ds;                                // residual path
+      }
+    }
+    flush_vec(dlg, c.g(ln.dg), lane);
+    flush_vec(dlb, c.g(ln.db), lane);
+  }
+  {   // pass 2 (W2ᵀ): dg = W2ᵀ ds * GELU'(h) -> KB (dY of W1)
+    AFr W2b;
+    loadA(W2b, m2.ba, lane);
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + NW * k;
+      if (rt < c.NT) {
+        const bool ok = tok_ok(rt, c);
+        const CT h = ct_unpack(ld_g(sv_h, c.tok0, rt, c.NR, lane));
         CT dg;
         ct_zero(dg);
-        mm(dg, W2b, dsr);
+        mm(dg, W2b, ld_lds(c.DA, rt, lane));
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int r = 0; r < 4; ++r) dg.v[i][r] = ok ? dg.v[i][r] * gelu_erf_grad(h.v[i][r]) : 0.f;
-        const CTr dgr = ct_pack(dg);
-        st_lds(c.KB, rt, dgr, ok, lane);     // dY of W1
-        st_lds(c.QB, rt, xs[k], ok, lane);   // X of W1
-        CT t = ds;
-        mm(t, W1b, dgr);
-        dx[k] = t;
+        st_lds(c.KB, rt, ct_pack(dg), ok, lane);
       }
     }
   }
-  flush_vec(dlg, c.g(ln.dg), lane);
-  flush_vec(dlb, c.g(ln.db), lane);
+  {   // pass 3 (W1ᵀ): dx += W1ᵀ dg
+    AFr W1b;
+    loadA(W1b, m1.ba, lane);
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + NW * k;
+      if (rt < c.NT) mm(dx[k], W1b, ld_lds(c.KB, rt, lane));
+    }
+  }
   __syncthreads();
   CP_MARK(2);
   wgrad64(c.DA, c.XB, m2, c);
@@ -709,40 +775,50 @@ __device__ __forceinline__ void self_attn_bwd_ct(const Mat* m, const LNp& ln, CT
     CT dlg, dlb;
     ct_zero(dlg);
     ct_zero(dlb);
-    AFr Wpf, Wpb;
-    loadA(Wpf, m[3].fa, lane);
-    loadA(Wpb, m[3].ba, lane);
-    const CT bp = ld_vec(m[3].b, lane), gam = ld_vec(ln.g, lane), bet = ld_vec(ln.b, lane);
-    CTr as[MAXRT];
+    {   // pass 1 (Wp): LN backward -> ds (dx) ; DQ = dY of Wp, XB = X of Wp
+      AFr Wpf;
+      loadA(Wpf, m[3].fa, lane);
+      const CT bp = ld_vec(m[3].b, lane), gam = ld_vec(ln.g, lane), bet = ld_vec(ln.b, lane);
+      CTr as[MAXRT];
 #pragma unroll
-    for (int k = 0; k < MAXRT; ++k) {
-      const int rt = c.wave + 4 * k;
-      if (rt < c.NT) {
-        as[k] = ld_g(sv_a, c.tok0, rt, c.NR, lane);
-        xin[k] = ld_g(sv_xin, c.tok0, rt, c.NR, lane);
+      for (int k = 0; k < MAXRT; ++k) {
+        const int rt = c.wave + NW * k;
+        if (rt < c.NT) {
+          as[k] = ld_g(sv_a, c.tok0, rt, c.NR, lane);
+          xin[k] = ld_g(sv_xin, c.tok0, rt, c.NR, lane);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < MAXRT; ++k) {
+        const int rt = c.wave + NW * k;
+        if (rt < c.NT) {
+          const bool ok = tok_ok(rt, c);
+          CT s = ct_add(bp, ct_unpack(xin[k])), xh, yy, ds;
+          mm(s, Wpf, as[k]);
+          const float rs = ln_fwd_ct(s, xh, yy, gam, bet);
+          ln_bwd_ct(dx[k], xh, rs, gam, ok, ds, dlg, dlb);
+          st_lds(c.DQ, rt, ct_pack(ds), ok, lane);   // dY of Wp
+          st_lds(c.XB, rt, as[k], ok, lane);         // X of Wp
+          dx[k] = ds;                                // residual path
+        }
+      }
+      flush_vec(dlg, c.g(ln.dg), lane);
+      flush_vec(dlb, c.g(ln.db), lane);
+    }
+    {   // pass 2 (Wpᵀ): dO = Wpᵀ ds -> DA
+      AFr Wpb;
+      loadA(Wpb, m[3].ba, lane);
+#pragma unroll
+      for (int k = 0; k < MAXRT; ++k) {
+        const int rt = c.wave + NW * k;
+        if (rt < c.NT) {
+          CT da;
+          ct_zero(da);
+          mm(da, Wpb, ld_lds(c.DQ, rt, lane));
+          st_lds(c.DA, rt, ct_pack(da), tok_ok(rt, c), lane);
+        }
       }
     }
-#pragma unroll
-    for (int k = 0; k < MAXRT; ++k) {
-      const int rt = c.wave + 4 * k;
-      if (rt < c.NT) {
-        const bool ok = tok_ok(rt, c);
-        CT s = ct_add(bp, ct_unpack(xin[k])), xh, yy, ds;
-        mm(s, Wpf, as[k]);
-        const float rs = ln_fwd_ct(s, xh, yy, gam, bet);
-        ln_bwd_ct(dx[k], xh, rs, gam, ok, ds, dlg, dlb);
-        const CTr dsr = ct_pack(ds);
-        st_lds(c.DQ, rt, dsr, ok, lane);     // dY of Wp
-        st_lds(c.XB, rt, as[k], ok, lane);   // X of Wp
-        CT da;
-        ct_zero(da);
-        mm(da, Wpb, dsr);
-        st_lds(c.DA, rt, ct_pack(da), ok, lane);   // dO
-        dx[k] = ds;                                // residual path
-      }
-    }
-    flush_vec(dlg, c.g(ln.dg), lane);
-    flush_vec(dlb, c.g(ln.db), lane);
   }
   __syncthreads();
   CP_MARK(11);
@@ -752,7 +828,7 @@ __device__ __forceinline__ void self_attn_bwd_ct(const Mat* m, const LNp& ln, CT
   proj3(m, 0, xin, c);
 #pragma unroll
   for (int k = 0; k < MAXRT; ++k) {
-    const int rt = c.wave + 4 * k;
+    const int rt = c.wave + NW * k;
     if (rt < c.NT) st_lds(c.XB, rt, xin[k], tok_ok(rt, c), lane);   // X of dWq / dWk / dWv
   }
   load_lse(sv_lse, c);

@@ -31,9 +31,10 @@ def read(fn):
 def main(B=3200, L=33, reps=3):
     dev = torch.device("cuda")
     lib = kernels.lib()
-    for n in ("mdl_ctprof_enc", "mdl_ctprof_dec"):
+    for n in ("mdl_ctprof_enc", "mdl_ctprof_dec", "mdl_ctprof_enc_bwd", "mdl_ctprof_dec_bwd"):
         getattr(lib, n).argtypes = [ctypes.c_void_p, ctypes.c_int]
-    penc, pdec = lib.mdl_ctprof_enc, lib.mdl_ctprof_dec
+    # the backward kernels live in their own translation units (mat_*_ct_bwd.hip) with their own counters
+    penc, pdec, penc_b, pdec_b = lib.mdl_ctprof_enc, lib.mdl_ctprof_dec, lib.mdl_ctprof_enc_bwd, lib.mdl_ctprof_dec_bwd
     m = make(L, dev, seed=0, scale=0.05)
     obs = torch.rand(B, L, 7, device=dev)
     ava = torch.ones(B, L, 2, device=dev)
@@ -43,11 +44,11 @@ def main(B=3200, L=33, reps=3):
     enc, dec = mat_train.EncoderFused(m), mat_train.DecoderFused(m)
     res = {}
     for r in range(reps + 1):
-        read(penc), read(pdec)
+        read(penc), read(pdec), read(penc_b), read(pdec_b)
         v, rep = enc.forward(obs); torch.cuda.synchronize(); a = read(penc)
         lp, ent = dec.forward(rep, actions, ava); torch.cuda.synchronize(); b = read(pdec)
-        drep = dec.backward(torch.ones_like(lp), torch.ones_like(ent)); torch.cuda.synchronize(); c = read(pdec)
-        enc.backward(drep, torch.ones_like(v)); torch.cuda.synchronize(); d = read(penc)
+        drep = dec.backward(torch.ones_like(lp), torch.ones_like(ent)); torch.cuda.synchronize(); c = read(pdec_b)
+        enc.backward(drep, torch.ones_like(v)); torch.cuda.synchronize(); d = read(penc_b)
         if r:
             for name, arr in (("enc_fwd", a), ("dec_fwd", b), ("dec_bwd", c), ("enc_bwd", d)):
                 acc = res.setdefault(name, [0] * 64)
