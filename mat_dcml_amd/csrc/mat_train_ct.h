@@ -322,16 +322,18 @@ __device__ __forceinline__ void flush_vec(const CT& acc, float* dst, int lane) {
 
 // ------------------------------------------------------------------------------------------ weight gradients
 // dW[n][k] (row stride ld) += Σ_t Y[t][n] X[t][k] for n < nrows, k < ncols, and db[n] += Σ_t Y[t][n], from
-// token-major swizzled LDS tiles of KP rows (KP % 32 == 0, padded rows zero).  Wave w owns dW rows
-// [16(w&3), 16(w&3)+16) and 16/NW of the 4 column tiles (all four at 4 waves, two at 8).  The bias gradient is one
-// extra MFMA per k-step against a ones fragment (waves of the first column group).  fp32 atomics.
+// token-major swizzled LDS tiles of KP rows (KP % 32 == 0, padded rows zero).  The 16 output blocks (row block
+// j & 3, column tile j >> 2) are dealt round robin, j = wave + NW i: a wave's blocks share one row block (NW % 4 == 0)
+// and so one Y fragment per k-step.  The bias gradient is one extra MFMA per k-step against a ones fragment (the
+// waves holding column tile 0).  fp32 atomics.
 __device__ __forceinline__ void wgrad_g(const bf16_t* Y, const bf16_t* X, int KP, float* dW, int ld, int nrows, int ncols,
                                         float* db, int wave, int lane) {
-  constexpr int NCT = 16 / NW;                      // column tiles per wave
-  const int rb = wave & 3, ct0 = (wave >> 2) * NCT;
-  if (ct0 > 0) db = nullptr;
+  static_assert(NW % 4 == 0, "row block per wave");
+  constexpr int NCT = (16 + NW - 1) / NW;           // column tiles per wave (at most)
+  const int rb = wave & 3;
+  if (wave >= 4) db = nullptr;
   const int nct = dW ? (ncols + 15) >> 4 : 0;
-  if ((!db && ct0 >= nct) || 16 * rb >= nrows) return;
+  if ((!db && (wave >> 2) >= nct) || 16 * rb >= nrows) return;
   const int g = lane >> 4, c16 = lane & 15;
   f32x4 acc[NCT];
 #pragma unroll
@@ -342,8 +344,9 @@ __device__ __forceinline__ void wgrad_g(const bf16_t* Y, const bf16_t* X, int KP
     const bf16x8 a = ld_frag_T(Y, k0, 16 * rb, lane);
 #pragma unroll
     for (int j = 0; j < NCT; ++j) {
-      if (ct0 + j < nct) {
-        const bf16x8 b = ld_frag_T(X, k0, 16 * (ct0 + j), lane);
+      const int bj = wave + NW * j, ct = bj >> 2;
+      if (bj < 16 && ct < nct) {
+        const bf16x8 b = ld_frag_T(X, k0, 16 * ct, lane);
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[j], 0, 0, 0);
       }
     }
@@ -351,16 +354,19 @@ __device__ __forceinline__ void wgrad_g(const bf16_t* Y, const bf16_t* X, int KP
   }
   if (dW) {
 #pragma unroll
-    for (int j = 0; j < NCT; ++j)
+    for (int j = 0; j < NCT; ++j) {
+      const int bj = wave + NW * j, ct = bj >> 2;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int n = 16 * rb + 4 * g + r, k = 16 * (ct0 + j) + c16;
+        const int n = 16 * rb + 4 * g + r, k = 16 * ct + c16;
+        const bool ok = bj < 16 && ct < nct && n < nrows && k < ncols;
 #ifdef MDL_ABLATE_WGRAD_ATOMIC   // timing experiment only: plain stores instead of the fp32 atomics (wrong sums)
-        if (ct0 + j < nct && n < nrows && k < ncols) dW[n * ld + k] = acc[j][r];
+        if (ok) dW[n * ld + k] = acc[j][r];
 #else
-        if (ct0 + j < nct && n < nrows && k < ncols) atomicAdd(dW + n * ld + k, acc[j][r]);
+        if (ok) atomicAdd(dW + n * ld + k, acc[j][r]);
 #endif
       }
+    }
   }
   if (db && c16 < 4) {
     const float v = c16 == 0 ? accb[0] : c16 == 1 ? accb[1] : c16 == 2 ? accb[2] : accb[3];
