@@ -6,24 +6,27 @@
 // one block of rows) at a time against a KV cache of the earlier rows reproduces the full recompute.
 //
 // Work decomposition (D = 64, 2 heads x 32, n_block = NB):
-//   * one 256-thread workgroup = 4 waves owns EPW envs; its 16-row MFMA tile holds (env, row) pairs of the
-//     current pass (stochastic rollout: 1 row per env; deterministic stride mode: up to 16/EPW rows per env);
+//   * one 256-thread workgroup = 4 waves owns one env (EPW = 1); its 16-row MFMA tile holds the agent rows of the
+//     current pass (stochastic rollout: 1 row; deterministic stride mode: up to 16 rows);
 //   * every 64x64 Linear is a 16x64x64 GEMM on v_mfma_f32_16x16x32_bf16: wave w owns output columns
 //     [16w, 16w+16); its B fragments (all 10·NB+1 decoder weight matrices) are loaded ONCE into VGPRs and stay
 //     register-resident for the whole decode (one wave per SIMD, ~170 VGPRs of weights);
 //   * activations move through LDS; the post-LN residual sums are kept in f32 and LayerNorm is fused into the
 //     NEXT GEMM's A-fragment load (each lane normalises the 16 values it feeds the MFMA, row statistics by two
 //     xor-shuffles), so no separate LN phase/barrier exists;
-//   * the self- and cross-attention K/V caches of every block live in LDS as bf16 with an XOR-swizzled 16-byte
-//     chunk order (conflict-free row gathers); attention over <= L cached rows runs on the VALU,
-//     8 lanes per (tile row, head);
+//   * the self- and cross-attention K/V caches of every block live in LDS as ONE token-major swizzled bf16 array
+//     (tile.h tmo: row = (block, kind, agent row), 16-byte chunks XOR-swizzled by row) and attention runs on MFMA
+//     (round 2): the pass's query rows are the 16 B-operand columns, the cached keys the A rows, so one
+//     v_mfma_f32_16x16x32_bf16 pair scores 32 keys for every live query and P·V is 4 more — the round-1 VALU
+//     attention (one wave, a lane per key, two 32-lane reductions and an LDS round trip for P) was half of every
+//     agent step (profiles/r2_decode);
 //   * the action head, availability masking, inverse-CDF categorical sampling / Normal sampling, log-probs and
 //     the next row's action-embedding token are fused into the last phase.
 // Inputs rep (encoder output, f32), ava, and the uniform / normal draws come from HBM — staged into LDS once at
 // kernel start when they fit (`stage`), so no row of the sequential agent loop waits on an HBM miss (the rep row
 // of phase D and the mask / draws of the head phase were first-touch loads on the critical path); outputs are
 // actions and log-probs (B, L).  Numerics: bf16 MFMA operands, f32 accumulation, f32 LayerNorm / softmax / log-softmax.
-#include "common.h"
+#include "tile.h"
 #include <cstdlib>
 
 using namespace mdl;
@@ -42,7 +45,7 @@ struct DecParams {
   const float* rnd_n;    // [B][L][act_dim]
   float* out_a;          // [B][L]
   float* out_lp;         // [B][L]
-  int B, L, act_dim, n_disc, stride, deterministic, epw, rmax, n_tok, tok_start, tok_zero;
+  int B, L, act_dim, n_disc, stride, deterministic, epw, rmax, n_tok, tok_start, tok_zero;   // epw must be 1
   int stage;             // 1: rep / ava / draws of the workgroup's envs are staged in LDS at kernel start
   int cont;              // 1: "Continuous" action type — every agent samples act_dim Gaussians and the next
                          //    row's input is LN(GELU(W_a · x + b_a)) of the sampled vector (not a token row)
@@ -54,21 +57,9 @@ struct DecParams {
 constexpr int SP = 68;   // f32 staging row pitch (floats)
 constexpr int XP = 72;   // bf16 A staging row pitch (elements)
 
-__device__ __forceinline__ int kv_off(int b, int kind, int m, int j, int col, int epw, int L) {
-  // 64-element rows of 8 x 16-byte chunks; chunk index XOR (j & 7) spreads row gathers over all banks
-  const int chunk = (col >> 3) ^ (j & 7);
-  return ((((b * 4 + kind) * epw + m) * L + j) << 6) + (chunk << 3) + (col & 7);
-}
-
-#ifdef MDL_DECODE_PROF
-__device__ unsigned long long g_attn_prof[8];
-#define MDL_ATT_MARK(k) do { if (aprof) { const unsigned long long t_ = clock64(); g_attn_prof[k] += t_ - at_; at_ = t_; } } while (0)
-#define MDL_ATT_INIT() const bool aprof = blockIdx.x == 0 && tid == 0; unsigned long long at_ = clock64()
-#else
-#define MDL_ATT_INIT() do { } while (0)
-#define MDL_ATT_MARK(k) do { } while (0)
-#endif
-
+// K / V caches: one token-major swizzled array, row (block b, kind (0 self K, 1 self V, 2 cross K, 3 cross V), agent j)
+__device__ __forceinline__ int kv_row(int b, int kind, int j, int L) { return (b * 4 + kind) * L + j; }
+__device__ __forceinline__ int kv_off(int b, int kind, int j, int col, int L) { return tmo(kv_row(b, kind, j, L), col); }
 __device__ __forceinline__ f32x4 mfma2(const bf16x8 a[2], const bf16x8 w[2], f32x4 acc) {
   acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], w[0], acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], w[1], acc, 0, 0, 0);
@@ -142,142 +133,83 @@ __device__ __forceinline__ void store_xf(float* X, int lane, const float xf[16])
 }
 
 
-// Causal attention of the pass's live tile rows over cached rows 0..i of their env.  lpi lanes (half a wave at
-// the rollout shape) per (tile row, head): scores with lanes striding over the keys; P·V with the lanes split
-// into 8 groups of 4 output dims x lpi/8 key groups (each lane sums ~i/(lpi/8) keys, the key groups combined by
-// DPP / permlane shuffles).  An item's lanes live in one wave, so the score -> P·V hand-off through PR needs only
-// a wave-level LDS wait.  Latency structure (the decode runs one row per env per step): only live items are
-// visited (dead tile rows' XA rows are never consumed by a live row — MFMA rows are independent — and XA is
-// zeroed once at kernel start), and the score / P·V loops issue all their LDS loads before using any of them
-// (indices clamped to row i and masked, instead of per-key branches that serialised the load latencies).
-template <int lpi>
-__device__ __forceinline__ void attention_phase_t(const bf16_t* KV, const float* Q, float* PR, bf16_t* XA,
-                                                  const int* ROWI, int R, int EPW, int L, int b, int kind,
-                                                  float scale, int tid, int live) {
-  const int u = tid & (lpi - 1);
-  const int dg = u & 7, kg = u >> 3, nkg = lpi >> 3;
-  MDL_ATT_INIT();
-  for (int item = tid / lpi; item < 2 * live; item += 256 / lpi) {
-    const int t = item >> 1, h = item & 1;
-    const int i = ROWI[t];          // uniform over the item's lanes; >= 0 for every live row
-    const int m = t / R;
-    float* pr = PR + (t * 2 + h) * L;
-    float q[32];
-#pragma unroll
-    for (int d = 0; d < 32; ++d) q[d] = Q[t * SP + 32 * h + d];
-    MDL_ATT_MARK(0);
-    auto krow_of = [&](int j) { return KV + kv_off(b, kind, m, j, 0, EPW, L) - ((0 ^ (j & 7)) << 3); };
-    // the first KR keys of every lane: loads for all of them first, then the dot products (four independent
-    // 8-long FMA chains per key), masked beyond row i
-    constexpr int KR = lpi >= 32 ? 2 : 4;
-    bf16x8 kv[KR][4];
-#pragma unroll
-    for (int kk = 0; kk < KR; ++kk) {
-      const int j = min(u + kk * lpi, i);
-      const bf16_t* krow = krow_of(j);
-#pragma unroll
-      for (int lc = 0; lc < 4; ++lc) kv[kk][lc] = *(const bf16x8*)(krow + (((4 * h + lc) ^ (j & 7)) << 3));
-    }
-    float scr[KR];
-    float mx = -INFINITY;
-#pragma unroll
-    for (int kk = 0; kk < KR; ++kk) {
-      float d4[4];
-#pragma unroll
-      for (int lc = 0; lc < 4; ++lc) {
-        float d = 0.f;
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) d += q[lc * 8 + jj] * bf2f((bf16_t)kv[kk][lc][jj]);
-        d4[lc] = d;
-      }
-      scr[kk] = u + kk * lpi <= i ? ((d4[0] + d4[1]) + (d4[2] + d4[3])) * scale : -INFINITY;
-      mx = fmaxf(mx, scr[kk]);
-    }
-    for (int j = u + KR * lpi; j <= i; j += lpi) {      // long rows only (L > KR * lpi)
-      const bf16_t* krow = krow_of(j);
-      float d4[4];
-#pragma unroll
-      for (int lc = 0; lc < 4; ++lc) {
-        const bf16x8 k8 = *(const bf16x8*)(krow + (((4 * h + lc) ^ (j & 7)) << 3));
-        float d = 0.f;
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) d += q[lc * 8 + jj] * bf2f((bf16_t)k8[jj]);
-        d4[lc] = d;
-      }
-      const float sc = ((d4[0] + d4[1]) + (d4[2] + d4[3])) * scale;
-      pr[j] = sc;
-      mx = fmaxf(mx, sc);
-    }
-    MDL_ATT_MARK(1);
-    mx = group_max<lpi>(mx);
-    MDL_ATT_MARK(2);
-    float sum = 0.f;
-#pragma unroll
-    for (int kk = 0; kk < KR; ++kk) {
-      const int j = u + kk * lpi;
-      const float pj = j <= i ? __expf(scr[kk] - mx) : 0.f;
-      if (j <= i) pr[j] = pj;
-      sum += pj;
-    }
-    for (int j = u + KR * lpi; j <= i; j += lpi) {
-      const float pj = __expf(pr[j] - mx);
-      pr[j] = pj;
-      sum += pj;
-    }
-    sum = group_sum<lpi>(sum);
-    MDL_ATT_MARK(3);
-    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // PR written by this item's lanes (same wave)
-    MDL_ATT_MARK(4);
-    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
-    const int lc = 4 * h + (dg >> 1), off = 4 * (dg & 1);
-    for (int j0 = kg; j0 <= i; j0 += 4 * nkg) {         // 4 keys per lane per trip: loads first, then FMAs
-      float pj[4];
-      uint2 v4[4];
-#pragma unroll
-      for (int uu = 0; uu < 4; ++uu) {
-        const int j = j0 + uu * nkg, jc = min(j, i);
-        pj[uu] = pr[jc];
-        const bf16_t* vrow = KV + kv_off(b, kind + 1, m, jc, 0, EPW, L) - ((0 ^ (jc & 7)) << 3);
-        v4[uu] = *(const uint2*)(vrow + ((lc ^ (jc & 7)) << 3) + off);
-      }
-#pragma unroll
-      for (int uu = 0; uu < 4; ++uu) {
-        const float w = j0 + uu * nkg <= i ? pj[uu] : 0.f;
-        acc0 += w * __uint_as_float(v4[uu].x << 16);
-        acc1 += w * __uint_as_float(v4[uu].x & 0xFFFF0000u);
-        acc2 += w * __uint_as_float(v4[uu].y << 16);
-        acc3 += w * __uint_as_float(v4[uu].y & 0xFFFF0000u);
-      }
-    }
-    MDL_ATT_MARK(5);
-    if (lpi > 8) {   // reduce over the key groups kg: lane ^ 8 (DPP row_ror:8), then lane ^ 16
-      acc0 += dppf<DPP_ROW_ROR8>(acc0); acc1 += dppf<DPP_ROW_ROR8>(acc1);
-      acc2 += dppf<DPP_ROW_ROR8>(acc2); acc3 += dppf<DPP_ROW_ROR8>(acc3);
-    }
-    if (lpi > 16) {
-      acc0 += xor16_partner(acc0); acc1 += xor16_partner(acc1);
-      acc2 += xor16_partner(acc2); acc3 += xor16_partner(acc3);
-    }
-    if (kg == 0) {
-      const float inv = 1.f / sum;
-      bf16_t* xa = XA + t * XP + 32 * h + 4 * dg;
-      xa[0] = f2bf(acc0 * inv); xa[1] = f2bf(acc1 * inv); xa[2] = f2bf(acc2 * inv); xa[3] = f2bf(acc3 * inv);
-    }
-    MDL_ATT_MARK(6);
-  }
-  MDL_ATT_MARK(7);
+__device__ __forceinline__ uint32_t pk2f(float a, float b) {   // one v_cvt_pk_bf16_f32 (RNE)
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2v __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2v){a, b}, b2v));
+}
+__device__ __forceinline__ float xrow_max(float x) {   // max over the 4 lane rows g of a column c
+  float a, b;
+  swap16(x, a, b);
+  x = fmaxf(a, b);
+  swap32(x, a, b);
+  return fmaxf(a, b);
 }
 
-__device__ __forceinline__ void attention_phase(const bf16_t* KV, const float* Q, float* PR, bf16_t* XA,
-                                                const int* ROWI, int R, int EPW, int L, int b, int kind,
-                                                float scale, int tid, int lpi, int live) {
-#ifdef MDL_LPI_ONLY32   // code-size experiment: rollout-only build (stride-mode passes need 16 / 8)
-  attention_phase_t<32>(KV, Q, PR, XA, ROWI, R, EPW, L, b, kind, scale, tid, live);
-#else
-  if (lpi == 32) attention_phase_t<32>(KV, Q, PR, XA, ROWI, R, EPW, L, b, kind, scale, tid, live);
-  else if (lpi == 16) attention_phase_t<16>(KV, Q, PR, XA, ROWI, R, EPW, L, b, kind, scale, tid, live);
-  else attention_phase_t<8>(KV, Q, PR, XA, ROWI, R, EPW, L, b, kind, scale, tid, live);
-#endif
+// Causal attention of the pass's query rows t (ROWI[t] = agent row i, -1 = dead) over the cached rows 0..i, head h
+// = wave (waves 0, 1).  Scores Sᵀ = K·Qᵀ in 32-key chunks: the A rows are keys in the permuted order pi(t, m) =
+// 8(m>>2) + 4t + (m&3), so lane (g, c) of the two MFMA outputs holds S[query c][keys kb + 8g + j] (j < 8) — already
+// the B operand of Oᵀ = Vᵀ·Pᵀ, whose A operand comes from ds_read_b64_tr_b16 of the token-major V cache.
+// Single-pass online softmax in log2 units; P enters as a hi/lo bf16 pair (fp32-like P·V).  O (bf16) -> XA rows.
+// Masked keys (j > i, or rows of other caches beyond the chunk) get P = 0; every cache row is finite (zeroed at
+// kernel start, plus 32 zero rows after the last cache) so 0 · V stays 0.
+__device__ __forceinline__ void attention_mfma(const bf16_t* KV, int rowK, int rowV, const bf16_t* QT, bf16_t* XA,
+                                               const int* ROWI, int imax, int wave, int lane) {
+  if (wave >= 2) return;
+  const int h = wave, g = lane >> 4, c = lane & 15;
+  constexpr float SL2 = 0.17677669529663687f * 1.4426950408889634f;   // 1/sqrt(32) * log2(e)
+  const int iq = ROWI[c];
+  const bf16x8 qB = lda_tm(QT, c, 4 * h + g);
+  float m = -INFINITY, l = 0.f;
+  f32x4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
+  for (int kb = 0; kb <= imax; kb += 32) {
+    float sc[8];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const bf16x8 a = lda_tm(KV, rowK + kb + 8 * (c >> 2) + 4 * t + (c & 3), 4 * h + g);
+      const f32x4 r = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qB, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sc[4 * t + i] = r[i];
+    }
+    float cm = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sc[j] = kb + 8 * g + j <= iq ? sc[j] * SL2 : -INFINITY;
+      cm = fmaxf(cm, sc[j]);
+    }
+    const float nm = fmaxf(m, xrow_max(cm));
+    const float mr = nm == -INFINITY ? 0.f : nm;
+    const float alpha = exp2f(m - mr);
+    float ps = 0.f;
+    uint32_t hi[4], lo[4];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sc[j] = exp2f(sc[j] - mr);
+      ps += sc[j];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      hi[i] = pk2f(sc[2 * i], sc[2 * i + 1]);
+      lo[i] = pk2f(sc[2 * i] - __uint_as_float(hi[i] << 16), sc[2 * i + 1] - __uint_as_float(hi[i] & 0xFFFF0000u));
+    }
+    typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+    const bf16x8 ph = __builtin_bit_cast(bf16x8, (u4v){hi[0], hi[1], hi[2], hi[3]});
+    const bf16x8 pl = __builtin_bit_cast(bf16x8, (u4v){lo[0], lo[1], lo[2], lo[3]});
+    l = l * alpha + ps;
+    o0 *= alpha;
+    o1 *= alpha;
+    const bf16x8 va = ld_frag_T(KV, rowV + kb, 32 * h, lane), vb = ld_frag_T(KV, rowV + kb, 32 * h + 16, lane);
+    o0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, ph, o0, 0, 0, 0);
+    o0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pl, o0, 0, 0, 0);
+    o1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vb, ph, o1, 0, 0, 0);
+    o1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vb, pl, o1, 0, 0, 0);
+    m = nm;
+  }
+  l = cross_row_sum(l);
+  const float il = l > 0.f ? 1.f / l : 0.f;
+  bf16_t* xa = XA + c * XP + 32 * h + 4 * g;
+  *(uint2*)xa = make_uint2(pk2f(o0[0] * il, o0[1] * il), pk2f(o0[2] * il, o0[3] * il));
+  *(uint2*)(xa + 16) = make_uint2(pk2f(o1[0] * il, o1[1] * il), pk2f(o1[2] * il, o1[3] * il));
 }
 
 // Action head: LN(head1 output) · W_h2 + b -> logits; availability mask, sampling, log-prob (16 lanes per row).
@@ -415,15 +347,15 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
   const int RMAX = p.rmax;
 
   // ---------------------------------------------------------------- LDS carve (16-byte aligned pieces)
-  const size_t kv_elems = (size_t)NB * 4 * EPW * L * 64;
+  const size_t kv_elems = ((size_t)NB * 4 * L + 32) * 64;    // + 32 zero rows: chunk reads past the last cache
   bf16_t* KV = (bf16_t*)smem;
   char* ptr = smem + ((kv_elems * 2 + 15) & ~(size_t)15);
   float* S = (float*)ptr;   ptr += 16 * SP * 4;
-  float* Q = (float*)ptr;   ptr += 16 * SP * 4;
+  float* Q = (float*)ptr;   ptr += 16 * SP * 4;   // head1 output (f32)
   float* XR = (float*)ptr;  ptr += 16 * SP * 4;
   bf16_t* XA = (bf16_t*)ptr; ptr += 16 * XP * 2;
+  bf16_t* QT = (bf16_t*)ptr; ptr += 16 * 64 * 2;   // attention queries, token-major swizzled (tile.h tmo)
   float* LNP = (float*)ptr; ptr += NLN * 128 * 4;
-  float* PR = (float*)ptr;  ptr += ((EPW * RMAX * 2 * L * 4 + 15) & ~15);
   int* TOK = (int*)ptr;     ptr += ((EPW * L * 4 + 15) & ~15);
   int* PEND = (int*)ptr;    ptr += ((EPW * L * 4 + 15) & ~15);
   int* ROWI = (int*)ptr;    ptr += 16 * 4;
@@ -451,6 +383,8 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
   for (int i = tid; i < NLN * 128; i += 256) LNP[i] = p.lnp[i];
   for (int i = tid; i < EPW * L; i += 256) { TOK[i] = (i % L == 0) ? p.tok_start : p.tok_zero; PEND[i] = -1; }
   for (int i = tid; i < 16 * XP; i += 256) XA[i] = 0;   // dead tile rows keep finite A-operand rows
+  for (size_t i = (size_t)tid * 8; i < kv_elems; i += 256 * 8) *(uint4*)(KV + i) = make_uint4(0, 0, 0, 0);
+  for (int i = tid; i < 16 * 64; i += 256) QT[i] = 0;
   if (stage) {   // the workgroup's envs are contiguous in every input
     const int nrow = n_env * L;
     const float4* src = (const float4*)(p.rep + (size_t)env0 * L * 64);
@@ -466,8 +400,6 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
   const float* wh2 = stage ? WH2 : p.wh2;
   const float* bh2 = stage ? WH2 + AD * 64 : p.bh2;
   __syncthreads();
-
-  const float scale = 0.17677669529663687f;  // 1/sqrt(32)
 
   // ---------------------------------------------------------------- block schedule (transformer_act.py:37-75)
   int prev_s = -1, s = 0, e = 1;
@@ -487,8 +419,7 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) { crow_i[r] = ROWI[4 * g4 + r]; crow_m[r] = (4 * g4 + r) / R; }
       const int arow_i = ROWI[c16], arow_m = c16 / R;
-      const int live = n_env * R;                           // live tile rows this pass
-      const int lpi = live <= 4 ? 32 : (live <= 8 ? 16 : 8);
+      const int imax = plo + R - 1;                         // last live agent row of the pass
 
 #pragma unroll
       for (int b = 0; b < NB; ++b) {
@@ -512,17 +443,17 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = 4 * g4 + r;
-            Q[row * SP + col] = q1[r] + bcol[b * 10 + 0];
+            QT[tmo(row, col)] = f2bf(q1[r] + bcol[b * 10 + 0]);
             if (crow_i[r] >= 0) {
-              KV[kv_off(b, 0, crow_m[r], crow_i[r], col, EPW, L)] = f2bf(k1[r] + bcol[b * 10 + 1]);
-              KV[kv_off(b, 1, crow_m[r], crow_i[r], col, EPW, L)] = f2bf(v1[r] + bcol[b * 10 + 2]);
+              KV[kv_off(b, 0, crow_i[r], col, L)] = f2bf(k1[r] + bcol[b * 10 + 1]);
+              KV[kv_off(b, 1, crow_i[r], col, L)] = f2bf(v1[r] + bcol[b * 10 + 2]);
             }
           }
         }
         __syncthreads();
         MDL_PROF_MARK(1);
         // ---------------- [B] causal self-attention over cached rows 0..i
-        attention_phase(KV, Q, PR, XA, ROWI, R, EPW, L, b, 0, scale, tid, lpi, live);
+        attention_mfma(KV, kv_row(b, 0, 0, L), kv_row(b, 1, 0, L), QT, XA, ROWI, imax, wave, lane);
         __syncthreads();
         MDL_PROF_MARK(2);
         // ---------------- [C] proj1 + bias + residual x -> S
@@ -554,17 +485,17 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = 4 * g4 + r;
-            Q[row * SP + col] = q2[r] + bcol[b * 10 + 4];
+            QT[tmo(row, col)] = f2bf(q2[r] + bcol[b * 10 + 4]);
             if (crow_i[r] >= 0) {
-              KV[kv_off(b, 2, crow_m[r], crow_i[r], col, EPW, L)] = f2bf(k2[r] + bcol[b * 10 + 5]);
-              KV[kv_off(b, 3, crow_m[r], crow_i[r], col, EPW, L)] = f2bf(v2[r] + bcol[b * 10 + 6]);
+              KV[kv_off(b, 2, crow_i[r], col, L)] = f2bf(k2[r] + bcol[b * 10 + 5]);
+              KV[kv_off(b, 3, crow_i[r], col, L)] = f2bf(v2[r] + bcol[b * 10 + 6]);
             }
           }
         }
         __syncthreads();
         MDL_PROF_MARK(4);
         // ---------------- [E] causal cross-attention (q = rep rows, k/v = x1 rows)
-        attention_phase(KV, Q, PR, XA, ROWI, R, EPW, L, b, 2, scale, tid, lpi, live);
+        attention_mfma(KV, kv_row(b, 2, 0, L), kv_row(b, 3, 0, L), QT, XA, ROWI, imax, wave, lane);
         __syncthreads();
         MDL_PROF_MARK(5);
         // ---------------- [F] proj2 + bias + rep_i -> S
@@ -653,11 +584,8 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
 
 #ifdef MDL_DECODE_PROF
 MDL_API int mdl_decode_prof_read(unsigned long long* out) {
-  int rc = (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_decode_prof), sizeof(unsigned long long) * 16, 0,
-                                    hipMemcpyDeviceToHost);
-  if (rc == 0) rc = (int)hipMemcpyFromSymbol(out + 16, HIP_SYMBOL(g_attn_prof), sizeof(unsigned long long) * 8, 0,
-                                             hipMemcpyDeviceToHost);
-  return rc;
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_decode_prof), sizeof(unsigned long long) * 16, 0,
+                                  hipMemcpyDeviceToHost);
 }
 #endif
 
@@ -666,32 +594,26 @@ size_t mat_decode_stage_bytes(int epw, int L, int AD, int n_tok) {
 }
 
 size_t mat_decode_lds_bytes(int NB, int epw, int rmax, int L) {
-  size_t kv = (size_t)NB * 4 * epw * L * 64 * 2;
+  (void)rmax;
+  size_t kv = ((size_t)NB * 4 * L + 32) * 64 * 2;
   kv = (kv + 15) & ~(size_t)15;
-  size_t rest = 3 * 16 * SP * 4 + 16 * XP * 2 + (3 * NB + 1) * 128 * 4 + ((epw * rmax * 2 * L * 4 + 15) & ~15) +
-                2 * ((epw * L * 4 + 15) & ~15) + 16 * 4 + (size_t)epw * 64 * 4;
+  size_t rest = 3 * 16 * SP * 4 + 16 * XP * 2 + 16 * 64 * 2 + (3 * NB + 1) * 128 * 4 + 2 * ((epw * L * 4 + 15) & ~15) +
+                16 * 4 + (size_t)epw * 64 * 4;
   return kv + rest;
 }
 
-// Tile geometry: EPW envs per workgroup (largest power of two <= min(16, B) that fits the 160 KiB LDS of a CU
-// with one row per env), then RMAX rows per env per pass (largest <= 16/EPW that still fits).
-// Returns EPW | (RMAX << 8), or 0 if even one env does not fit.
+// Tile geometry: one env per workgroup (the MFMA attention shares the K / V A-operand over the tile's query rows,
+// so they must be one env's rows; envs per workgroup only ever shortened the round-1 VALU attention, and at the
+// rollout shape one env per CU was already the fastest, 642 vs 690 us), RMAX = 16 rows per pass (stride mode).
+// Returns EPW | (RMAX << 8), or 0 if the caches do not fit.
 MDL_API int mdl_mat_decode_geometry(int NB, int L, int B) {
-  int cap = 16;
-  while (cap > 1 && cap > B) cap >>= 1;
-  for (int epw = cap; epw >= 1; epw >>= 1) {
-    if (mat_decode_lds_bytes(NB, epw, 1, L) <= 160 * 1024) {
-      int rmax = 16 / epw;
-      while (rmax > 1 && mat_decode_lds_bytes(NB, epw, rmax, L) > 160 * 1024) --rmax;
-      return epw | (rmax << 8);
-    }
-  }
-  return 0;
+  (void)B;
+  return mat_decode_lds_bytes(NB, 1, 16, L) <= 160 * 1024 ? 1 | (16 << 8) : 0;
 }
 
 MDL_API int mdl_mat_decode(const DecParams* p, int NB, hipStream_t st) {
   const int epw = p->epw;
-  if (epw <= 0 || p->act_dim > 64 || p->act_dim < 1) return -1;
+  if (epw != 1 || p->act_dim > 64 || p->act_dim < 1) return -1;
   if (p->cont && (!p->wa || !p->ba || !p->lnd || p->n_disc != 0)) return -5;
   if (p->rmax < 1 || p->rmax * epw > 16) return -4;
   size_t lds = mat_decode_lds_bytes(NB, epw, p->rmax, p->L);

@@ -68,10 +68,9 @@ def supports(model, L=None) -> bool:
     return not unsupported_reasons(model, L)
 
 
-# envs per decode workgroup cap (kernel maximum 16).  The decode is latency bound (one dependent chain of ~20
-# barrier-separated phases per agent), so spreading envs over more CUs only shortens the attention phases:
-# 256 envs x 33 agents: 690 us at 16 envs per workgroup, 642 us at 1 (tests/bench_decode.py)
-_EPW_CAP = int(os.environ.get("MAT_DCML_DECODE_EPW", "1"))
+# envs per decode workgroup: the kernel runs one env per workgroup (its MFMA attention shares the K / V operand
+# over the tile's query rows); the geometry query still takes the cap for its signature.
+_EPW_CAP = 1
 
 
 def bump_version(model):

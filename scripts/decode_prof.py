@@ -32,8 +32,3 @@ for L in (33, 101):
         print(f"  {n:16s} {out[k]:10d} {100 * out[k] / max(tot, 1):5.1f}%  {out[k] / L:8.0f}/agent")
     print("  phase G sub-marks (12: since the previous sub-mark / barrier, 13: afrag_ln, 14: store_xf + MFMA, "
           "15: GELU + XA stores):", [out[k] for k in (12, 13, 14, 15)])
-    sub = ["q load", "scores", "max", "exp+sum", "waitcnt", "P.V", "reduce+store", "dead items"]
-    at = sum(out[16:24])
-    print(f"  attention sub-phases (thread 0, cumulative over both kinds, all launches): {at}")
-    for k, n in enumerate(sub):
-        print(f"    {n:14s} {out[16 + k]:10d} {100 * out[16 + k] / max(at, 1):5.1f}%")
