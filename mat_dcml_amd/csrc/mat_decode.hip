@@ -52,7 +52,23 @@ struct DecParams {
   const float* wa;       // [64][act_dim] action-encoder weight (cont)
   const float* ba;       // [64] action-encoder bias (cont)
   const float* lnd;      // [2][64] decoder input LayerNorm (cont)
+  int gen;               // 1: draw the sampling noise in-kernel (Philox4x32-10, key (rk0, rk1), counter (env, row,
+  uint32_t rk0, rk1, rctr;   //    rctr, purpose)) instead of reading rnd_u / rnd_n — no per-step torch.rand launches
 };
+
+// in-kernel sampling noise: one Philox block per (env, row, purpose); purpose 0 = the categorical uniform (x) and
+// the Normal draws of dims 0, 1 (Box-Muller of y, z); purpose 1 + k = dims 2 + 2k, 3 + 2k
+__device__ __forceinline__ float draw_u(const DecParams& p, int env, int row) {
+  const u4 r = philox4x32_10((uint32_t)env, (uint32_t)row, p.rctr, (uint32_t)P_POLICY, p.rk0, p.rk1);
+  return u01_open_f(r.x);
+}
+__device__ __forceinline__ float draw_n(const DecParams& p, int env, int row, int a) {
+  const int k = a >> 1;
+  const u4 r = philox4x32_10((uint32_t)env, (uint32_t)row, p.rctr, (uint32_t)(P_POLICY + k), p.rk0, p.rk1);
+  const uint32_t b0 = k == 0 ? r.y : r.x, b1 = k == 0 ? r.z : r.y;
+  const float rad = sqrtf(-2.f * __logf(u01_open_f(b0))), th = 6.283185307179586f * u01_open_f(b1);
+  return (a & 1) ? rad * __sinf(th) : rad * __cosf(th);
+}
 
 constexpr int SP = 68;   // f32 staging row pitch (floats)
 constexpr int XP = 72;   // bf16 A staging row pitch (elements)
@@ -250,7 +266,7 @@ __device__ __forceinline__ void head_phase(const DecParams& p, const float* H1, 
     for (int k = 0; k < 4; ++k) ev[k] = p.ba[4 * q + k];
     for (int a = 0; a < AD; ++a) {
       const float mean_a = lg[a], sd = p.stdv[a];
-      const float x = p.deterministic ? mean_a : mean_a + sd * (stage ? RN[li * AD + a] : p.rnd_n[oi * AD + a]);
+      const float x = p.deterministic ? mean_a : mean_a + sd * (stage ? RN[li * AD + a] : p.gen ? draw_n(p, env0 + m, i, a) : p.rnd_n[oi * AD + a]);
       if (q == 0) {
         const float z = (x - mean_a) / sd;
         p.out_a[oi * AD + a] = x;
@@ -294,7 +310,7 @@ __device__ __forceinline__ void head_phase(const DecParams& p, const float* H1, 
     const float lse = mx + __logf(se);
     int act = amax;
     if (!p.deterministic) {
-      const float uu = stage ? RU[li] : p.rnd_u[oi];
+      const float uu = stage ? RU[li] : p.gen ? draw_u(p, env, i) : p.rnd_u[oi];
       float cdf = 0.f;
       int cnt = 0;
       for (int a = 0; a < AD; ++a) {
@@ -310,7 +326,7 @@ __device__ __forceinline__ void head_phase(const DecParams& p, const float* H1, 
   } else {
     const int a = AD - 1;
     const float mean_a = lg[a], sd = p.stdv[a];
-    const float x = p.deterministic ? mean_a : mean_a + sd * (stage ? RN[li * AD + a] : p.rnd_n[oi * AD + a]);
+    const float x = p.deterministic ? mean_a : mean_a + sd * (stage ? RN[li * AD + a] : p.gen ? draw_n(p, env, i, a) : p.rnd_n[oi * AD + a]);
     const float z = (x - mean_a) / sd;
     p.out_a[oi] = x;
     p.out_lp[oi] = -0.5f * z * z - __logf(sd) - 0.91893853320467274f;
@@ -391,8 +407,13 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
     float4* dst = (float4*)REP;
     for (int i = tid; i < nrow * 16; i += 256) dst[i] = src[i];
     if (p.ava) for (int i = tid; i < nrow * AD; i += 256) AVA[i] = p.ava[(size_t)env0 * L * AD + i];
-    if (p.rnd_u) for (int i = tid; i < nrow; i += 256) RU[i] = p.rnd_u[(size_t)env0 * L + i];
-    if (p.rnd_n) for (int i = tid; i < nrow * AD; i += 256) RN[i] = p.rnd_n[(size_t)env0 * L * AD + i];
+    if (p.gen && !p.deterministic) {
+      for (int i = tid; i < nrow; i += 256) RU[i] = draw_u(p, env0 + i / L, i % L);
+      for (int i = tid; i < nrow * AD; i += 256) RN[i] = draw_n(p, env0 + i / (L * AD), (i / AD) % L, i % AD);
+    } else {
+      if (p.rnd_u) for (int i = tid; i < nrow; i += 256) RU[i] = p.rnd_u[(size_t)env0 * L + i];
+      if (p.rnd_n) for (int i = tid; i < nrow * AD; i += 256) RN[i] = p.rnd_n[(size_t)env0 * L * AD + i];
+    }
     for (int i = tid; i < p.n_tok * 64; i += 256) EMB[i] = p.emb[i];
     for (int i = tid; i < AD * 65; i += 256) WH2[i] = i < AD * 64 ? p.wh2[i] : p.bh2[i - AD * 64];
   }

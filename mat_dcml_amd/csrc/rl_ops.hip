@@ -243,3 +243,85 @@ MDL_API int mdl_gather_rows(const GatherArgs* a, hipStream_t s) {
   MDL_CHECK_LAUNCH();
   return 0;
 }
+
+// ------------------------------------------------------------------------------------------ rollout insert
+// The DCML runner's per-step bookkeeping in ONE launch (runner/dcml_runner.py _track + insert; reference
+// runner/dcml_runner.py:250-288 insert and shared_buffer.py insert): the buffer-slot copies of the step's
+// observations / share obs / availability / actions / log-probs / values, the agent-expanded rewards and masks,
+// and the episode accumulators with the finished-episode statistics.  Round 1 ran these as ~30 torch launches per
+// env step (1,500 per PPO iteration).  Workgroups 1.. copy; workgroup 0 does the per-env part, its statistics
+// reduced in a fixed order (bit-reproducible run to run).
+struct InsSeg { const float* src; float* dst; int n; };
+constexpr int INS_SEGS = 6;
+struct InsArgs {
+  InsSeg seg[INS_SEGS];
+  int E, A, n_obj;
+  const float *reward, *delay, *pay;
+  const unsigned char* done;
+  float *d_rew, *d_mask;          // rewards[t] (E, A, n_obj), masks[t + 1] (E, A, 1)
+  float *ep_r, *ep_d, *ep_p;      // (E) running episode sums
+  double* stats;                  // [4] += (finished episodes, Σ their reward, Σ delay, Σ payment)
+};
+
+__global__ __launch_bounds__(256) void rollout_insert_kernel(InsArgs a) {
+  const int tid = threadIdx.x;
+  if (blockIdx.x > 0) {
+    const int stride = (gridDim.x - 1) * 256;
+#pragma unroll
+    for (int k = 0; k < INS_SEGS; ++k) {
+      const InsSeg s = a.seg[k];
+      for (int i = (blockIdx.x - 1) * 256 + tid; i < s.n; i += stride) s.dst[i] = s.src[i];
+    }
+    return;
+  }
+  __shared__ double red[4][256];
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int e = tid; e < a.E; e += 256) {
+    const float r = a.reward[e], dl = a.delay[e], py = a.pay[e];
+    const bool d = a.done[e] != 0;
+    for (int ag = 0; ag < a.A; ++ag) {
+      const size_t o = (size_t)e * a.A + ag;
+      a.d_mask[o] = d ? 0.f : 1.f;
+      if (a.n_obj == 2) {
+        a.d_rew[2 * o] = -dl;
+        a.d_rew[2 * o + 1] = -py;
+      } else {
+        a.d_rew[o] = r;
+      }
+    }
+    const float er = a.ep_r[e] + r, ed = a.ep_d[e] + dl, ep = a.ep_p[e] + py;
+    if (d) {
+      acc[0] += 1.0;
+      acc[1] += (double)er;
+      acc[2] += (double)ed;
+      acc[3] += (double)ep;
+    }
+    a.ep_r[e] = d ? 0.f : er;
+    a.ep_d[e] = d ? 0.f : ed;
+    a.ep_p[e] = d ? 0.f : ep;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) red[k][tid] = acc[k];
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (tid < w)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) red[k][tid] += red[k][tid + w];
+    __syncthreads();
+  }
+  if (tid < 4) a.stats[tid] += red[tid][0];
+}
+
+MDL_API int mdl_rollout_insert(const InsArgs* a, hipStream_t s) {
+  if (a->E < 1 || a->A < 1 || (a->n_obj != 1 && a->n_obj != 2)) return -1;
+  int most = 0;
+  for (int k = 0; k < INS_SEGS; ++k) {
+    if (a->seg[k].n < 0 || (a->seg[k].n > 0 && (!a->seg[k].src || !a->seg[k].dst))) return -2;
+    most = a->seg[k].n > most ? a->seg[k].n : most;
+  }
+  int gx = (most + 255) / 256;
+  gx = gx < 1 ? 1 : (gx > 64 ? 64 : gx);
+  hipLaunchKernelGGL(rollout_insert_kernel, dim3(gx + 1), dim3(256), 0, s, *a);
+  MDL_CHECK_LAUNCH();
+  return 0;
+}

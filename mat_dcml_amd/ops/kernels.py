@@ -190,6 +190,39 @@ def gather_rows(srcs, idx, norm_sums=None, norm_keys=(), eps=1e-5):
     return out
 
 
+# ----------------------------------------------------------------------------------------- rollout insert
+class InsSeg(ctypes.Structure):
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("n", ctypes.c_int)]
+
+
+class InsArgs(ctypes.Structure):
+    _fields_ = [("seg", InsSeg * 6), ("E", ctypes.c_int), ("A", ctypes.c_int), ("n_obj", ctypes.c_int)] + \
+               [(n, ctypes.c_void_p) for n in ("reward", "delay", "pay", "done", "d_rew", "d_mask", "ep_r", "ep_d",
+                                               "ep_p", "stats")]
+
+
+sig("mdl_rollout_insert", ctypes.POINTER(InsArgs), vp)
+
+
+def rollout_insert(copies, reward, delay, pay, done, rew_slot, mask_slot, ep_r, ep_d, ep_p, stats):
+    """One launch: ``dst.copy_(src)`` for up to 6 (src, dst) pairs of contiguous f32 tensors, the agent-expanded
+    rewards ((E, A, n_obj) slot; n_obj 2 = (-delay, -payment)) and masks, the episode sums and done statistics
+    (runner/dcml_runner.py _track / insert)."""
+    a = InsArgs()
+    for k, (src, dst) in enumerate(copies):
+        assert src.dtype == dst.dtype == torch.float32 and src.numel() == dst.numel()
+        assert src.is_contiguous() and dst.is_contiguous()
+        a.seg[k] = InsSeg(src.data_ptr(), dst.data_ptr(), src.numel())
+    E, A, n_obj = rew_slot.shape
+    a.E, a.A, a.n_obj = E, A, n_obj
+    for n, t in (("reward", reward), ("delay", delay), ("pay", pay), ("done", done), ("d_rew", rew_slot),
+                 ("d_mask", mask_slot), ("ep_r", ep_r), ("ep_d", ep_d), ("ep_p", ep_p), ("stats", stats)):
+        assert t.is_contiguous(), n
+        setattr(a, n, t.data_ptr())
+    assert done.dtype == torch.bool and stats.dtype == torch.float64 and mask_slot.numel() == E * A
+    check(lib().mdl_rollout_insert(ctypes.byref(a), _stream()), "rollout_insert")
+
+
 # ----------------------------------------------------------------------------------------- DCML env
 class EnvCfg(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in ("E", "W", "A", "P", "obs_dim", "share_dim", "fixed", "preset",

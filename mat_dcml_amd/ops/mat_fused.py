@@ -25,7 +25,8 @@ class DecParams(ctypes.Structure):
                                                "rnd_u", "rnd_n", "out_a", "out_lp")] + \
                [(n, ctypes.c_int) for n in ("B", "L", "act_dim", "n_disc", "stride", "deterministic", "epw", "rmax", "n_tok",
                                             "tok_start", "tok_zero", "stage", "cont")] + \
-               [(n, ctypes.c_void_p) for n in ("wa", "ba", "lnd")]
+               [(n, ctypes.c_void_p) for n in ("wa", "ba", "lnd")] + \
+               [("gen", ctypes.c_int)] + [(n, ctypes.c_uint32) for n in ("rk0", "rk1", "rctr")]
 
 
 sig("mdl_mat_decode", ctypes.POINTER(DecParams), i32, vp)
@@ -133,8 +134,17 @@ def decode(model, rep, ava=None, deterministic=False, stride=1, rand=None):
     pk = decoder_pack(model)
     rep = rep.float().contiguous()
     dev = rep.device
-    if rand is None and not deterministic:
-        rand = {"u": torch.rand(B, L, device=dev), "n": torch.randn(B, L, A, device=dev)}
+    # sampling noise: explicit draws (tests) or in-kernel Philox keyed by a per-model key taken from torch's CPU
+    # generator on first use (torch.manual_seed reproducible; per-rank after Comm.seed_sampling_rng) and a call counter
+    gen = rand is None and not deterministic
+    rk0 = rk1 = rctr = 0
+    if gen:
+        key = getattr(model, "_mdl_draw_key", None)
+        if key is None:
+            key = [int(x) for x in torch.randint(0, 2 ** 31 - 1, (2,))] + [0]
+            model._mdl_draw_key = key
+        rk0, rk1, rctr = key
+        key[2] = (key[2] + 1) & 0xFFFFFFFF
     u = rand["u"].float().contiguous() if rand is not None else None
     n = rand["n"].float().contiguous() if rand is not None else None
     ava_c = ava.float().contiguous() if ava is not None else None
@@ -150,7 +160,7 @@ def decode(model, rep, ava=None, deterministic=False, stride=1, rand=None):
                     P(u).value, P(n).value, P(out_a).value, P(out_lp).value,
                     B, L, A, _n_disc(model, L), int(stride if deterministic else 1), int(bool(deterministic)), epw, rmax,
                     pk["n_tok"], pk["tok_start"], pk["tok_zero"], 0, cont,
-                    P(pk.get("wa")).value, P(pk.get("ba")).value, P(pk.get("lnd")).value)
+                    P(pk.get("wa")).value, P(pk.get("ba")).value, P(pk.get("lnd")).value, int(gen), rk0, rk1, rctr)
     check(lib().mdl_mat_decode(ctypes.byref(prm), model.n_block, kernels._stream()), "mat_decode")
     return out_a, out_lp
 

@@ -137,6 +137,16 @@ sig("mdl_pack_weights", VP, ctypes.c_int, VP)
 MAX_ACTION_DIM = 64 if TRAIN_KERNELS == "ct" else 8
 
 
+def _spread(B, L, SQ, NRP, dev):
+    """Fewer sequences per workgroup when B / SQ tiles would leave CUs idle (the rollout encoder at 256 envs ran
+    52 workgroups of 5 sequences on a 256-CU device)."""
+    n_cu = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 1
+    sq = max(1, min(SQ, -(-B // n_cu)))
+    if sq == SQ:
+        return SQ, NRP
+    return sq, max(64, ((sq * L + 31) // 32) * 32)
+
+
 def geometry(L):
     """(SQ sequences per tile, NRP padded rows, kernel-variant suffix) — the first variant whose tiling fits L."""
     for sfx in VARIANTS:
@@ -328,6 +338,8 @@ class EncoderFused:
         B, L, od = obs.shape
         dev = obs.device
         SQ, NRP, sfx = geometry(L)
+        if not save:   # rollout / value passes: small batches — spread them over every CU (nothing is saved, so
+            SQ, NRP = _spread(B, L, SQ, NRP, dev)   # the backward's tiling need not match)
         n_tok = B * L
         obs = obs.float().contiguous()
         pre = stat = None

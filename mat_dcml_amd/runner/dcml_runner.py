@@ -129,8 +129,36 @@ class DCMLRunner:
             with self.timers("env"):
                 obs, share, reward, done, delay, pay, ava = self.envs.step(actions)
             with self.timers("insert"):
-                self._track(reward, done, delay, pay)
-                self.insert(obs, share, reward, done, ava, values, actions, logp, delay, pay)
+                if not self._insert_fused(obs, share, reward, done, ava, values, actions, logp, delay, pay):
+                    self._track(reward, done, delay, pay)
+                    self.insert(obs, share, reward, done, ava, values, actions, logp, delay, pay)
+
+    def _insert_fused(self, obs, share, reward, done, ava, values, actions, logp, delay, pay):
+        """_track + insert as one HIP launch (ops/kernels.rollout_insert) when every operand is a contiguous f32
+        device tensor of the buffer's slot size; False -> the torch path."""
+        b = self.buffer
+        if getattr(self, "_ins_ok", None) is None:
+            from ..ops import kernels
+            self._ins_ok = (self.device.type == "cuda" and kernels.available() and b.share_obs is not None
+                            and b.n_objective in (1, 2))
+        if not self._ins_ok:
+            return False
+        from ..ops import kernels
+        t = b.step
+        sh = share if share.dim() == 2 else share[:, 0]
+        pairs = [(sh, b.share_obs[t + 1]), (obs, b.obs[t + 1]), (ava, b.available_actions[t + 1]),
+                 (actions, b.actions[t]), (logp, b.action_log_probs[t]), (values, b.value_preds[t])]
+        for src, dst in pairs:
+            if (src.dtype != torch.float32 or src.numel() != dst.numel() or not src.is_contiguous()
+                    or not dst.is_contiguous()):
+                return False
+        if done.dtype != torch.bool or not b.rewards[t].is_contiguous():
+            return False
+        kernels.rollout_insert(pairs, reward.contiguous(), delay.contiguous(), pay.contiguous(), done.contiguous(),
+                               b.rewards[t], b.masks[t + 1], self._ep_reward, self._ep_delay, self._ep_pay,
+                               self._done_stats)
+        b.step = (t + 1) % b.T
+        return True
 
     def _track(self, reward, done, delay, pay):
         self._ep_reward += reward

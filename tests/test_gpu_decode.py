@@ -42,12 +42,19 @@ def test_decode_matches_torch(gpu, L, B, det):
     disc = slice(0, L - 1)
     agree = (a_ref[:, disc] == a_k[:, disc]).float().mean().item()
     assert agree > 0.97, agree
+    # localised by row: the first divergence of an env propagates to its later rows, so disagreement grows with the
+    # row index; a fault confined to some rows would stand out well above the average bound
+    if B >= 64:
+        per_row = (a_ref[:, disc] != a_k[:, disc]).float().mean(0).squeeze(-1)
+        assert per_row.max().item() < 0.1, per_row.tolist()
     assert (a_k[:, disc][ava[:, disc, 1:] == 0] == 0).all()  # masked workers never selected
     # kernel log-probs are the teacher-forced log-probs of the kernel's own actions
     with torch.no_grad():
         lp_tf, _ = act.parallel_act(m, rep, obs, a_k, ava)
     err = (lp_tf - lp_k).abs()
     assert err.mean().item() < 2e-2 and err.max().item() < 0.2, (err.mean().item(), err.max().item())
+    row_err = err.mean(0).view(-1)
+    assert row_err.max().item() < 4e-2, row_err.tolist()
     if det:
         assert torch.allclose(a_ref[:, -1], a_k[:, -1], atol=5e-2)
 
@@ -117,3 +124,25 @@ def test_decode_continuous_matches_torch(gpu, L, A, B, det):
         lp_tf, _ = act.parallel_act(m, rep, obs, a_k, ava)
     err = (lp_tf - lp_k).abs()
     assert err.mean().item() < 2e-2 and err.max().item() < 0.2, (err.mean().item(), err.max().item())
+
+
+def test_decode_inkernel_draws(gpu):
+    """rand=None: the kernel draws its own Philox noise.  Discrete rows: the frequency of action 1 matches the mean
+    probability the kernel assigned to it (from its own log-probs); the continuous last row: the standardised
+    samples recovered from the log-probs have E[z^2] = 1; successive calls draw fresh noise."""
+    L, B = 9, 4096
+    m = make(L, gpu, seed=5)
+    obs, ava, rep, _ = inputs(m, B, L, gpu)
+    ava = torch.ones_like(ava)
+    a1, lp1 = mat_fused.decode(m, rep, ava, False, 1, None)
+    a2, _ = mat_fused.decode(m, rep, ava, False, 1, None)
+    torch.cuda.synchronize()
+    assert not torch.equal(a1, a2)
+    a, p = a1[:, :L - 1, 0], lp1[:, :L - 1, 0].exp()
+    p1 = torch.where(a == 1, p, 1 - p)                      # P(action 1) of every (env, row)
+    freq, mean_p = (a == 1).float().mean(0), p1.mean(0)
+    se = (mean_p * (1 - mean_p) / B).sqrt()
+    assert ((freq - mean_p).abs() < 5 * se + 1e-3).all(), (freq.tolist(), mean_p.tolist())
+    sd = m.action_std().float()[-1]
+    z2 = -2 * (lp1[:, -1, 0] + sd.log() + 0.9189385332)
+    assert abs(z2.mean().item() - 1) < 5 * (2 / B) ** 0.5, z2.mean().item()

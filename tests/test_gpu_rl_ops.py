@@ -126,3 +126,35 @@ def test_mb_stats_matches_torch(gpu):
         ref = torch.cat([r.sum(0), (r * r).sum(0), torch.tensor([float(r.shape[0])], device=gpu, dtype=torch.float64),
                          act[idx].double().sum().reshape(1)])
         assert torch.allclose(out[m], ref, rtol=1e-10, atol=1e-8), (m, out[m], ref)
+
+
+@pytest.mark.parametrize("n_obj", [1, 2])
+def test_rollout_insert_matches_torch(gpu, n_obj):
+    """the one-launch rollout bookkeeping (kernels.rollout_insert) == DCMLRunner._track + insert (torch path):
+    buffer slots, agent-expanded rewards / masks, episode sums and the finished-episode statistics"""
+    from mat_dcml_amd.config import get_config, parse_args
+    from mat_dcml_amd.runner.dcml_runner import DCMLRunner
+    argv = ["--n_workers", "8", "--n_rollout_threads", "40", "--episode_length", "6"]
+    if n_obj == 2:
+        argv += ["--n_objective", "2"]
+    args = parse_args(argv, get_config(), warn=False)
+    runs = []
+    for fused in (False, True):
+        torch.manual_seed(3)
+        r = DCMLRunner({"all_args": args, "device": gpu, "run_dir": None})
+        assert r.buffer.n_objective == n_obj
+        if not fused:
+            r._ins_ok = False
+        r.warmup()
+        r.rollout()
+        torch.cuda.synchronize()
+        runs.append(r)
+    a, b = runs
+    assert b._ins_ok
+    for name in ("obs", "share_obs", "available_actions", "actions", "action_log_probs", "value_preds", "rewards",
+                 "masks"):
+        torch.testing.assert_close(getattr(a.buffer, name), getattr(b.buffer, name), rtol=0, atol=0, msg=name)
+    assert a.buffer.step == b.buffer.step
+    for name in ("_ep_reward", "_ep_delay", "_ep_pay"):
+        torch.testing.assert_close(getattr(a, name), getattr(b, name), rtol=1e-6, atol=1e-4, msg=name)
+    torch.testing.assert_close(a._done_stats, b._done_stats, rtol=1e-9, atol=1e-6)
