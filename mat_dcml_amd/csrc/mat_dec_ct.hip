@@ -119,7 +119,7 @@ __device__ __forceinline__ void cross_attn_fwd_ct(const Mat* m, const LNp& ln, C
 // backward: dx (w.r.t. the sublayer output) -> d x1 (returned in dx); d rep accumulated into global drep
 __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, CT* dx, const float* rep, float* drep,
                                                   const bf16_t* sv_x1, const bf16_t* sv_a, const float* sv_lse,
-                                                  const Ctx& c) {
+                                                  bool first, const Ctx& c) {
   const int lane = c.lane;
   CT dres[MAXRT];
   {
@@ -214,9 +214,12 @@ __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, C
   {
     CT cur[MAXRT];
 #pragma unroll
-    for (int k = 0; k < MAXRT; ++k) {   // d rep read-modify-write (each row owned by exactly one wave of one workgroup)
-      const int rt = c.wave + NW * k;
-      if (rt < c.NT) cur[k] = ld_gf(drep, c.tok0, rt, c.NR, lane);
+    for (int k = 0; k < MAXRT; ++k) {   // d rep read-modify-write (each row owned by exactly one wave of one workgroup);
+      const int rt = c.wave + NW * k;   // the first block written (the last decoder block) overwrites: no zero fill
+      if (rt < c.NT) {
+        if (first) ct_zero(cur[k]);
+        else cur[k] = ld_gf(drep, c.tok0, rt, c.NR, lane);
+      }
     }
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
@@ -336,6 +339,10 @@ __device__ __forceinline__ HeadStat head_stats(const DecP& p, const f32x4* L, un
 
 constexpr float HALF_LOG_2PI = 0.91893853320467274f;
 
+// Normal-head std = sigmoid(log_std) * 0.5 (transformer_act.py:6, ma_transformer.py action std), from the parameter
+// itself (round 1 read a per-minibatch torch copy: three launches per minibatch)
+__device__ __forceinline__ float head_sd(const DecP& p, int a) { return 0.5f / (1.f + __expf(-p.log_std[a])); }
+
 template <int MA, bool CONT>
 __device__ __forceinline__ void head_fwd_ct(const DecP& p, const CT* xr, bool save, const Ctx& c) {
   const int lane = c.lane, g = lane >> 4;
@@ -368,7 +375,7 @@ __device__ __forceinline__ void head_fwd_ct(const DecP& p, const CT* xr, bool sa
           for (int r = 0; r < 4; ++r) {
             const int a = 16 * ma + 4 * g + r;
             if (ok && a < p.A) {
-              const float sd = p.stdv[a], z = (p.act[tok * p.A + a] - L[ma][r]) / sd;
+              const float sd = head_sd(p, a), z = (p.act[tok * p.A + a] - L[ma][r]) / sd;
               p.logp[tok * p.A + a] = -0.5f * z * z - __logf(sd) - HALF_LOG_2PI;
               p.ent[tok * p.A + a] = 0.5f + HALF_LOG_2PI + __logf(sd);
             }
@@ -383,7 +390,7 @@ __device__ __forceinline__ void head_fwd_ct(const DecP& p, const CT* xr, bool sa
         lp = st.la;
         en = st.H;
       } else {
-        const float sd = p.stdv[p.A - 1], z = (actf - st.mean) / sd;
+        const float sd = head_sd(p, p.A - 1), z = (actf - st.mean) / sd;
         lp = -0.5f * z * z - __logf(sd) - HALF_LOG_2PI;
         en = 0.5f + HALF_LOG_2PI + __logf(sd);
       }
@@ -471,7 +478,7 @@ __device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c)
             for (int r = 0; r < 4; ++r) {
               const int a = 16 * ma + 4 * g + r;
               if (ok && a < p.A) {
-                const float sd = p.stdv[a], diff = p.act[tok * p.A + a] - L[ma][r];
+                const float sd = head_sd(p, a), diff = p.act[tok * p.A + a] - L[ma][r];
                 const float dl = p.dlogp[tok * p.A + a], de = p.dent[tok * p.A + a];
                 Z[ma][r] = dl * diff / (sd * sd);
                 const float dsd = dl * (diff * diff / (sd * sd * sd) - 1.f / sd) + de / sd;
@@ -491,7 +498,7 @@ __device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c)
               Z[ma][r] = (ok && a < p.A) ? z : 0.f;
             }
         } else {
-          const float sd = p.stdv[p.A - 1], diff = actf - st.mean;
+          const float sd = head_sd(p, p.A - 1), diff = actf - st.mean;
 #pragma unroll
           for (int ma = 0; ma < MA; ++ma)
 #pragma unroll
@@ -632,7 +639,7 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
     Ctx cc = c;
     asm volatile("" : "+v"(cc.lane), "+v"(cc.tid));
     mlp_bwd_ct(B.m[8], B.m[9], B.ln[2], dx, p.sv[bb].x2, p.sv[bb].h, cc);
-    cross_attn_bwd_ct(B.m, B.ln[1], dx, p.rep, p.drep, p.sv[bb].x1, p.sv[bb].a2, p.sv[bb].lse2, cc);
+    cross_attn_bwd_ct(B.m, B.ln[1], dx, p.rep, p.drep, p.sv[bb].x1, p.sv[bb].a2, p.sv[bb].lse2, bb == NB - 1, cc);
     self_attn_bwd_ct(B.m, B.ln[0], dx, p.sv[bb].xin, p.sv[bb].a1, p.sv[bb].lse1, true, cc);
   }
   // ---------------- embedding backward: dW_a[:, token] += d pre ; LN_dec params

@@ -214,6 +214,7 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
     const CT w0 = ld_vec(p.wh2, lane);
     CT w1;
     if (p.n_obj > 1) w1 = ld_vec(p.wh2 + 64, lane); else ct_zero(w1);
+    float sdv0 = 0.f, sdv1 = 0.f;   // Σ dv of this lane's tokens (value-head bias gradient)
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
       const int rt = c.wave + NW * k;
@@ -222,6 +223,8 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
         const size_t tok = (size_t)(c.tok0 + (ok ? rt * 16 + (lane & 15) : 0));
         const float dv0 = ok ? p.dv[tok * p.n_obj] : 0.f;
         const float dv1 = (ok && p.n_obj > 1) ? p.dv[tok * p.n_obj + 1] : 0.f;
+        sdv0 += dv0;
+        sdv1 += dv1;
         const CT& hh = hhs[k];
         CT gl = hh, xh, n, dn, dg;
         gelu_ct(gl);
@@ -259,6 +262,13 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
     flush_vec(dlb, c.g(p.lnh.db), lane);
     flush_vec(dw0, c.g(p.d_wh2), lane);
     if (p.n_obj > 1) flush_vec(dw1, c.g(p.d_wh2 ? p.d_wh2 + 64 : nullptr), lane);
+    if (p.d_bh2) {   // lanes g = 0 carry each token once
+      const float s0 = group_sum<16>(sdv0), s1 = group_sum<16>(sdv1);
+      if (lane == 0) {
+        atomicAdd(c.g(p.d_bh2), s0);
+        if (p.n_obj > 1) atomicAdd(c.g(p.d_bh2) + 1, s1);
+      }
+    }
     __syncthreads();
     wgrad64(c.DQ, c.XB, p.h1, c);
     __syncthreads();

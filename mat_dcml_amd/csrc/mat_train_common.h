@@ -81,6 +81,7 @@ struct EncP {
   const float* dv;
   long long g_delta, g_stride;   // dW workspace: copy k of a gradient lives at grad + g_delta + k * g_stride
   int g_copies;                  // 0: atomics straight into the gradients
+  float* d_bh2;                  // value-head bias gradient Σ dv (round-2 backward; null: summed by the caller)
 };
 
 struct DecP {

@@ -43,7 +43,7 @@ class EncP(ctypes.Structure):
                                   "d_be", "d_ln0_g", "d_ln0_b")] + \
                [("blk", Blk * 3), ("h1", Mat), ("lnh", LNp), ("wh2", VP), ("bh2", VP), ("d_wh2", VP), ("rep", VP),
                 ("v", VP), ("sv", Sv * 3), ("drep", VP), ("dv", VP), ("g_delta", ctypes.c_longlong),
-                ("g_stride", ctypes.c_longlong), ("g_copies", ctypes.c_int)]
+                ("g_stride", ctypes.c_longlong), ("g_copies", ctypes.c_int), ("d_bh2", VP)]
 
 
 class DecP(ctypes.Structure):
@@ -381,11 +381,15 @@ class EncoderFused:
         if p.g_copies:
             check_grad_ptrs(p, m._mdl_gws_buf[1])
         dpre = torch.empty_like(pre) if pre is not None else None
+        b = m.encoder.head[3].bias
+        in_kernel = sfx == "_ct" and b.grad is not None   # the CT backward sums dv into the bias gradient itself
+        p.d_bh2 = b.grad.data_ptr() if in_kernel else None
+        if in_kernel and p.g_copies:
+            check_grad_ptrs(p, m._mdl_gws_buf[1])
         check(_enc_bwd(sfx, p, _ptr(pre), _ptr(dpre), m.n_block), "mat_enc_bwd")
         if pre is not None:
             self.emb.backward(obs.view(-1, od), stat, dpre)
-        b = m.encoder.head[3].bias
-        if b.grad is not None:
+        if b.grad is not None and not in_kernel:
             b.grad.add_(dv.reshape(-1, dv.shape[-1]).sum(0))
 
 
@@ -448,10 +452,10 @@ class DecoderFused:
         m = self.model
         model_pack(m)
         self._build()
-        if m.action_type != "Discrete":
+        B, L, _ = rep.shape
+        if m.action_type != "Discrete" and geometry(L)[2] != "_ct":   # the CT kernels read log_std directly
             with torch.no_grad():
                 self.std.copy_(m.action_std())
-        B, L, _ = rep.shape
         dev = rep.device
         n_tok = B * L
         rep = rep.float().contiguous()
@@ -488,7 +492,8 @@ class DecoderFused:
         p = self.p
         dlogp = dlogp.reshape(-1).float().contiguous()
         dent = dent.reshape(-1).float().contiguous()
-        drep = torch.zeros_like(rep)
+        # the CT backward writes every row of d rep (its last decoder block overwrites); round 1 accumulates
+        drep = torch.empty_like(rep) if sfx == "_ct" else torch.zeros_like(rep)
         p.act, p.ava, p.rep = act.data_ptr(), _ptr(ava_c), rep.data_ptr()
         p.dlogp, p.dent, p.drep, p.sv_head = dlogp.data_ptr(), dent.data_ptr(), drep.data_ptr(), head
         for i, s in enumerate(svs):
