@@ -54,6 +54,9 @@ struct DecParams {
   const float* lnd;      // [2][64] decoder input LayerNorm (cont)
   int gen;               // 1: draw the sampling noise in-kernel (Philox4x32-10, key (rk0, rk1), counter (env, row,
   uint32_t rk0, rk1, rctr;   //    rctr, purpose)) instead of reading rnd_u / rnd_n — no per-step torch.rand launches
+  int avail_cont;        // with cont: "Available_Continuous" (transformer_act.py:234-283) — a categorical over the
+                         // first 2 logits (masked by ava[.., :2]) + Normals over the rest; the action vector
+                         // [onehot(a), x] feeds the next row; log-probs [B][L][act_dim - 1] = [lp(a), lp(x)]
 };
 
 // in-kernel sampling noise: one Philox block per (env, row, purpose); purpose 0 = the categorical uniform (x) and
@@ -264,13 +267,31 @@ __device__ __forceinline__ void head_phase(const DecParams& p, const float* H1, 
     float ev[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) ev[k] = p.ba[4 * q + k];
+    int cat = -1;   // Available_Continuous: the categorical choice over logits 0, 1 (every lane of the row alike)
+    if (p.avail_cont) {
+      const float* av = p.ava ? (stage ? AVA + li * AD : p.ava + oi * AD) : nullptr;
+      const float l0 = (av && av[0] == 0.f) ? -1e10f : lg[0], l1 = (av && av[1] == 0.f) ? -1e10f : lg[1];
+      const float mx = fmaxf(l0, l1), lse = mx + __logf(__expf(l0 - mx) + __expf(l1 - mx));
+      if (p.deterministic) cat = l1 > l0 ? 1 : 0;
+      else {
+        const float uu = stage ? RU[li] : p.gen ? draw_u(p, env0 + m, i) : p.rnd_u[oi];
+        cat = __expf(l0 - lse) < uu ? 1 : 0;
+      }
+      if (q == 0) p.out_lp[oi * (AD - 1)] = (cat ? l1 : l0) - lse;
+    }
     for (int a = 0; a < AD; ++a) {
-      const float mean_a = lg[a], sd = p.stdv[a];
-      const float x = p.deterministic ? mean_a : mean_a + sd * (stage ? RN[li * AD + a] : p.gen ? draw_n(p, env0 + m, i, a) : p.rnd_n[oi * AD + a]);
-      if (q == 0) {
-        const float z = (x - mean_a) / sd;
-        p.out_a[oi * AD + a] = x;
-        p.out_lp[oi * AD + a] = -0.5f * z * z - __logf(sd) - 0.91893853320467274f;
+      float x;
+      if (cat >= 0 && a < 2) {
+        x = a == cat ? 1.f : 0.f;
+        if (q == 0) p.out_a[oi * AD + a] = x;
+      } else {
+        const float mean_a = lg[a], sd = p.stdv[a];
+        x = p.deterministic ? mean_a : mean_a + sd * (stage ? RN[li * AD + a] : p.gen ? draw_n(p, env0 + m, i, a) : p.rnd_n[oi * AD + a]);
+        if (q == 0) {
+          const float z = (x - mean_a) / sd;
+          p.out_a[oi * AD + a] = x;
+          p.out_lp[cat >= 0 ? oi * (AD - 1) + a - 1 : oi * AD + a] = -0.5f * z * z - __logf(sd) - 0.91893853320467274f;
+        }
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) ev[k] += p.wa[(4 * q + k) * AD + a] * x;
@@ -636,6 +657,7 @@ MDL_API int mdl_mat_decode(const DecParams* p, int NB, hipStream_t st) {
   const int epw = p->epw;
   if (epw != 1 || p->act_dim > 64 || p->act_dim < 1) return -1;
   if (p->cont && (!p->wa || !p->ba || !p->lnd || p->n_disc != 0)) return -5;
+  if (p->avail_cont && (!p->cont || p->act_dim < 3)) return -6;
   if (p->rmax < 1 || p->rmax * epw > 16) return -4;
   size_t lds = mat_decode_lds_bytes(NB, epw, p->rmax, p->L);
   if (lds > 160 * 1024) return -2;

@@ -131,7 +131,10 @@ class Decoder(nn.Module):
                                      nn.LayerNorm(n_embd), _init(Linear(n_embd, action_dim)))
             self.mlp = actor() if share_actor else nn.ModuleList([actor() for _ in range(n_agent)])
         else:
-            if action_type in ("Discrete", "Semi_Discrete"):
+            # Available_Continuous feeds the same (A+1)-wide shifted input as the discrete types (start flag +
+            # action vector, transformer_act.py:235-237, :280-281); the reference builds Linear(A, 64) for it
+            # (ma_transformer.py:193-197), which cannot take that input — the first decode step fails there
+            if action_type in ("Discrete", "Semi_Discrete", "Available_Continuous", "Available_Continous"):
                 self.action_encoder = nn.Sequential(_init(Linear(action_dim + 1, n_embd, bias=False), activate=True), nn.GELU())
             else:
                 self.action_encoder = nn.Sequential(_init(Linear(action_dim, n_embd), activate=True), nn.GELU())

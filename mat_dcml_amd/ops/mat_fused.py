@@ -26,7 +26,8 @@ class DecParams(ctypes.Structure):
                [(n, ctypes.c_int) for n in ("B", "L", "act_dim", "n_disc", "stride", "deterministic", "epw", "rmax", "n_tok",
                                             "tok_start", "tok_zero", "stage", "cont")] + \
                [(n, ctypes.c_void_p) for n in ("wa", "ba", "lnd")] + \
-               [("gen", ctypes.c_int)] + [(n, ctypes.c_uint32) for n in ("rk0", "rk1", "rctr")]
+               [("gen", ctypes.c_int)] + [(n, ctypes.c_uint32) for n in ("rk0", "rk1", "rctr")] + \
+               [("avail_cont", ctypes.c_int)]
 
 
 sig("mdl_mat_decode", ctypes.POINTER(DecParams), i32, vp)
@@ -37,10 +38,14 @@ def _is_cont(model):
     return model.action_type in ("Continuous", "Continous")
 
 
+def _is_avail_cont(model):
+    return model.action_type in ("Available_Continuous", "Available_Continous")
+
+
 def _n_disc(model, L):
     if model.action_type == "Discrete":
         return L
-    if _is_cont(model):
+    if _is_cont(model) or _is_avail_cont(model):
         return 0
     return L + model.semi_index if model.semi_index < 0 else model.semi_index
 
@@ -50,8 +55,11 @@ def unsupported_reasons(model, L=None) -> list:
     if not kernels.available():
         return ["HIP library not loaded (kernels=torch or not built)"]
     r = []
-    if model.action_type not in ("Semi_Discrete", "Discrete", "Continuous", "Continous"):
+    if model.action_type not in ("Semi_Discrete", "Discrete", "Continuous", "Continous", "Available_Continuous",
+                                 "Available_Continous"):
         r.append(f"action_type {model.action_type}")
+    if _is_avail_cont(model) and model.action_dim < 3:
+        r.append(f"Available_Continuous with action_dim {model.action_dim} < 3")
     if model.decoder.dec_actor:
         r.append("dec_actor (mat_dec) has no autoregressive decode")
     if model.n_embd != 64 or model.n_head != 2 or model.n_block not in (1, 2, 3):
@@ -103,7 +111,13 @@ def decoder_pack(model):
     A = model.action_dim
     dev = dec.ln.weight.device
     cont = _is_cont(model)
-    if cont:
+    avail = _is_avail_cont(model)
+    if avail:
+        # start row = the [1, 0, ..] token; later rows: W_a[:, 1:] · [onehot(a), x] (no bias), built in-kernel
+        toks = torch.zeros(2, A + 1, device=dev)
+        toks[0, 0] = 1
+        tok_start, tok_zero = 0, 1
+    elif cont:
         # continuous inputs: row 0 = the zero start action; later rows are built in-kernel from the sampled vector
         toks = torch.zeros(2, A, device=dev)
         tok_start, tok_zero = 0, 1
@@ -118,8 +132,13 @@ def decoder_pack(model):
     pack = dict(wpack=mp.decoder_fw, bias=torch.stack([l.bias.detach() for l in lins]).float().contiguous(),
                 lnp=torch.stack(lns).float().contiguous(), emb=emb.contiguous(),
                 wh2=dec.head[3].weight.detach().float().contiguous(), bh2=dec.head[3].bias.detach().float().contiguous(),
-                stdv=std.contiguous(), n_tok=toks.shape[0], tok_start=tok_start, tok_zero=tok_zero, cont=int(cont))
-    if cont:
+                stdv=std.contiguous(), n_tok=toks.shape[0], tok_start=tok_start, tok_zero=tok_zero,
+                cont=int(cont or avail), avail=int(avail))
+    if avail:
+        lin = dec.action_encoder[0]
+        pack.update(wa=lin.weight.detach()[:, 1:].float().contiguous(), ba=torch.zeros(64, device=dev),
+                    lnd=torch.stack([dec.ln.weight.detach(), dec.ln.bias.detach()]).float().contiguous())
+    elif cont:
         lin = dec.action_encoder[0]
         pack.update(wa=lin.weight.detach().float().contiguous(), ba=lin.bias.detach().float().contiguous(),
                     lnd=torch.stack([dec.ln.weight.detach(), dec.ln.bias.detach()]).float().contiguous())
@@ -148,9 +167,9 @@ def decode(model, rep, ava=None, deterministic=False, stride=1, rand=None):
     u = rand["u"].float().contiguous() if rand is not None else None
     n = rand["n"].float().contiguous() if rand is not None else None
     ava_c = ava.float().contiguous() if ava is not None else None
-    cont = pk["cont"]
+    cont, avail = pk["cont"], pk["avail"]
     out_a = torch.empty(B, L, A if cont else 1, device=dev)
-    out_lp = torch.empty(B, L, A if cont else 1, device=dev)
+    out_lp = torch.empty(B, L, (A - 1 if avail else A) if cont else 1, device=dev)
     geo = lib().mdl_mat_decode_geometry(model.n_block, L, min(B, _EPW_CAP))
     epw, rmax = geo & 0xFF, geo >> 8
     if epw <= 0:
@@ -160,7 +179,8 @@ def decode(model, rep, ava=None, deterministic=False, stride=1, rand=None):
                     P(u).value, P(n).value, P(out_a).value, P(out_lp).value,
                     B, L, A, _n_disc(model, L), int(stride if deterministic else 1), int(bool(deterministic)), epw, rmax,
                     pk["n_tok"], pk["tok_start"], pk["tok_zero"], 0, cont,
-                    P(pk.get("wa")).value, P(pk.get("ba")).value, P(pk.get("lnd")).value, int(gen), rk0, rk1, rctr)
+                    P(pk.get("wa")).value, P(pk.get("ba")).value, P(pk.get("lnd")).value, int(gen), rk0, rk1, rctr,
+                    avail)
     check(lib().mdl_mat_decode(ctypes.byref(prm), model.n_block, kernels._stream()), "mat_decode")
     return out_a, out_lp
 

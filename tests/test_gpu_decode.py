@@ -146,3 +146,31 @@ def test_decode_inkernel_draws(gpu):
     sd = m.action_std().float()[-1]
     z2 = -2 * (lp1[:, -1, 0] + sd.log() + 0.9189385332)
     assert abs(z2.mean().item() - 1) < 5 * (2 / B) ** 0.5, z2.mean().item()
+
+
+@pytest.mark.parametrize("L,A,B", [(5, 4, 64), (17, 3, 32)])
+@pytest.mark.parametrize("det", [False, True])
+def test_decode_available_continuous_matches_torch(gpu, L, A, B, det):
+    """"Available_Continuous" (transformer_act.py:234-283): per agent a categorical over the first two logits
+    (availability-masked) plus Normals over the rest; the action vector [onehot(a), x] feeds the next row."""
+    torch.manual_seed(0)
+    m = MultiAgentTransformer(L + 1, 7, A, L, 2, 64, 2, action_type="Available_Continuous").to(gpu)
+    g = torch.Generator().manual_seed(2)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_((torch.randn(p.shape, generator=g) * 0.3).to(gpu))
+    assert mat_fused.supports(m), mat_fused.unsupported_reasons(m)
+    obs, ava, rep, rand = inputs(m, B, L, gpu, A=A)
+    ava = torch.ones(B, L, A, device=gpu)
+    ava[:, 1::2, 1] = 0   # every other agent may not take option 1
+    a_ref, lp_ref = act.autoregressive_act(m, rep, obs, ava, det, 1, rand)
+    a_k, lp_k = mat_fused.decode(m, rep, ava, det, 1, rand)
+    torch.cuda.synchronize()
+    assert a_k.shape == (B, L, A) and lp_k.shape == (B, L, A - 1)
+    assert (a_k[:, 1::2, 1] == 0).all()   # masked option never chosen
+    agree = (a_ref[..., :2] == a_k[..., :2]).all(-1).float().mean().item()
+    assert agree > 0.97, agree
+    with torch.no_grad():
+        lp_tf, _ = act.parallel_act(m, rep, obs, a_k, ava)
+    err = (lp_tf - lp_k).abs()
+    assert err.mean().item() < 2e-2 and err.max().item() < 0.2, (err.mean().item(), err.max().item())
