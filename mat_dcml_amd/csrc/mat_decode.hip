@@ -57,6 +57,10 @@ struct DecParams {
   int avail_cont;        // with cont: "Available_Continuous" (transformer_act.py:234-283) — a categorical over the
                          // first 2 logits (masked by ava[.., :2]) + Normals over the rest; the action vector
                          // [onehot(a), x] feeds the next row; log-probs [B][L][act_dim - 1] = [lp(a), lp(x)]
+  const float* qkv0;     // [n_tok][3][64] block-0 q / k / v (bias included) of every action token, or null:
+                         // with one row per pass (stride 1, token inputs) the head phase writes the NEXT row's
+                         // block-0 query / K / V / residual straight from this table and block 0's projection
+                         // phase (one MFMA GEMM + barrier per agent step) disappears
 };
 
 // in-kernel sampling noise: one Philox block per (env, row, purpose); purpose 0 = the categorical uniform (x) and
@@ -235,7 +239,9 @@ __device__ __forceinline__ void attention_mfma(const bf16_t* KV, int rowK, int r
 __device__ __forceinline__ void head_phase(const DecParams& p, const float* H1, float* LG, const float* lnh,
                                            const int* ROWI, int* PEND, int R, int s, int e, int env0, int tid,
                                            const float* AVA, const float* RU, const float* RN, bool stage,
-                                           const float* wh2, const float* bh2, float* EROW) {
+                                           const float* wh2, const float* bh2, float* EROW,
+                                           bool fast0, const float* QKV0, const float* emb, bf16_t* QT, bf16_t* KV,
+                                           float* XR) {
   const int t = tid >> 4, q = tid & 15;
   const int i = ROWI[t];
   const int AD = p.act_dim, L = p.L;
@@ -313,7 +319,8 @@ __device__ __forceinline__ void head_phase(const DecParams& p, const float* H1, 
     }
     return;
   }
-  if (q != 0 || i < 0 || i < s || i >= e) return;
+  if (i < 0 || i < s || i >= e) return;
+  if (q != 0 && !(fast0 && i < p.n_disc && i + 1 < L)) return;   // fast0: the row's 16 lanes sample alike
   const int m = t / R, env = env0 + m;
   const float* lg = LG + t * SP;
   const size_t oi = (size_t)env * L + i;
@@ -341,9 +348,20 @@ __device__ __forceinline__ void head_phase(const DecParams& p, const float* H1, 
       act = min(cnt, AD - 1);
     }
     const float la = (av && av[act] == 0.f) ? -1e10f : lg[act];
-    p.out_a[oi] = (float)act;
-    p.out_lp[oi] = la - lse;
-    PEND[m * L + i] = act;
+    if (q == 0) {
+      p.out_a[oi] = (float)act;
+      p.out_lp[oi] = la - lse;
+      PEND[m * L + i] = act;
+    }
+    if (fast0 && i + 1 < L) {   // next row (tile row 0 of the next pass): block-0 q / K / V and residual x,
+      const float4* tq = (const float4*)(QKV0 + (size_t)(1 + act) * 192) + q;   // lane q: columns 4q .. 4q+3
+      const float4 vq = tq[0], vk = tq[16], vv = tq[32];
+      const float4 ve = ((const float4*)(emb + (size_t)(1 + act) * 64))[q];
+      *(uint2*)(QT + tmo(0, 4 * q)) = make_uint2(pk2f(vq.x, vq.y), pk2f(vq.z, vq.w));
+      *(uint2*)(KV + kv_off(0, 0, i + 1, 4 * q, L)) = make_uint2(pk2f(vk.x, vk.y), pk2f(vk.z, vk.w));
+      *(uint2*)(KV + kv_off(0, 1, i + 1, 4 * q, L)) = make_uint2(pk2f(vv.x, vv.y), pk2f(vv.z, vv.w));
+      *(float4*)(XR + 4 * q) = ve;
+    }
   } else {
     const int a = AD - 1;
     const float mean_a = lg[a], sd = p.stdv[a];
@@ -404,7 +422,9 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
   float* RN = RU + pad4((size_t)EPW * L);                    // [EPW][L][AD]
   float* EMB = RN + pad4((size_t)EPW * L * AD);              // [n_tok][64] action-embedding rows (float4 reads)
   float* WH2 = EMB + (size_t)p.n_tok * 64;                   // [AD][64], then bh2 [AD]
+  float* QKV0S = WH2 + pad4((size_t)AD * 65);                // [n_tok][3][64] block-0 token table (p.qkv0)
   const bool stage = p.stage != 0;
+  const bool fast0 = p.qkv0 != nullptr && !p.cont && p.stride == 1;   // one row per pass, token inputs
 
   // ---------------------------------------------------------------- one-time loads
   bf16x8 wb[NG][2];
@@ -437,11 +457,21 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
     }
     for (int i = tid; i < p.n_tok * 64; i += 256) EMB[i] = p.emb[i];
     for (int i = tid; i < AD * 65; i += 256) WH2[i] = i < AD * 64 ? p.wh2[i] : p.bh2[i - AD * 64];
+    if (p.qkv0) for (int i = tid; i < p.n_tok * 192; i += 256) QKV0S[i] = p.qkv0[i];
   }
   const float* emb = stage ? EMB : p.emb;
   const float* wh2 = stage ? WH2 : p.wh2;
   const float* bh2 = stage ? WH2 + AD * 64 : p.bh2;
+  const float* qkv0 = stage ? QKV0S : p.qkv0;
   __syncthreads();
+  if (fast0 && tid < 64) {   // row 0 (the start token): block-0 query / K / V / residual x from the table
+    const float* tq = qkv0 + (size_t)p.tok_start * 192;
+    QT[tmo(0, tid)] = f2bf(tq[tid]);
+    KV[kv_off(0, 0, 0, tid, L)] = f2bf(tq[64 + tid]);
+    KV[kv_off(0, 1, 0, tid, L)] = f2bf(tq[128 + tid]);
+    XR[tid] = emb[(size_t)p.tok_start * 64 + tid];
+  }
+  // (the head phase's float4 table reads need 16-byte rows: QKV0S / EMB are float4-aligned pieces of the carve)
 
   // ---------------------------------------------------------------- block schedule (transformer_act.py:37-75)
   int prev_s = -1, s = 0, e = 1;
@@ -467,7 +497,8 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
       for (int b = 0; b < NB; ++b) {
         bf16x8 a[2];
         float xf[16];
-        // ---------------- [A] x = emb(token) (b == 0) or LN3(S) ; q1, k1, v1
+        // ---------------- [A] x = emb(token) (b == 0) or LN3(S) ; q1, k1, v1   (fast0: block 0's came from the table)
+        if (!(fast0 && b == 0)) {
         if (b == 0) {
           const float* row = nullptr;
           if (arow_i >= 0)
@@ -493,6 +524,7 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
           }
         }
         __syncthreads();
+        }
         MDL_PROF_MARK(1);
         // ---------------- [B] causal self-attention over cached rows 0..i
         attention_mfma(KV, kv_row(b, 0, 0, L), kv_row(b, 1, 0, L), QT, XA, ROWI, imax, wave, lane);
@@ -599,7 +631,8 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
       __syncthreads();
       MDL_PROF_MARK(9);
       // ---------------- [J] head LN + W_h2 -> logits; mask, sample, log-prob; record pending tokens
-      head_phase(p, Q, S, LNP + 3 * NB * 128, ROWI, PEND, R, s, e, env0, tid, AVA, RU, RN, stage, wh2, bh2, EROW);
+      head_phase(p, Q, S, LNP + 3 * NB * 128, ROWI, PEND, R, s, e, env0, tid, AVA, RU, RN, stage, wh2, bh2, EROW,
+                 fast0, qkv0, emb, QT, KV, XR);
       __syncthreads();
       MDL_PROF_MARK(10);
     }
@@ -632,7 +665,7 @@ MDL_API int mdl_decode_prof_read(unsigned long long* out) {
 #endif
 
 size_t mat_decode_stage_bytes(int epw, int L, int AD, int n_tok) {
-  return ((size_t)epw * L * (64 + 2 * AD + 1) + (size_t)n_tok * 64 + (size_t)AD * 65) * 4 + 64;   // + padding
+  return ((size_t)epw * L * (64 + 2 * AD + 1) + (size_t)n_tok * (64 + 192) + (size_t)AD * 65) * 4 + 96;   // + padding
 }
 
 size_t mat_decode_lds_bytes(int NB, int epw, int rmax, int L) {

@@ -13,6 +13,7 @@ import ctypes
 import os
 
 import torch
+import torch.nn.functional as F
 
 from . import kernels
 from .kernels import P, check, lib, sig
@@ -27,7 +28,7 @@ class DecParams(ctypes.Structure):
                                             "tok_start", "tok_zero", "stage", "cont")] + \
                [(n, ctypes.c_void_p) for n in ("wa", "ba", "lnd")] + \
                [("gen", ctypes.c_int)] + [(n, ctypes.c_uint32) for n in ("rk0", "rk1", "rctr")] + \
-               [("avail_cont", ctypes.c_int)]
+               [("avail_cont", ctypes.c_int), ("qkv0", ctypes.c_void_p)]
 
 
 sig("mdl_mat_decode", ctypes.POINTER(DecParams), i32, vp)
@@ -134,6 +135,11 @@ def decoder_pack(model):
                 wh2=dec.head[3].weight.detach().float().contiguous(), bh2=dec.head[3].bias.detach().float().contiguous(),
                 stdv=std.contiguous(), n_tok=toks.shape[0], tok_start=tok_start, tok_zero=tok_zero,
                 cont=int(cont or avail), avail=int(avail))
+    if not (cont or avail):
+        # block-0 q / k / v of every token row (the decode's first projection depends only on the previous action)
+        a1 = dec.blocks[0].attn1
+        pack["qkv0"] = torch.stack([F.linear(emb, lin.weight.float(), lin.bias.float())
+                                    for lin in (a1.query, a1.key, a1.value)], 1).contiguous()
     if avail:
         lin = dec.action_encoder[0]
         pack.update(wa=lin.weight.detach()[:, 1:].float().contiguous(), ba=torch.zeros(64, device=dev),
@@ -180,7 +186,7 @@ def decode(model, rep, ava=None, deterministic=False, stride=1, rand=None):
                     B, L, A, _n_disc(model, L), int(stride if deterministic else 1), int(bool(deterministic)), epw, rmax,
                     pk["n_tok"], pk["tok_start"], pk["tok_zero"], 0, cont,
                     P(pk.get("wa")).value, P(pk.get("ba")).value, P(pk.get("lnd")).value, int(gen), rk0, rk1, rctr,
-                    avail)
+                    avail, P(pk.get("qkv0")).value)
     check(lib().mdl_mat_decode(ctypes.byref(prm), model.n_block, kernels._stream()), "mat_decode")
     return out_a, out_lp
 
