@@ -13,6 +13,7 @@ masks, so the speaker / listener / comm scenarios the reference MAT cannot run t
 """
 from __future__ import annotations
 
+import os
 import time
 
 import torch
@@ -97,3 +98,30 @@ class MPERunner(SMACRunner):
             self.writter.add_scalars("eval_average_episode_rewards", {"eval_average_episode_rewards": avg},
                                      total_num_steps)
         return avg
+
+    @torch.no_grad()
+    def render(self):
+        """``render`` of the reference MPE runner (``mpe_runner.py:193-254``): ``render_episodes`` deterministic
+        episodes of env 0, every frame captured when ``save_gifs`` (written to ``<run_dir>/gifs/render.gif``,
+        ``ifi`` seconds per frame); prints the average episode reward.  Returns the frames."""
+        from ..envs.mpe.render import render_frame, save_gif
+        a = self.all_args
+        env = self.envs
+        frames = []
+        for _ in range(a.render_episodes):
+            obs, share, ava = env.reset()
+            if a.save_gifs:
+                frames.append(render_frame(env.world, 0))
+            rewards = []
+            for _ in range(self.episode_length):   # (the reference sleeps to ifi per frame for its live viewer;
+                actions = self.policy.get_actions(None, obs, ava, deterministic=True)[1]   # GIF timing is ifi)
+                obs, share, r, dones, info, ava = env.step(actions)
+                rewards.append(r[:, 0, 0])
+                if a.save_gifs:
+                    frames.append(render_frame(env.world, 0))
+            print("average episode rewards is: " + str(float(torch.stack(rewards).sum(0).mean())))
+        if a.save_gifs and frames and self.comm.is_main:
+            gif_dir = os.path.join(str(self.run_dir) if self.run_dir else ".", "gifs")
+            os.makedirs(gif_dir, exist_ok=True)
+            save_gif(frames, os.path.join(gif_dir, "render.gif"), a.ifi)
+        return frames

@@ -210,3 +210,23 @@ def test_mpe_spread_learns_gpu(gpu):
         ret = float(r.buffer.rewards.mean()) * 25
         first = ret if first is None else first
     assert ret > first + 20, (first, ret)
+
+
+def test_render_gif(tmp_path):
+    """MPE runner render (mpe_runner.py:193-254): deterministic episodes, one frame per step plus the reset frame,
+    written as an animated GIF"""
+    from PIL import Image
+    from mat_dcml_amd.config import _MPE_FLAGS, get_config, parse_args
+    from mat_dcml_amd.runner.mpe_runner import MPERunner
+    args = parse_args(["--env_name", "MPE", "--scenario_name", "simple_spread", "--num_agents", "3",
+                       "--num_landmarks", "3", "--n_rollout_threads", "2", "--episode_length", "5", "--n_block", "1",
+                       "--use_render", "--save_gifs", "--render_episodes", "2"], get_config(), extra=_MPE_FLAGS,
+                      warn=False)
+    args.scenario = args.scenario_name
+    r = MPERunner({"all_args": args, "device": torch.device("cpu"), "run_dir": tmp_path})
+    frames = r.render()
+    assert len(frames) == 2 * (5 + 1) and frames[0].shape == (400, 400, 3)
+    agent_px = (frames[0] == (89, 89, 217)).all(-1).sum()      # AGENT_RGB
+    assert agent_px > 0
+    gif = Image.open(tmp_path / "gifs" / "render.gif")
+    assert gif.n_frames >= 2

@@ -255,7 +255,10 @@ def test_fused_planar_step_matches_torch(scenario, conf, monkeypatch):
             ok &= d <= 2e-3
             err = torch.maximum(err, d)
         frac = ok.float().mean().item()
-        assert frac >= 0.9, f"step {t}: only {frac:.3f} of envs match"
+        if fs.m.kind == "ground":   # the contact switch exists only for ground models
+            assert frac >= 0.9, f"step {t}: only {frac:.3f} of envs match"
+        else:                           # fluid (swimmers) / arm (Reacher): smooth dynamics, every env must match
+            assert frac == 1.0, f"step {t}: {fs.m.kind} model, only {frac:.3f} of envs match"
         assert err.median().item() < 1e-4, f"step {t}: median per-env error {err.median().item():.2e}"
 
 

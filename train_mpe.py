@@ -36,7 +36,10 @@ def main(argv):
     torch.manual_seed(all_args.seed)
     np.random.seed(all_args.seed)
     runner = MPERunner({"all_args": all_args, "device": comm.device, "run_dir": run_dir, "comm": comm})
-    runner.run()
+    if all_args.use_render:   # render_mpe: deterministic episodes of a (restored, --model_dir) policy -> gifs/
+        runner.render()
+    else:
+        runner.run()
     if comm.is_main:
         runner.writter.export_scalars_to_json(os.path.join(runner.log_dir, "summary.json"))
         runner.writter.close()
