@@ -89,37 +89,53 @@ __device__ __forceinline__ f32x4 mfma2(const bf16x8 a[2], const bf16x8 w[2], f32
   return acc;
 }
 
-__device__ __forceinline__ bf16x8 pack8(const float* v) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (short)f2bf(v[j]);
-  return r;
+__device__ __forceinline__ uint32_t pk2f(float a, float b) {   // one v_cvt_pk_bf16_f32 (RNE)
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2v __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2v){a, b}, b2v));
+}
+__device__ __forceinline__ bf16x8 pack8(const float* v) {   // 4 packed conversions
+  typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+  return __builtin_bit_cast(bf16x8, (u4v){pk2f(v[0], v[1]), pk2f(v[2], v[3]), pk2f(v[4], v[5]), pk2f(v[6], v[7])});
 }
 
 // A fragment from an f32 LDS row with fused LayerNorm.  Lane (g = lane>>4, r = lane&15) owns row r, columns
 // 8g..8g+7 and 32+8g..32+8g+7.  xf receives the normalised f32 values (for the residual copy).
+// One pass: Σx and Σx² reduce together (one cross-row exchange chain instead of two) and the elementwise work runs
+// on packed fp32 pairs (v_pk_add / v_pk_mul / v_pk_fma_f32) — this load sits at the head of 3 phases per block.
+typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void afrag_ln(const float* S, const float* gam, const float* bet, int lane,
                                         bf16x8 a[2], float xf[16]) {
   const int g = lane >> 4, r = lane & 15;
   const float* row = S + r * SP;
-  float v[16];
+  f2 v[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { v[j] = row[8 * g + j]; v[8 + j] = row[32 + 8 * g + j]; }
-  float s = 0.f;
+  for (int j = 0; j < 4; ++j) {
+    v[j] = *(const f2*)(row + 8 * g + 2 * j);
+    v[4 + j] = *(const f2*)(row + 32 + 8 * g + 2 * j);
+  }
+  f2 s2 = (v[0] + v[1]) + (v[2] + v[3]) + ((v[4] + v[5]) + (v[6] + v[7]));
+  f2 q2 = v[0] * v[0];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) s += v[j];
-  s = cross_row_sum(s);
-  const float mean = s * (1.f / 64.f);
-  float q = 0.f;
+  for (int j = 1; j < 8; ++j) q2 = v[j] * v[j] + q2;
+  f2 sq = {s2.x + s2.y, q2.x + q2.y};   // (Σx, Σx²) of the lane's 16 values
+  float a0, b0, a1, b1;
+  swap16(sq.x, a0, b0);
+  swap16(sq.y, a1, b1);
+  sq = f2{a0 + b0, a1 + b1};
+  swap32(sq.x, a0, b0);
+  swap32(sq.y, a1, b1);
+  const float mean = (a0 + b0) * (1.f / 64.f);
+  const float var = fmaxf((a1 + b1) * (1.f / 64.f) - mean * mean, 0.f);
+  const float rstd = rsqrtf(var + 1e-5f);
+  const f2 mr = {mean, mean}, rr = {rstd, rstd};
 #pragma unroll
-  for (int j = 0; j < 16; ++j) { const float d = v[j] - mean; q += d * d; }
-  q = cross_row_sum(q);
-  const float rstd = rsqrtf(q * (1.f / 64.f) + 1e-5f);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int c0 = 8 * g + j, c1 = 32 + 8 * g + j;
-    xf[j] = (v[j] - mean) * rstd * gam[c0] + bet[c0];
-    xf[8 + j] = (v[8 + j] - mean) * rstd * gam[c1] + bet[c1];
+  for (int j = 0; j < 4; ++j) {
+    const int c0 = 8 * g + 2 * j, c1 = 32 + 8 * g + 2 * j;
+    const f2 y0 = (v[j] - mr) * rr * *(const f2*)(gam + c0) + *(const f2*)(bet + c0);
+    const f2 y1 = (v[4 + j] - mr) * rr * *(const f2*)(gam + c1) + *(const f2*)(bet + c1);
+    xf[2 * j] = y0.x; xf[2 * j + 1] = y0.y;
+    xf[8 + 2 * j] = y1.x; xf[8 + 2 * j + 1] = y1.y;
   }
   a[0] = pack8(xf);
   a[1] = pack8(xf + 8);
@@ -156,11 +172,6 @@ __device__ __forceinline__ void store_xf(float* X, int lane, const float xf[16])
 }
 
 
-__device__ __forceinline__ uint32_t pk2f(float a, float b) {   // one v_cvt_pk_bf16_f32 (RNE)
-  typedef float f2v __attribute__((ext_vector_type(2)));
-  typedef __bf16 b2v __attribute__((ext_vector_type(2)));
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2v){a, b}, b2v));
-}
 __device__ __forceinline__ float xrow_max(float x) {   // max over the 4 lane rows g of a column c
   float a, b;
   swap16(x, a, b);
@@ -248,14 +259,11 @@ __device__ __forceinline__ void head_phase(const DecParams& p, const float* H1, 
   float v[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) v[k] = H1[t * SP + 4 * q + k];
-  float sm = v[0] + v[1] + v[2] + v[3];
-  sm = group_sum<16>(sm);
+  // one pass: Σx and Σx² reduce side by side (two independent DPP chains instead of two dependent ones)
+  const float sm = group_sum<16>((v[0] + v[1]) + (v[2] + v[3]));
+  const float sq = group_sum<16>((v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]));
   const float mean = sm * (1.f / 64.f);
-  float sq = 0.f;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) { const float d = v[k] - mean; sq += d * d; }
-  sq = group_sum<16>(sq);
-  const float rstd = rsqrtf(sq * (1.f / 64.f) + 1e-5f);
+  const float rstd = rsqrtf(fmaxf(sq * (1.f / 64.f) - mean * mean, 0.f) + 1e-5f);
   float hn[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) hn[k] = (v[k] - mean) * rstd * lnh[4 * q + k] + lnh[64 + 4 * q + k];
