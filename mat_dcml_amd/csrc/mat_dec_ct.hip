@@ -6,6 +6,7 @@
 // The action head's second linear (64 -> A, A <= 64) runs on MFMA in the transposed layout: the logits of a token
 // are spread over its 4 lanes (a = 16ma + 4g + r), so the softmax statistics are in-lane + 2 permlane swaps.
 // Logits use a hi/lo bf16 split of both operands (fp32-like: they feed exp(logp - old_logp)).
+#define MDL_LN_ONEPASS
 #include "mat_train_ct.h"
 
 namespace {
