@@ -180,7 +180,7 @@ __device__ __forceinline__ float xrow_max(float x) {   // max over the 4 lane ro
   return fmaxf(a, b);
 }
 
-// Causal attention of the pass's query rows t (ROWI[t] = agent row i, -1 = dead) over the cached rows 0..i, head h
+// Causal attention of the pass's query rows t (agent row plo + t for t < R, else dead) over the cached rows 0..i, head h
 // = wave (waves 0, 1).  Scores Sᵀ = K·Qᵀ in 32-key chunks: the A rows are keys in the permuted order pi(t, m) =
 // 8(m>>2) + 4t + (m&3), so lane (g, c) of the two MFMA outputs holds S[query c][keys kb + 8g + j] (j < 8) — already
 // the B operand of Oᵀ = Vᵀ·Pᵀ, whose A operand comes from ds_read_b64_tr_b16 of the token-major V cache.
@@ -188,11 +188,11 @@ __device__ __forceinline__ float xrow_max(float x) {   // max over the 4 lane ro
 // Masked keys (j > i, or rows of other caches beyond the chunk) get P = 0; every cache row is finite (zeroed at
 // kernel start, plus 32 zero rows after the last cache) so 0 · V stays 0.
 __device__ __forceinline__ void attention_mfma(const bf16_t* KV, int rowK, int rowV, const bf16_t* QT, bf16_t* XA,
-                                               const int* ROWI, int imax, int wave, int lane) {
+                                               int plo, int R, int imax, int wave, int lane) {
   if (wave >= 2) return;
   const int h = wave, g = lane >> 4, c = lane & 15;
   constexpr float SL2 = 0.17677669529663687f * 1.4426950408889634f;   // 1/sqrt(32) * log2(e)
-  const int iq = ROWI[c];
+  const int iq = c < R ? plo + c : -1;
   const bf16x8 qB = lda_tm(QT, c, 4 * h + g);
   float m = -INFINITY, l = 0.f;
   f32x4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
@@ -248,13 +248,13 @@ __device__ __forceinline__ void attention_mfma(const bf16_t* KV, int rowK, int r
 
 // Action head: LN(head1 output) · W_h2 + b -> logits; availability mask, sampling, log-prob (16 lanes per row).
 __device__ __forceinline__ void head_phase(const DecParams& p, const float* H1, float* LG, const float* lnh,
-                                           const int* ROWI, int* PEND, int R, int s, int e, int env0, int tid,
+                                           int plo, int* PEND, int R, int s, int e, int env0, int tid,
                                            const float* AVA, const float* RU, const float* RN, bool stage,
                                            const float* wh2, const float* bh2, float* EROW,
                                            bool fast0, const float* QKV0, const float* emb, bf16_t* QT, bf16_t* KV,
                                            float* XR) {
   const int t = tid >> 4, q = tid & 15;
-  const int i = ROWI[t];
+  const int i = t < R ? plo + t : -1;   // one env per workgroup: tile row t = agent row plo + t
   const int AD = p.act_dim, L = p.L;
   float v[4];
 #pragma unroll
@@ -267,11 +267,29 @@ __device__ __forceinline__ void head_phase(const DecParams& p, const float* H1, 
   float hn[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) hn[k] = (v[k] - mean) * rstd * lnh[4 * q + k] + lnh[64 + 4 * q + k];
-  for (int a = 0; a < AD; ++a) {
-    const float* w = wh2 + a * 64 + 4 * q;
-    float part = w[0] * hn[0] + w[1] * hn[1] + w[2] * hn[2] + w[3] * hn[3];
-    part = group_sum<16>(part);
-    if (q == 0) LG[t * SP + a] = part + bh2[a];
+  // logits: up to 4 actions (DCML's 2) unrolled with every row lane holding all of them in registers (the
+  // discrete sampling below reads them there, no LDS round trip); larger heads loop and go through LG
+  constexpr int SMALL = 4;
+  const bool small = AD <= SMALL;
+  float lgr[SMALL];
+  if (small) {
+#pragma unroll
+    for (int a = 0; a < SMALL; ++a) {
+      float part = 0.f;
+      if (a < AD) {
+        const float4 w = *(const float4*)(wh2 + a * 64 + 4 * q);
+        part = w.x * hn[0] + w.y * hn[1] + w.z * hn[2] + w.w * hn[3];
+      }
+      lgr[a] = group_sum<16>(part) + (a < AD ? bh2[a] : 0.f);
+      if (q == 0 && a < AD) LG[t * SP + a] = lgr[a];
+    }
+  } else {
+    for (int a = 0; a < AD; ++a) {
+      const float* w = wh2 + a * 64 + 4 * q;
+      float part = w[0] * hn[0] + w[1] * hn[1] + w[2] * hn[2] + w[3] * hn[3];
+      part = group_sum<16>(part);
+      if (q == 0) LG[t * SP + a] = part + bh2[a];
+    }
   }
   if (p.cont) {   // all act_dim dims are Gaussian; the 16 lanes of the row also build the next row's input
     if (i < 0 || i < s || i >= e) return;
@@ -335,27 +353,58 @@ __device__ __forceinline__ void head_phase(const DecParams& p, const float* H1, 
   const size_t li = (size_t)m * L + i;                  // row in the staged (workgroup-local) inputs
   if (i < p.n_disc) {
     const float* av = p.ava ? (stage ? AVA + li * AD : p.ava + oi * AD) : nullptr;
-    float mx = -INFINITY;
-    int amax = 0;
-    for (int a = 0; a < AD; ++a) {
-      const float l = (av && av[a] == 0.f) ? -1e10f : lg[a];
-      if (l > mx) { mx = l; amax = a; }
-    }
-    float se = 0.f;
-    for (int a = 0; a < AD; ++a) se += __expf(((av && av[a] == 0.f) ? -1e10f : lg[a]) - mx);
-    const float lse = mx + __logf(se);
-    int act = amax;
-    if (!p.deterministic) {
-      const float uu = stage ? RU[li] : p.gen ? draw_u(p, env, i) : p.rnd_u[oi];
-      float cdf = 0.f;
-      int cnt = 0;
-      for (int a = 0; a < AD; ++a) {
-        cdf += __expf(((av && av[a] == 0.f) ? -1e10f : lg[a]) - lse);
-        cnt += cdf < uu;
+    const float uu = p.deterministic ? 0.f : stage ? RU[li] : p.gen ? draw_u(p, env, i) : p.rnd_u[oi];
+    int act;
+    float la, lse;
+    if (small) {   // registers, fully unrolled
+      float l[SMALL];
+#pragma unroll
+      for (int a = 0; a < SMALL; ++a) l[a] = a < AD ? ((av && av[a] == 0.f) ? -1e10f : lgr[a]) : -INFINITY;
+      float mx = l[0];
+      int amax = 0;
+#pragma unroll
+      for (int a = 1; a < SMALL; ++a) if (l[a] > mx) { mx = l[a]; amax = a; }
+      float e[SMALL], se = 0.f;
+#pragma unroll
+      for (int a = 0; a < SMALL; ++a) { e[a] = a < AD ? __expf(l[a] - mx) : 0.f; se += e[a]; }
+      lse = mx + __logf(se);
+      act = amax;
+      if (!p.deterministic) {
+        const float inv = 1.f / se;
+        float cdf = 0.f;
+        int cnt = 0;
+#pragma unroll
+        for (int a = 0; a < SMALL; ++a) {
+          cdf += e[a] * inv;
+          cnt += (a < AD) & (cdf < uu);
+        }
+        act = min(cnt, AD - 1);
       }
-      act = min(cnt, AD - 1);
+      la = l[0];
+#pragma unroll
+      for (int a = 1; a < SMALL; ++a) la = act == a ? l[a] : la;
+    } else {
+      float mx = -INFINITY;
+      int amax = 0;
+      for (int a = 0; a < AD; ++a) {
+        const float l = (av && av[a] == 0.f) ? -1e10f : lg[a];
+        if (l > mx) { mx = l; amax = a; }
+      }
+      float se = 0.f;
+      for (int a = 0; a < AD; ++a) se += __expf(((av && av[a] == 0.f) ? -1e10f : lg[a]) - mx);
+      lse = mx + __logf(se);
+      act = amax;
+      if (!p.deterministic) {
+        float cdf = 0.f;
+        int cnt = 0;
+        for (int a = 0; a < AD; ++a) {
+          cdf += __expf(((av && av[a] == 0.f) ? -1e10f : lg[a]) - lse);
+          cnt += cdf < uu;
+        }
+        act = min(cnt, AD - 1);
+      }
+      la = (av && av[act] == 0.f) ? -1e10f : lg[act];
     }
-    const float la = (av && av[act] == 0.f) ? -1e10f : lg[act];
     if (q == 0) {
       p.out_a[oi] = (float)act;
       p.out_lp[oi] = la - lse;
@@ -421,7 +470,6 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
   float* LNP = (float*)ptr; ptr += NLN * 128 * 4;
   int* TOK = (int*)ptr;     ptr += ((EPW * L * 4 + 15) & ~15);
   int* PEND = (int*)ptr;    ptr += ((EPW * L * 4 + 15) & ~15);
-  int* ROWI = (int*)ptr;    ptr += 16 * 4;
   float* EROW = (float*)ptr; ptr += EPW * 64 * 4;            // cont: next row's input embedding per env
   float* REP = (float*)ptr;                                  // staged inputs (p.stage): [EPW][L][64]
   auto pad4 = [](size_t n) { return (n + 3) & ~(size_t)3; };  // keep every region 16-byte aligned
@@ -479,6 +527,7 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
     KV[kv_off(0, 1, 0, tid, L)] = f2bf(tq[128 + tid]);
     XR[tid] = emb[(size_t)p.tok_start * 64 + tid];
   }
+  __syncthreads();
   // (the head phase's float4 table reads need 16-byte rows: QKV0S / EMB are float4-aligned pieces of the carve)
 
   // ---------------------------------------------------------------- block schedule (transformer_act.py:37-75)
@@ -488,17 +537,14 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
     if (lo > s) lo = s;
     for (int plo = lo; plo < e; plo += RMAX) {
       const int R = min(RMAX, e - plo);
-      if (tid < 16) {
-        const int m = tid / R, rr = tid % R;
-        ROWI[tid] = (m < n_env && rr < R && tid < EPW * R) ? plo + rr : -1;
-      }
-      __syncthreads();
+      // tile row t = agent row plo + t (t < R; one env per workgroup) — known to every lane, so a pass starts
+      // without publishing a row table (the previous pass ended on a barrier)
       MDL_PROF_MARK(0);
       // per-lane tile rows for the C layout (rows 4*g4 + r) and the A layout (row c16)
       int crow_i[4], crow_m[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) { crow_i[r] = ROWI[4 * g4 + r]; crow_m[r] = (4 * g4 + r) / R; }
-      const int arow_i = ROWI[c16], arow_m = c16 / R;
+      for (int r = 0; r < 4; ++r) { crow_i[r] = 4 * g4 + r < R ? plo + 4 * g4 + r : -1; crow_m[r] = 0; }
+      const int arow_i = c16 < R ? plo + c16 : -1, arow_m = 0;
       const int imax = plo + R - 1;                         // last live agent row of the pass
 
 #pragma unroll
@@ -535,7 +581,7 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
         }
         MDL_PROF_MARK(1);
         // ---------------- [B] causal self-attention over cached rows 0..i
-        attention_mfma(KV, kv_row(b, 0, 0, L), kv_row(b, 1, 0, L), QT, XA, ROWI, imax, wave, lane);
+        attention_mfma(KV, kv_row(b, 0, 0, L), kv_row(b, 1, 0, L), QT, XA, plo, R, imax, wave, lane);
         __syncthreads();
         MDL_PROF_MARK(2);
         // ---------------- [C] proj1 + bias + residual x -> S
@@ -577,7 +623,7 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
         __syncthreads();
         MDL_PROF_MARK(4);
         // ---------------- [E] causal cross-attention (q = rep rows, k/v = x1 rows)
-        attention_mfma(KV, kv_row(b, 2, 0, L), kv_row(b, 3, 0, L), QT, XA, ROWI, imax, wave, lane);
+        attention_mfma(KV, kv_row(b, 2, 0, L), kv_row(b, 3, 0, L), QT, XA, plo, R, imax, wave, lane);
         __syncthreads();
         MDL_PROF_MARK(5);
         // ---------------- [F] proj2 + bias + rep_i -> S
@@ -639,20 +685,23 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
       __syncthreads();
       MDL_PROF_MARK(9);
       // ---------------- [J] head LN + W_h2 -> logits; mask, sample, log-prob; record pending tokens
-      head_phase(p, Q, S, LNP + 3 * NB * 128, ROWI, PEND, R, s, e, env0, tid, AVA, RU, RN, stage, wh2, bh2, EROW,
+      head_phase(p, Q, S, LNP + 3 * NB * 128, plo, PEND, R, s, e, env0, tid, AVA, RU, RN, stage, wh2, bh2, EROW,
                  fast0, qkv0, emb, QT, KV, XR);
       __syncthreads();
       MDL_PROF_MARK(10);
     }
-    // apply the block's actions to the token rows of the next passes (in-block rows kept at zero, as the reference)
-    for (int idx = tid; idx < n_env * L; idx += 256) {
-      const int m = idx / L, i = idx % L;
-      if (i >= s && i < e) {
-        const int a = PEND[m * L + i];
-        if (a >= 0 && i + 1 < L) TOK[m * L + i + 1] = 1 + a;
+    // apply the block's actions to the token rows of the next passes (in-block rows kept at zero, as the reference);
+    // fast0 passes read no token rows (the head phase already wrote the next row's block-0 operands)
+    if (!fast0) {
+      for (int idx = tid; idx < n_env * L; idx += 256) {
+        const int m = idx / L, i = idx % L;
+        if (i >= s && i < e) {
+          const int a = PEND[m * L + i];
+          if (a >= 0 && i + 1 < L) TOK[m * L + i + 1] = 1 + a;
+        }
       }
+      __syncthreads();
     }
-    __syncthreads();
     MDL_PROF_MARK(11);
     prev_s = s;
     if (e >= L) break;
