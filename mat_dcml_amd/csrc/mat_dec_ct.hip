@@ -52,6 +52,9 @@ __device__ __forceinline__ CT dec_embed_pre_ct(const DecP& p, int rt, int& tokid
 // ------------------------------------------------------------------------------------------ cross attention
 // cross-attention projections: q = W_q rep (from global f32), k / v = W_k x1, W_v x1 (x1 = xr, or the saved x1 when
 // xr is null) -> QB / KB / VB; x1 optionally saved (forward) or staged into XB (backward, X of dW_k / dW_v)
+// (REG: x1 comes from the registers xr — a compile-time switch: a runtime `xr ? xr[k] : load` put the register
+// array's address into a pointer select, which kept all of xr in scratch memory in the forward kernel)
+template <bool REG>
 __device__ __forceinline__ void cross_proj(const Mat* m, const CT* xr, const bf16_t* sv_x1_in, const float* rep,
                                            bf16_t* sv_x1_out, const Ctx& c) {
   const int lane = c.lane;
@@ -61,9 +64,10 @@ __device__ __forceinline__ void cross_proj(const Mat* m, const CT* xr, const bf1
     const int rt = c.wave + NW * k;
     if (rt < c.NT) {
       rp[k] = ct_pack(ld_gf(rep, c.tok0, rt, c.NR, lane));
-      xp[k] = xr ? ct_pack(xr[k]) : ld_g(sv_x1_in, c.tok0, rt, c.NR, lane);
+      if constexpr (REG) xp[k] = ct_pack(xr[k]);
+      else xp[k] = ld_g(sv_x1_in, c.tok0, rt, c.NR, lane);
       if (sv_x1_out) st_g(sv_x1_out, c.tok0, rt, c.NR, xp[k], lane);
-      if (!xr) st_lds(c.XB, rt, xp[k], tok_ok(rt, c), lane);
+      if constexpr (!REG) st_lds(c.XB, rt, xp[k], tok_ok(rt, c), lane);
     }
   }
 #pragma unroll
@@ -89,7 +93,7 @@ __device__ __forceinline__ void cross_attn_fwd_ct(const Mat* m, const LNp& ln, C
                                                   bf16_t* sv_a, float* sv_lse, const Ctx& c) {
   const int lane = c.lane;
   __syncthreads();   // every wave done reading the self-attention's K / V
-  cross_proj(m, xr, nullptr, rep, SAVE ? sv_x1 : nullptr, c);
+  cross_proj<true>(m, xr, nullptr, rep, SAVE ? sv_x1 : nullptr, c);
   __syncthreads();
   CP_MARK(24);
   CT O[MAXRT];
@@ -177,7 +181,7 @@ __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, C
   wgrad64(c.DQ, c.XB, m[7], c);
   __syncthreads();
   CP_MARK(5);
-  cross_proj(m, nullptr, sv_x1, rep, nullptr, c);
+  cross_proj<false>(m, nullptr, sv_x1, rep, nullptr, c);
   load_lse(sv_lse, c);
   __syncthreads();
   CP_MARK(6);
