@@ -246,6 +246,53 @@ __device__ __forceinline__ void attention_mfma(const bf16_t* KV, int rowK, int r
   *(uint2*)(xa + 16) = make_uint2(pk2f(o1[0] * il, o1[1] * il), pk2f(o1[2] * il, o1[3] * il));
 }
 
+// categorical sample over <= 4 register logits (every lane of the row computes it alike): availability mask,
+// inverse-CDF draw (argmax when deterministic); returns the action, its masked logit and the log-sum-exp
+constexpr int SMALL_AD = 4;
+__device__ __forceinline__ int sample_small(const float* lgr, int AD, const float* av, float uu, bool det, float& la,
+                                            float& lse) {
+  float l[SMALL_AD];
+#pragma unroll
+  for (int a = 0; a < SMALL_AD; ++a) l[a] = a < AD ? ((av && av[a] == 0.f) ? -1e10f : lgr[a]) : -INFINITY;
+  float mx = l[0];
+  int amax = 0;
+#pragma unroll
+  for (int a = 1; a < SMALL_AD; ++a) if (l[a] > mx) { mx = l[a]; amax = a; }
+  float e[SMALL_AD], se = 0.f;
+#pragma unroll
+  for (int a = 0; a < SMALL_AD; ++a) { e[a] = a < AD ? __expf(l[a] - mx) : 0.f; se += e[a]; }
+  lse = mx + __logf(se);
+  int act = amax;
+  if (!det) {
+    const float inv = 1.f / se;
+    float cdf = 0.f;
+    int cnt = 0;
+#pragma unroll
+    for (int a = 0; a < SMALL_AD; ++a) {
+      cdf += e[a] * inv;
+      cnt += (a < AD) & (cdf < uu);
+    }
+    act = min(cnt, AD - 1);
+  }
+  la = l[0];
+#pragma unroll
+  for (int a = 1; a < SMALL_AD; ++a) la = act == a ? l[a] : la;
+  return act;
+}
+
+// next row's block-0 operands (tile row 0 of the next pass) from the token table: lane q of the row writes
+// columns 4q .. 4q+3 of the query, K, V (bf16) and the residual x (f32)
+__device__ __forceinline__ void write_next_row0(const float* QKV0, const float* emb, int tok, int row, int L, int q,
+                                                bf16_t* QT, bf16_t* KV, float* XR) {
+  const float4* tq = (const float4*)(QKV0 + (size_t)tok * 192) + q;
+  const float4 vq = tq[0], vk = tq[16], vv = tq[32];
+  const float4 ve = ((const float4*)(emb + (size_t)tok * 64))[q];
+  *(uint2*)(QT + tmo(0, 4 * q)) = make_uint2(pk2f(vq.x, vq.y), pk2f(vq.z, vq.w));
+  *(uint2*)(KV + kv_off(0, 0, row, 4 * q, L)) = make_uint2(pk2f(vk.x, vk.y), pk2f(vk.z, vk.w));
+  *(uint2*)(KV + kv_off(0, 1, row, 4 * q, L)) = make_uint2(pk2f(vv.x, vv.y), pk2f(vv.z, vv.w));
+  *(float4*)(XR + 4 * q) = ve;
+}
+
 // Action head: LN(head1 output) · W_h2 + b -> logits; availability mask, sampling, log-prob (16 lanes per row).
 __device__ __forceinline__ void head_phase(const DecParams& p, const float* H1, float* LG, const float* lnh,
                                            int plo, int* PEND, int R, int s, int e, int env0, int tid,
@@ -269,7 +316,7 @@ __device__ __forceinline__ void head_phase(const DecParams& p, const float* H1, 
   for (int k = 0; k < 4; ++k) hn[k] = (v[k] - mean) * rstd * lnh[4 * q + k] + lnh[64 + 4 * q + k];
   // logits: up to 4 actions (DCML's 2) unrolled with every row lane holding all of them in registers (the
   // discrete sampling below reads them there, no LDS round trip); larger heads loop and go through LG
-  constexpr int SMALL = 4;
+  constexpr int SMALL = SMALL_AD;
   const bool small = AD <= SMALL;
   float lgr[SMALL];
   if (small) {
@@ -357,32 +404,7 @@ __device__ __forceinline__ void head_phase(const DecParams& p, const float* H1, 
     int act;
     float la, lse;
     if (small) {   // registers, fully unrolled
-      float l[SMALL];
-#pragma unroll
-      for (int a = 0; a < SMALL; ++a) l[a] = a < AD ? ((av && av[a] == 0.f) ? -1e10f : lgr[a]) : -INFINITY;
-      float mx = l[0];
-      int amax = 0;
-#pragma unroll
-      for (int a = 1; a < SMALL; ++a) if (l[a] > mx) { mx = l[a]; amax = a; }
-      float e[SMALL], se = 0.f;
-#pragma unroll
-      for (int a = 0; a < SMALL; ++a) { e[a] = a < AD ? __expf(l[a] - mx) : 0.f; se += e[a]; }
-      lse = mx + __logf(se);
-      act = amax;
-      if (!p.deterministic) {
-        const float inv = 1.f / se;
-        float cdf = 0.f;
-        int cnt = 0;
-#pragma unroll
-        for (int a = 0; a < SMALL; ++a) {
-          cdf += e[a] * inv;
-          cnt += (a < AD) & (cdf < uu);
-        }
-        act = min(cnt, AD - 1);
-      }
-      la = l[0];
-#pragma unroll
-      for (int a = 1; a < SMALL; ++a) la = act == a ? l[a] : la;
+      act = sample_small(lgr, AD, av, uu, p.deterministic != 0, la, lse);
     } else {
       float mx = -INFINITY;
       int amax = 0;
@@ -410,15 +432,7 @@ __device__ __forceinline__ void head_phase(const DecParams& p, const float* H1, 
       p.out_lp[oi] = la - lse;
       PEND[m * L + i] = act;
     }
-    if (fast0 && i + 1 < L) {   // next row (tile row 0 of the next pass): block-0 q / K / V and residual x,
-      const float4* tq = (const float4*)(QKV0 + (size_t)(1 + act) * 192) + q;   // lane q: columns 4q .. 4q+3
-      const float4 vq = tq[0], vk = tq[16], vv = tq[32];
-      const float4 ve = ((const float4*)(emb + (size_t)(1 + act) * 64))[q];
-      *(uint2*)(QT + tmo(0, 4 * q)) = make_uint2(pk2f(vq.x, vq.y), pk2f(vq.z, vq.w));
-      *(uint2*)(KV + kv_off(0, 0, i + 1, 4 * q, L)) = make_uint2(pk2f(vk.x, vk.y), pk2f(vk.z, vk.w));
-      *(uint2*)(KV + kv_off(0, 1, i + 1, 4 * q, L)) = make_uint2(pk2f(vv.x, vv.y), pk2f(vv.z, vv.w));
-      *(float4*)(XR + 4 * q) = ve;
-    }
+    if (fast0 && i + 1 < L) write_next_row0(QKV0, emb, 1 + act, i + 1, L, q, QT, KV, XR);
   } else {
     const int a = AD - 1;
     const float mean_a = lg[a], sd = p.stdv[a];
@@ -493,6 +507,16 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
   float bcol[NG];
 #pragma unroll
   for (int gi = 0; gi < NG; ++gi) bcol[gi] = p.bias[gi * 64 + 16 * wave + c16];
+  // head1's other three column slices + biases (the fused head of one-row passes runs head1 whole in wave 0)
+  bf16x8 wh1x[3][2];
+  float bh1x[4];
+#pragma unroll
+  for (int ct = 1; ct < 4; ++ct)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      wh1x[ct - 1][ks] = *(const bf16x8*)(p.wpack + ((size_t)(((NG - 1) * 4 + ct) * 2 + ks) * 64 + lane) * 8);
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) bh1x[ct] = p.bias[(NG - 1) * 64 + 16 * ct + c16];
   for (int i = tid; i < NLN * 128; i += 256) LNP[i] = p.lnp[i];
   for (int i = tid; i < EPW * L; i += 256) { TOK[i] = (i % L == 0) ? p.tok_start : p.tok_zero; PEND[i] = -1; }
   for (int i = tid; i < 16 * XP; i += 256) XA[i] = 0;   // dead tile rows keep finite A-operand rows
@@ -672,6 +696,59 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
         __syncthreads();
         MDL_PROF_MARK(8);
       }
+      // ---------------- [I+J fused] one discrete row per pass, <= 4 actions: wave 0 runs head1 for all 64
+      // columns, the head LayerNorm, the logits and the sampling from registers — no Q staging, one barrier
+      if (fast0 && AD <= SMALL_AD && plo < p.n_disc) {
+        if (wave == 0) {
+          bf16x8 a[2];
+          float xf[16];
+          afrag_ln(S, LNP + (3 * (NB - 1) + 2) * 128, LNP + (3 * (NB - 1) + 2) * 128 + 64, lane, a, xf);
+          f32x4 acc[4];
+          acc[0] = mfma2(a, wb[NG - 1], f32x4{0, 0, 0, 0});
+#pragma unroll
+          for (int ct = 1; ct < 4; ++ct) acc[ct] = mfma2(a, wh1x[ct - 1], f32x4{0, 0, 0, 0});
+          if (g4 == 0) {   // lanes 0..15 hold tile row 0 (element r = 0): column 16 ct + c16
+            const float* lnh = LNP + 3 * NB * 128;
+            float x[4];
+#pragma unroll
+            for (int ct = 0; ct < 4; ++ct) x[ct] = gelu_erf(acc[ct][0] + bh1x[ct]);
+            const float sm = group_sum<16>((x[0] + x[1]) + (x[2] + x[3]));
+            const float sq = group_sum<16>((x[0] * x[0] + x[1] * x[1]) + (x[2] * x[2] + x[3] * x[3]));
+            const float mean = sm * (1.f / 64.f);
+            const float rstd = rsqrtf(fmaxf(sq * (1.f / 64.f) - mean * mean, 0.f) + 1e-5f);
+            float xn[4];
+#pragma unroll
+            for (int ct = 0; ct < 4; ++ct) {
+              const int col = 16 * ct + c16;
+              xn[ct] = (x[ct] - mean) * rstd * lnh[col] + lnh[64 + col];
+            }
+            float lgr[SMALL_AD];
+#pragma unroll
+            for (int aa = 0; aa < SMALL_AD; ++aa) {
+              float part = 0.f;
+              if (aa < AD) {
+#pragma unroll
+                for (int ct = 0; ct < 4; ++ct) part += xn[ct] * wh2[aa * 64 + 16 * ct + c16];
+              }
+              lgr[aa] = group_sum<16>(part) + (aa < AD ? bh2[aa] : 0.f);
+            }
+            const int i = plo;
+            const size_t oi = (size_t)env0 * L + i, li = (size_t)i;
+            const float* av = p.ava ? (stage ? AVA + li * AD : p.ava + oi * AD) : nullptr;
+            const float uu = p.deterministic ? 0.f : stage ? RU[li] : p.gen ? draw_u(p, env0, i) : p.rnd_u[oi];
+            float la, lse;
+            const int act = sample_small(lgr, AD, av, uu, p.deterministic != 0, la, lse);
+            if (c16 == 0) {
+              p.out_a[oi] = (float)act;
+              p.out_lp[oi] = la - lse;
+              PEND[i] = act;
+            }
+            if (i + 1 < L) write_next_row0(qkv0, emb, 1 + act, i + 1, L, c16, QT, KV, XR);
+          }
+        }
+        __syncthreads();
+        MDL_PROF_MARK(10);
+      } else {
       // ---------------- [I] head1: GELU(W_h1 · LN3(S) + b) -> Q (f32 staging)
       {
         bf16x8 a[2];
@@ -689,6 +766,7 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
                  fast0, qkv0, emb, QT, KV, XR);
       __syncthreads();
       MDL_PROF_MARK(10);
+      }
     }
     // apply the block's actions to the token rows of the next passes (in-block rows kept at zero, as the reference);
     // fast0 passes read no token rows (the head phase already wrote the next row's block-0 operands)
