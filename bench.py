@@ -42,6 +42,8 @@ def parse():
     p.add_argument("--kernels", default="auto")
     p.add_argument("--dtype", default="bf16")
     p.add_argument("--phases", action="store_true")
+    p.add_argument("--allreduce", default="rccl", choices=["rccl", "oneshot"],
+                   help="data-parallel gradient all-reduce: RCCL (default) or the one-shot peer-memory kernel")
     p.add_argument("--config", default="dcml", choices=["dcml", "smac"],
                    help="dcml: the headline 32-worker DCML config; smac: MAT on the SMAC-shaped 27m_vs_30m stress env")
     p.add_argument("--no_eval", action="store_true", help="skip the post-timing eval sweep (ct / payment / latency)")
@@ -96,6 +98,7 @@ def main():
     from mat_dcml_amd.parallel.comm import init_from_env
     from mat_dcml_amd.runner.dcml_runner import DCMLRunner
 
+    os.environ["MAT_DCML_ALLREDUCE"] = a.allreduce
     comm = init_from_env(prefer_gpu=True)
     if comm.world_size != a.gpus:
         raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={comm.world_size}: the launch does not match")
@@ -160,7 +163,7 @@ def main():
                        "ppo_epoch": a.ppo_epoch, "num_mini_batch": a.num_mini_batch,
                        "device": torch.cuda.get_device_name(dev) if dev.type == "cuda" else "cpu"},
             "ranks": n, "backend": topo["backend"], "rank_devices": topo["devices"], "hosts": topo["hosts"],
-            "kernels": paths,
+            "kernels": paths, "grad_allreduce": getattr(runner.trainer, "grad_allreduce", topo["backend"]) if n > 1 else None,
             "eval": eval_info,
         }), flush=True)
     comm.destroy()
@@ -214,6 +217,7 @@ def bench_smac(a):
     from mat_dcml_amd.config import _SMAC_FLAGS, get_config, parse_args
     from mat_dcml_amd.parallel.comm import init_from_env
     from mat_dcml_amd.runner.smac_runner import SMACRunner
+    os.environ["MAT_DCML_ALLREDUCE"] = a.allreduce
     comm = init_from_env(prefer_gpu=True)
     if comm.world_size != a.gpus:
         raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={comm.world_size}: the launch does not match")

@@ -102,6 +102,8 @@ class MATTrainer:
                 self.fused_reason = "gradient / parameter layouts differ"
                 return False
         self.loss_fused = ppo_fused.PPOLossFused(self, self.device)
+        if self.comm.world_size > 1:
+            self.grad_allreduce = self.comm.maybe_enable_oneshot(flat.buf.numel())
         copies = int(os.environ.get("MAT_DCML_GRAD_COPIES", "8"))
         if copies > 0:
             mat_train.attach_grad_workspace(m, flat.buf, copies=copies)
@@ -195,8 +197,7 @@ class MATTrainer:
             # ONE all-reduce of the whole 0.6 MB flat gradient per minibatch: at this size RCCL over xGMI is
             # latency-bound, so splitting it to overlap the decoder slice with the encoder backward only added a
             # collective (round-1 variant)
-            self.comm.all_reduce_sum_(buf)
-            buf.mul_(1.0 / self.comm.world_size)
+            self.comm.grad_mean_(buf)
             self.collectives += 1
         pol.optimizer.step()
         mat_fused.bump_version(m)

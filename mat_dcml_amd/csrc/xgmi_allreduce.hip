@@ -1,0 +1,146 @@
+// One-shot all-reduce over peer-mapped device memory (the xGMI full mesh of one MI355X node).  SURVEY.md §2.2 /
+// §2.4 "optional oneshot_allreduce P2P kernel"; the reference has no distributed path at all
+// (DCML_MAT_Train.py:104-106 pins cuda:0).
+//
+// Why: the data-parallel gradient is ONE flat fp32 buffer of ~0.6 MB per minibatch (parallel/comm.FlatGrads).  A
+// ring all-reduce over 8 GPUs takes 2(p-1) = 14 dependent hops of 1/8 of that, each bound by ONE xGMI link and by
+// per-hop latency.  On a full mesh every GPU has a direct link to every peer, so each GPU can read its peers'
+// buffers directly: one signal round + one read of (p-1) x 0.6 MB spread over all 7 links at once.
+//
+// Protocol (one launch per all-reduce, G workgroups, each owning the same contiguous slice of the buffer on every
+// rank):
+//   1. WG b copies its slice of the local gradient into this rank's shared buffer half (epoch parity), with
+//      system-scope stores, then fences at system scope;
+//   2. one lane per peer publishes `epoch` into flag[rank][b] of THAT peer's region (release, system scope), and
+//      one lane per peer waits for flag[peer][b] >= epoch in this rank's region (acquire, system scope);
+//   3. WG b sums slice b of every rank's buffer half in rank order 0..p-1 (so every rank gets bit-identical
+//      results) and writes scale * sum to the output.
+// Two buffer halves alternate by epoch parity: a rank can only overwrite half (e & 1) at epoch e + 2 after every
+// peer signalled epoch e + 1 for the slice, i.e. after every peer's epoch-e kernel (same stream) has finished
+// reading it.  Waits are bounded: a missing peer sets the local error word and the kernel exits (never a hang);
+// the host checks the word (`mdl_ar_error`).  All cross-GPU traffic uses vector-memory loads / stores / atomics.
+#include "common.h"
+#include <cstring>
+
+namespace {
+
+constexpr int AR_MAXW = 16;
+constexpr int AR_THREADS = 256;
+
+struct ArArgs {
+  float* region[AR_MAXW];   // every rank's shared region, mapped into this process (own one included)
+  const float* src;         // local input [n]
+  float* dst;               // local output [n] (may alias src)
+  long long n;              // floats per buffer half
+  long long flag_off;       // float offset of the flag array inside a region: flags[sender * G + wg]
+  long long err_off;        // float offset of this rank's error word
+  int world, rank;
+  unsigned epoch;
+  float scale;
+  int spin_max;
+};
+
+__device__ __forceinline__ void st_sys(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ float ld_sys(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(AR_THREADS) void oneshot_allreduce_kernel(ArArgs a) {
+  const int G = gridDim.x, b = blockIdx.x, tid = threadIdx.x;
+  const long long lo = a.n * b / G, hi = a.n * (b + 1) / G;
+  const long long half = (long long)(a.epoch & 1u) * a.n;
+  // 1. publish this rank's slice
+  float* mine = a.region[a.rank] + half;
+  for (long long i = lo + tid; i < hi; i += AR_THREADS) st_sys(mine + i, a.src[i]);
+  __threadfence_system();
+  __syncthreads();
+  // 2. signal every peer, then wait for every peer's signal for this slice
+  if (tid < a.world) {
+    unsigned* f = reinterpret_cast<unsigned*>(a.region[tid] + a.flag_off) + (long long)a.rank * G + b;
+    __hip_atomic_store(f, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    unsigned* w = reinterpret_cast<unsigned*>(a.region[a.rank] + a.flag_off) + (long long)tid * G + b;
+    int it = 0;
+    while (__hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.epoch) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++it > a.spin_max) {   // a peer never arrived: flag the error and leave (results are garbage)
+        atomicOr(reinterpret_cast<unsigned*>(a.region[a.rank] + a.err_off), 1u << (tid & 31));
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  // 3. reduce the slice over ranks in a fixed order
+  for (long long i = lo + tid; i < hi; i += AR_THREADS) {
+    float s = 0.f;
+    for (int r = 0; r < a.world; ++r) s += ld_sys(a.region[r] + half + i);
+    a.dst[i] = s * a.scale;
+  }
+}
+
+long long flag_off_of(long long n) { return 2 * n; }
+long long err_off_of(long long n, int G) { return 2 * n + (long long)AR_MAXW * G; }
+size_t region_bytes(long long n, int G) { return (size_t)(err_off_of(n, G) + 64) * sizeof(float); }
+
+}  // namespace
+
+// region for n floats and G workgroups (zeroed)
+MDL_API int mdl_ar_alloc(long long n, int G, void** out) {
+  if (n <= 0 || G <= 0) return -1;
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, region_bytes(n, G));
+  if (e != hipSuccess) return (int)e;
+  e = hipMemset(p, 0, region_bytes(n, G));
+  if (e != hipSuccess) return (int)e;
+  *out = p;
+  return 0;
+}
+
+MDL_API int mdl_ar_free(void* p) { return (int)hipFree(p); }
+
+MDL_API int mdl_ar_ipc_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
+
+MDL_API int mdl_ar_ipc_handle(void* p, void* out) {
+  hipIpcMemHandle_t h;
+  hipError_t e = hipIpcGetMemHandle(&h, p);
+  if (e != hipSuccess) return (int)e;
+  memcpy(out, &h, sizeof(h));
+  return 0;
+}
+
+MDL_API int mdl_ar_open(const void* handle, void** out) {
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle, sizeof(h));
+  return (int)hipIpcOpenMemHandle(out, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+MDL_API int mdl_ar_close(void* p) { return (int)hipIpcCloseMemHandle(p); }
+
+MDL_API int mdl_ar_run(void* const* regions, int world, int rank, const float* src, float* dst, long long n, int G,
+                       unsigned epoch, float scale, int spin_max, hipStream_t st) {
+  if (world < 1 || world > AR_MAXW || rank < 0 || rank >= world || n <= 0 || G <= 0 || G < 1 || epoch == 0) return -1;
+  ArArgs a{};
+  for (int r = 0; r < world; ++r) {
+    if (!regions[r]) return -2;
+    a.region[r] = static_cast<float*>(regions[r]);
+  }
+  a.src = src;
+  a.dst = dst;
+  a.n = n;
+  a.flag_off = flag_off_of(n);
+  a.err_off = err_off_of(n, G);
+  a.world = world;
+  a.rank = rank;
+  a.epoch = epoch;
+  a.scale = scale;
+  a.spin_max = spin_max;
+  hipLaunchKernelGGL(oneshot_allreduce_kernel, dim3(G), dim3(AR_THREADS), 0, st, a);
+  MDL_CHECK_LAUNCH();
+  return 0;
+}
+
+// this rank's error word (synchronous read): nonzero = some peer never signalled within spin_max
+MDL_API int mdl_ar_error(void* region, long long n, int G, unsigned* out) {
+  return (int)hipMemcpy(out, static_cast<float*>(region) + err_off_of(n, G), sizeof(unsigned), hipMemcpyDeviceToHost);
+}

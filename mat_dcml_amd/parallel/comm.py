@@ -11,6 +11,8 @@ hard-coded to ``cuda:0``).  This module is the new DP layer:
   the right granularity — splitting it into per-layer buckets to overlap with backward only adds latency.
 * ``all_reduce_sum_`` for the small statistics vectors (advantage moments, ValueNorm moments, metrics),
   packed by the callers into one message each.
+* ``grad_mean_`` averages the flat gradient: RCCL by default, or the one-shot peer-memory kernel over the xGMI
+  mesh (``parallel/oneshot.py``, ``csrc/xgmi_allreduce.hip``) with ``MAT_DCML_ALLREDUCE=oneshot``.
 """
 from __future__ import annotations
 
@@ -29,6 +31,7 @@ class Comm:
         self.group = group
         self._flat = None
         self.backend = "none"
+        self.oneshot = None          # OneShotAllReduce of the flat gradient (opt-in)
 
     @property
     def is_main(self):
@@ -88,8 +91,28 @@ class Comm:
         if self._flat is None or not self._flat.owns(params):
             self.attach_flat_grads(params)
         self._flat.ensure_views()
-        dist.all_reduce(self._flat.buf, op=dist.ReduceOp.SUM, group=self.group)
-        self._flat.buf.mul_(1.0 / self.world_size)
+        self.grad_mean_(self._flat.buf)
+
+    def grad_mean_(self, buf: torch.Tensor):
+        """Average the flat gradient buffer over ranks in place: one kernel launch with the one-shot peer-memory
+        all-reduce when enabled for this buffer size (the 1/world scale is applied in-kernel), else RCCL."""
+        if self.world_size == 1:
+            return buf
+        if self.oneshot is not None and buf.numel() == self.oneshot.n and buf.is_cuda:
+            return self.oneshot(buf, scale=1.0 / self.world_size)
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
+        return buf.mul_(1.0 / self.world_size)
+
+    def maybe_enable_oneshot(self, n: int, mode: str | None = None):
+        """Collective: build the one-shot all-reduce for n-float gradients when ``MAT_DCML_ALLREDUCE=oneshot``
+        (or ``mode="oneshot"``) and every rank owns a GPU.  Returns the selected gradient path."""
+        mode = (mode or os.environ.get("MAT_DCML_ALLREDUCE", "rccl")).lower()
+        if self.world_size == 1 or mode != "oneshot" or self.device.type != "cuda":
+            return "none" if self.world_size == 1 else self.backend
+        if self.oneshot is None or self.oneshot.n != n:
+            from .oneshot import OneShotAllReduce
+            self.oneshot = OneShotAllReduce(self, n)
+        return "oneshot"
 
     def all_reduce_sum_async(self, t: torch.Tensor):
         """Start a SUM all-reduce of ``t``; returns a work handle (``wait()`` makes the current stream wait) or None.
@@ -112,6 +135,10 @@ class Comm:
                 "shared_devices": len(set(allv)) < self.world_size}
 
     def destroy(self):
+        if self.oneshot is not None:
+            self.oneshot.check()
+            self.oneshot.close()
+            self.oneshot = None
         if self.world_size > 1 and dist.is_initialized():
             dist.destroy_process_group()
 
