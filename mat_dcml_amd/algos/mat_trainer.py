@@ -213,6 +213,12 @@ class MATTrainer:
         adv_sums = kernels.masked_sums(buffer.advantages, act) if native else rl_ops.masked_sums(buffer.advantages, act)
         dp = self.comm is not None and self.comm.world_size > 1
         if not dp:
+            if native and self.value_normalizer is not None:
+                # single process: the same one-launch per-epoch moments replace a memset + reduction launch per
+                # minibatch inside the fused loss (fixed-order sums instead of fp32 atomics)
+                mbs = kernels.mb_stats(buffer.flat("returns"), buffer.flat("active_masks"), torch.cat(idx_list),
+                                       len(idx_list))
+                return adv_sums, mbs.float().contiguous()
             return adv_sums, None
         mbs = None
         if self.value_normalizer is not None:

@@ -207,10 +207,14 @@ MDL_API int mdl_ppo_finish(const PPOArgs* a, hipStream_t st) {
 struct AdamArgs {
   int n;
   float* p; const float* g; float* m; float* v;
-  float* sumsq;       // [0] sum of squared grads (adam_norm), [1] grad norm (logging), [2] skipped steps
+  float* sumsq;       // [1] grad norm (logging), [2] skipped steps, [4 .. 4 + ADAM_NB) per-workgroup Σ g² partials
   float lr, beta1, beta2, eps, wd, t, max_norm;   // t = optimizer steps attempted so far, this one included
   int clip;
 };
+
+// The norm pass writes one Σ g² partial per workgroup; every step workgroup sums the ADAM_NB partials itself in a
+// fixed order (bit-identical norm everywhere, run to run) — no memset, no same-address atomics.
+constexpr int ADAM_NB = 128;
 
 __global__ __launch_bounds__(256) void adam_norm_kernel(AdamArgs a) {
   __shared__ float sm[4];
@@ -226,20 +230,31 @@ __global__ __launch_bounds__(256) void adam_norm_kernel(AdamArgs a) {
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(a.sumsq, sm[0] + sm[1] + sm[2] + sm[3]);
+  if (threadIdx.x == 0) a.sumsq[4 + blockIdx.x] = (sm[0] + sm[1]) + (sm[2] + sm[3]);
 }
 
 __global__ __launch_bounds__(256) void adam_step_kernel(AdamArgs a) {
-  const float norm = sqrtf(a.sumsq[0]);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    a.sumsq[1] = norm;
-    if (!isfinite(norm)) a.sumsq[2] += 1.f;   // skipped-step counter
+  __shared__ float snorm;
+  if (threadIdx.x < 64) {   // wave 0: Σ of the ADAM_NB partials (two per lane, fixed order)
+    const float v = a.sumsq[4 + threadIdx.x] + a.sumsq[4 + 64 + threadIdx.x];
+    const float tot = wave_sum(v);
+    if (threadIdx.x == 0) snorm = sqrtf(tot);
   }
-  if (!isfinite(norm)) return;   // non-finite guard: skip the whole step (params and moments untouched)
+  __syncthreads();
+  const float norm = snorm;
+  const float skipped = a.sumsq[2];   // read by every workgroup before workgroup 0 may bump it below
+  if (!isfinite(norm)) {   // non-finite guard: skip the whole step (params and moments untouched)
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      a.sumsq[1] = norm;
+      a.sumsq[2] = skipped + 1.f;   // skipped-step counter
+    }
+    return;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.sumsq[1] = norm;
   const float scale = a.clip ? fminf(1.f, a.max_norm / (norm + 1e-6f)) : 1.f;
   // bias corrections from the APPLIED step count (attempted minus skipped non-finite steps, both on device), as
   // torch.optim.Adam, which never sees a skipped step; nobody writes sumsq[2] on a non-skipped step
-  const float t = a.t - a.sumsq[2];
+  const float t = a.t - skipped;
   const float ib1 = 1.f / (1.f - powf(a.beta1, t)), ib2 = 1.f / (1.f - powf(a.beta2, t));
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
     float g = a.g[i] * scale;
@@ -254,11 +269,12 @@ __global__ __launch_bounds__(256) void adam_step_kernel(AdamArgs a) {
   }
 }
 
+MDL_API int mdl_adam_scratch_floats() { return 4 + ADAM_NB; }
+
 MDL_API int mdl_adam(const AdamArgs* a, hipStream_t st) {
   int g = (a->n + 255) / 256;
   if (g > 1024) g = 1024;
-  hipMemsetAsync(a->sumsq, 0, sizeof(float), st);
-  hipLaunchKernelGGL(adam_norm_kernel, dim3(g), dim3(256), 0, st, *a);
+  hipLaunchKernelGGL(adam_norm_kernel, dim3(ADAM_NB), dim3(256), 0, st, *a);
   MDL_CHECK_LAUNCH();
   hipLaunchKernelGGL(adam_step_kernel, dim3(g), dim3(256), 0, st, *a);
   MDL_CHECK_LAUNCH();

@@ -67,9 +67,13 @@ MDL_API int mdl_philox_fill(int64_t* out, int n, uint32_t c1, uint32_t c2, uint3
 //      element (mt, s, lane, j) = M[16*mt + (lane & 15)][32*s + 16*(j >> 2) + 4*(lane >> 4) + (j & 3)]
 struct PackEnt { const float* src; unsigned short* fw; unsigned short* bw; unsigned short* fa; unsigned short* ba; };
 
+// grid (matrices, PACK_SPLIT): each workgroup packs 4096 / PACK_SPLIT elements of one matrix (34 single-workgroup
+// matrices left the launch latency-bound at ~12.6 us; split over 8 it is a one-pass gather/scatter)
+constexpr int PACK_SPLIT = 8;
 __global__ __launch_bounds__(256) void pack_weights_kernel(const PackEnt* tab) {
   const PackEnt e = tab[blockIdx.x];
-  for (int idx = threadIdx.x; idx < 4096; idx += 256) {
+  constexpr int PER = 4096 / PACK_SPLIT;
+  for (int idx = blockIdx.y * PER + threadIdx.x; idx < (blockIdx.y + 1) * PER; idx += 256) {
     const int j = idx & 7, lane = (idx >> 3) & 63, ks = (idx >> 9) & 1, ct = idx >> 10;
     const int n = 16 * ct + (lane & 15), k = 32 * ks + 8 * (lane >> 4) + j;
     if (e.fw) e.fw[idx] = mdl::f2bf(e.src[n * 64 + k]);
@@ -82,7 +86,7 @@ __global__ __launch_bounds__(256) void pack_weights_kernel(const PackEnt* tab) {
 
 MDL_API int mdl_pack_weights(const void* tab, int n, hipStream_t s) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(pack_weights_kernel, dim3(n), dim3(256), 0, s, (const PackEnt*)tab);
+  hipLaunchKernelGGL(pack_weights_kernel, dim3(n, PACK_SPLIT), dim3(256), 0, s, (const PackEnt*)tab);
   MDL_CHECK_LAUNCH();
   return 0;
 }

@@ -91,6 +91,13 @@ def param_offsets(module):
     return out
 
 
+def _adam_scratch_floats():
+    try:
+        return int(lib().mdl_adam_scratch_floats())
+    except Exception:   # CPU-only state handling without the library: same layout (4 + ADAM_NB)
+        return 4 + 128
+
+
 class FlatAdam:
     """Adam + clip over the flat buffers.  The step counter used for the bias corrections is the number of APPLIED
     steps (attempted ``t`` minus the device-side count of skipped non-finite steps), like ``torch.optim.Adam``.
@@ -102,7 +109,8 @@ class FlatAdam:
         self.p, self.g = flat_params, flat_grads
         self.m = torch.zeros_like(flat_params)
         self.v = torch.zeros_like(flat_params)
-        self.scratch = torch.zeros(3, dtype=torch.float32, device=flat_params.device)   # sumsq, norm, skipped
+        # [1] grad norm, [2] skipped steps, [4:] per-workgroup Σ g² partials of the norm pass (csrc/ppo.hip)
+        self.scratch = torch.zeros(_adam_scratch_floats(), dtype=torch.float32, device=flat_params.device)
         self.param_groups = [{"lr": lr, "betas": betas, "eps": eps, "weight_decay": weight_decay}]
         self.max_grad_norm = max_grad_norm
         self.layout = layout   # [(param, flat offset)] (ops/ppo_fused.param_offsets)
