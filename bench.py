@@ -42,8 +42,9 @@ def parse():
     p.add_argument("--kernels", default="auto")
     p.add_argument("--dtype", default="bf16")
     p.add_argument("--phases", action="store_true")
-    p.add_argument("--allreduce", default="rccl", choices=["rccl", "oneshot"],
-                   help="data-parallel gradient all-reduce: RCCL (default) or the one-shot peer-memory kernel")
+    p.add_argument("--allreduce", default="rccl", choices=["rccl", "oneshot", "auto"],
+                   help="data-parallel gradient all-reduce: RCCL (default), the one-shot peer-memory kernel, or auto "
+                        "(one-shot only if it matches RCCL and is faster at start-up)")
     p.add_argument("--config", default="dcml", choices=["dcml", "smac"],
                    help="dcml: the headline 32-worker DCML config; smac: MAT on the SMAC-shaped 27m_vs_30m stress env")
     p.add_argument("--no_eval", action="store_true", help="skip the post-timing eval sweep (ct / payment / latency)")
@@ -164,6 +165,7 @@ def main():
                        "device": torch.cuda.get_device_name(dev) if dev.type == "cuda" else "cpu"},
             "ranks": n, "backend": topo["backend"], "rank_devices": topo["devices"], "hosts": topo["hosts"],
             "kernels": paths, "grad_allreduce": getattr(runner.trainer, "grad_allreduce", topo["backend"]) if n > 1 else None,
+            "grad_allreduce_probe": comm.oneshot_probe,
             "eval": eval_info,
         }), flush=True)
     comm.destroy()

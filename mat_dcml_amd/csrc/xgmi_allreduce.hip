@@ -9,8 +9,8 @@
 //
 // Protocol (one launch per all-reduce, G workgroups, each owning the same contiguous slice of the buffer on every
 // rank):
-//   1. WG b copies its slice of the local gradient into this rank's shared buffer half (epoch parity), with
-//      system-scope stores, then fences at system scope;
+//   1. WG b copies its slice of the local gradient into this rank's shared buffer half (epoch parity), then
+//      fences at system scope;
 //   2. one lane per peer publishes `epoch` into flag[rank][b] of THAT peer's region (release, system scope), and
 //      one lane per peer waits for flag[peer][b] >= epoch in this rank's region (acquire, system scope);
 //   3. WG b sums slice b of every rank's buffer half in rank order 0..p-1 (so every rank gets bit-identical
@@ -34,26 +34,31 @@ struct ArArgs {
   long long n;              // floats per buffer half
   long long flag_off;       // float offset of the flag array inside a region: flags[sender * G + wg]
   long long err_off;        // float offset of this rank's error word
+  long long wait_cycles;    // bound of one peer wait (shader-clock cycles) before the error path
   int world, rank;
   unsigned epoch;
   float scale;
-  int spin_max;
+  int vec;                  // 1: src / dst / regions are 16-byte aligned and n % 4 == 0 (float4 path)
 };
 
-__device__ __forceinline__ void st_sys(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ float ld_sys(const float* p) {
-  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
+// Visibility: the publishing workgroup stores its slice with ordinary stores, then every thread fences at system
+// scope (L2 write-back) before the barrier and the release-store of the flags; the waiting lanes' acquire-load at
+// system scope invalidates this XCD's non-coherent cache lines, and the workgroup barrier orders every thread's
+// peer reads after it — so ordinary (float4) loads of the peers' halves see the published data.
 __global__ __launch_bounds__(AR_THREADS) void oneshot_allreduce_kernel(ArArgs a) {
   const int G = gridDim.x, b = blockIdx.x, tid = threadIdx.x;
-  const long long lo = a.n * b / G, hi = a.n * (b + 1) / G;
   const long long half = (long long)(a.epoch & 1u) * a.n;
+  const long long m = a.vec ? a.n >> 2 : a.n;   // items of this launch: float4s or floats
+  const long long lo = m * b / G, hi = m * (b + 1) / G;
   // 1. publish this rank's slice
   float* mine = a.region[a.rank] + half;
-  for (long long i = lo + tid; i < hi; i += AR_THREADS) st_sys(mine + i, a.src[i]);
+  if (a.vec) {
+    const float4* s4 = reinterpret_cast<const float4*>(a.src);
+    float4* d4 = reinterpret_cast<float4*>(mine);
+    for (long long i = lo + tid; i < hi; i += AR_THREADS) d4[i] = s4[i];
+  } else {
+    for (long long i = lo + tid; i < hi; i += AR_THREADS) mine[i] = a.src[i];
+  }
   __threadfence_system();
   __syncthreads();
   // 2. signal every peer, then wait for every peer's signal for this slice
@@ -61,10 +66,10 @@ __global__ __launch_bounds__(AR_THREADS) void oneshot_allreduce_kernel(ArArgs a)
     unsigned* f = reinterpret_cast<unsigned*>(a.region[tid] + a.flag_off) + (long long)a.rank * G + b;
     __hip_atomic_store(f, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     unsigned* w = reinterpret_cast<unsigned*>(a.region[a.rank] + a.flag_off) + (long long)tid * G + b;
-    int it = 0;
+    const long long t0 = clock64();
     while (__hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.epoch) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++it > a.spin_max) {   // a peer never arrived: flag the error and leave (results are garbage)
+      __builtin_amdgcn_s_sleep(4);
+      if (clock64() - t0 > a.wait_cycles) {   // a peer never arrived: flag the error and leave (garbage results)
         atomicOr(reinterpret_cast<unsigned*>(a.region[a.rank] + a.err_off), 1u << (tid & 31));
         break;
       }
@@ -72,10 +77,25 @@ __global__ __launch_bounds__(AR_THREADS) void oneshot_allreduce_kernel(ArArgs a)
   }
   __syncthreads();
   // 3. reduce the slice over ranks in a fixed order
-  for (long long i = lo + tid; i < hi; i += AR_THREADS) {
-    float s = 0.f;
-    for (int r = 0; r < a.world; ++r) s += ld_sys(a.region[r] + half + i);
-    a.dst[i] = s * a.scale;
+  if (a.vec) {
+    float4* d4 = reinterpret_cast<float4*>(a.dst);
+    for (long long i = lo + tid; i < hi; i += AR_THREADS) {
+      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int r = 0; r < a.world; ++r) {
+        const float4 x = reinterpret_cast<const float4*>(a.region[r] + half)[i];
+        s.x += x.x;
+        s.y += x.y;
+        s.z += x.z;
+        s.w += x.w;
+      }
+      d4[i] = make_float4(s.x * a.scale, s.y * a.scale, s.z * a.scale, s.w * a.scale);
+    }
+  } else {
+    for (long long i = lo + tid; i < hi; i += AR_THREADS) {
+      float s = 0.f;
+      for (int r = 0; r < a.world; ++r) s += a.region[r][half + i];
+      a.dst[i] = s * a.scale;
+    }
   }
 }
 
@@ -118,13 +138,16 @@ MDL_API int mdl_ar_open(const void* handle, void** out) {
 MDL_API int mdl_ar_close(void* p) { return (int)hipIpcCloseMemHandle(p); }
 
 MDL_API int mdl_ar_run(void* const* regions, int world, int rank, const float* src, float* dst, long long n, int G,
-                       unsigned epoch, float scale, int spin_max, hipStream_t st) {
-  if (world < 1 || world > AR_MAXW || rank < 0 || rank >= world || n <= 0 || G <= 0 || G < 1 || epoch == 0) return -1;
+                       unsigned epoch, float scale, long long wait_cycles, hipStream_t st) {
+  if (world < 1 || world > AR_MAXW || rank < 0 || rank >= world || n <= 0 || G <= 0 || epoch == 0) return -1;
   ArArgs a{};
+  bool aligned = (n & 3) == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0;
   for (int r = 0; r < world; ++r) {
     if (!regions[r]) return -2;
     a.region[r] = static_cast<float*>(regions[r]);
+    aligned = aligned && ((uintptr_t)regions[r] & 15) == 0;
   }
+  a.vec = aligned ? 1 : 0;
   a.src = src;
   a.dst = dst;
   a.n = n;
@@ -134,13 +157,13 @@ MDL_API int mdl_ar_run(void* const* regions, int world, int rank, const float* s
   a.rank = rank;
   a.epoch = epoch;
   a.scale = scale;
-  a.spin_max = spin_max;
+  a.wait_cycles = wait_cycles;
   hipLaunchKernelGGL(oneshot_allreduce_kernel, dim3(G), dim3(AR_THREADS), 0, st, a);
   MDL_CHECK_LAUNCH();
   return 0;
 }
 
-// this rank's error word (synchronous read): nonzero = some peer never signalled within spin_max
+// this rank's error word (synchronous read): nonzero = some peer never signalled within wait_cycles
 MDL_API int mdl_ar_error(void* region, long long n, int G, unsigned* out) {
   return (int)hipMemcpy(out, static_cast<float*>(region) + err_off_of(n, G), sizeof(unsigned), hipMemcpyDeviceToHost);
 }

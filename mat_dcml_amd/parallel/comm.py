@@ -32,6 +32,7 @@ class Comm:
         self._flat = None
         self.backend = "none"
         self.oneshot = None          # OneShotAllReduce of the flat gradient (opt-in)
+        self.oneshot_probe = None    # start-up check / timing of the one-shot path (mode "auto")
 
     @property
     def is_main(self):
@@ -104,15 +105,23 @@ class Comm:
         return buf.mul_(1.0 / self.world_size)
 
     def maybe_enable_oneshot(self, n: int, mode: str | None = None):
-        """Collective: build the one-shot all-reduce for n-float gradients when ``MAT_DCML_ALLREDUCE=oneshot``
-        (or ``mode="oneshot"``) and every rank owns a GPU.  Returns the selected gradient path."""
+        """Collective: pick the flat-gradient all-reduce for n-float gradients.  ``MAT_DCML_ALLREDUCE`` (or ``mode``):
+        ``rccl`` (default), ``oneshot`` (forced; every rank raises together if it cannot be built) or ``auto``
+        (``oneshot.probe``: kept only when it matches RCCL and is faster).  Returns the selected path."""
         mode = (mode or os.environ.get("MAT_DCML_ALLREDUCE", "rccl")).lower()
-        if self.world_size == 1 or mode != "oneshot" or self.device.type != "cuda":
-            return "none" if self.world_size == 1 else self.backend
-        if self.oneshot is None or self.oneshot.n != n:
-            from .oneshot import OneShotAllReduce
-            self.oneshot = OneShotAllReduce(self, n)
-        return "oneshot"
+        if self.world_size == 1:
+            return "none"
+        if mode not in ("oneshot", "auto") or self.device.type != "cuda":
+            return self.backend
+        if self.oneshot is not None and self.oneshot.n == n:
+            return "oneshot"
+        from . import oneshot
+        if mode == "oneshot":
+            self.oneshot = oneshot.OneShotAllReduce(self, n)
+            return "oneshot"
+        chosen, ar, self.oneshot_probe = oneshot.probe(self, n)
+        self.oneshot = ar
+        return "oneshot" if chosen == "oneshot" else self.backend
 
     def all_reduce_sum_async(self, t: torch.Tensor):
         """Start a SUM all-reduce of ``t``; returns a work handle (``wait()`` makes the current stream wait) or None.

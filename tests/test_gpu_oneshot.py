@@ -57,6 +57,26 @@ def test_oneshot_allreduce_matches_dist_all_reduce(gpu):
     assert out[0][2] == out[1][2]                # every rank holds the same result
 
 
+def _probe_case(comm):
+    from mat_dcml_amd.parallel import oneshot
+    chosen, ar, info = oneshot.probe(comm, 151_472)
+    if ar is not None:
+        ar.close()
+    return chosen, info
+
+
+@pytest.mark.gpu
+def test_oneshot_probe_agrees_and_decides_identically(gpu):
+    """The start-up probe (mode "auto"): one-shot result matches dist.all_reduce, both are timed, and every rank
+    takes the same decision."""
+    out = spawn(_probe_case, world=2, gpu=True)
+    (c0, i0), (c1, i1) = out[0], out[1]
+    assert c0 == c1 and c0 in ("oneshot", "rccl")
+    assert i0["agree"] and i0["max_rel_err"] <= 1e-5, i0
+    assert i0["oneshot_us"] > 0 and i0["rccl_us"] > 0
+    print("probe:", i0)
+
+
 def _runner_oneshot(comm):
     os.environ["MAT_DCML_ALLREDUCE"] = "oneshot"
     from mat_dcml_amd.config import get_config, parse_args
