@@ -145,9 +145,11 @@ class Comm:
 
     def destroy(self):
         if self.oneshot is not None:
-            self.oneshot.check()
-            self.oneshot.close()
-            self.oneshot = None
+            ar, self.oneshot = self.oneshot, None
+            try:
+                ar.check()   # a timed-out peer wait anywhere in the run fails the run loudly
+            finally:
+                ar.close()
         if self.world_size > 1 and dist.is_initialized():
             dist.destroy_process_group()
 

@@ -248,3 +248,20 @@ def test_dp_runner_ranks_stay_in_sync_at_4_and_8(world):
     for r in range(1, world):
         assert out[r][0] == out[0][0] and out[r][1] == out[0][1] and out[r][3] == out[0][3]
     assert out[0][2] == 2 * (2 + 1)   # 2 epochs x (1 statistics + 2 gradient all-reduces)
+
+
+def _allreduce_mode_case(comm):
+    os.environ["MAT_DCML_ALLREDUCE"] = "auto"
+    path = comm.maybe_enable_oneshot(1024)
+    buf = torch.full((1024,), float(comm.rank + 1))
+    comm.grad_mean_(buf)
+    return path, comm.oneshot is None, float(buf[0])
+
+
+def test_gradient_allreduce_mode_falls_back_to_the_backend_on_cpu():
+    """One-shot needs a GPU per rank: on CPU ranks every mode resolves to the process-group backend, and grad_mean_
+    averages over ranks."""
+    out = spawn(_allreduce_mode_case)
+    for r in (0, 1):
+        path, none, v = out[r]
+        assert path == "gloo" and none and v == 1.5
