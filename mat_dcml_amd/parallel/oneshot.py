@@ -139,8 +139,9 @@ class OneShotAllReduce:
 
 
 def probe(comm, n: int, iters: int = 20, margin: float = 0.95):
-    """Collective: build the one-shot all-reduce for n floats, check it against ``dist.all_reduce`` on random data and
-    time both back to back (median per call, max over ranks).  Returns (chosen, OneShotAllReduce or None, info):
+    """Collective: build the one-shot all-reduce for n floats, check it against ``dist.all_reduce`` (the process
+    group's backend: RCCL on a GPU node) on random data and time both back to back (median per call, max over
+    ranks).  Returns (chosen, OneShotAllReduce or None, info):
     one-shot is chosen only if it agrees with RCCL and is faster by ``margin``; every rank takes the same decision."""
     import torch.distributed as dist
     info = {"n": int(n)}
@@ -178,9 +179,9 @@ def probe(comm, n: int, iters: int = 20, margin: float = 0.95):
     t_rc = timed(lambda: dist.all_reduce(y2, group=comm.group))
     ok = ok and ar.error_word() == 0
     rows = comm.all_gather_object((ok, err, t_os, t_rc))
-    info.update(agree=all(r[0] for r in rows), max_rel_err=max(r[1] for r in rows),
-                oneshot_us=round(max(r[2] for r in rows), 2), rccl_us=round(max(r[3] for r in rows), 2))
-    if info["agree"] and info["oneshot_us"] < margin * info["rccl_us"]:
+    info.update(agree=all(r[0] for r in rows), max_rel_err=max(r[1] for r in rows), backend=comm.backend,
+                oneshot_us=round(max(r[2] for r in rows), 2), backend_us=round(max(r[3] for r in rows), 2))
+    if info["agree"] and info["oneshot_us"] < margin * info["backend_us"]:
         return "oneshot", ar, info
     ar.close()
     return "rccl", None, info
