@@ -7,7 +7,8 @@ Replaces the numpy ``SharedReplayBuffer`` (reference ``mat_src/mat/utils/shared_
 * ``compute_returns`` is GAE on ValueNorm-denormalised values (``shared_buffer.py:207-238``); the reverse
   scan runs as one fused HIP kernel when available (``csrc/rl_ops.hip: gae_reverse_scan``).
 * ``minibatches`` = ``feed_forward_generator_transformer`` (``:240-314``): randperm over the T·E sequences,
-  split into ``num_mini_batch`` chunks, whole agent sequences kept (the agent shuffle is the identity).
+  split into ``num_mini_batch`` chunks, whole agent sequences kept (the agent shuffle is the identity); on the
+  HIP path the permutation is one keyed-Feistel launch (``csrc/rl_ops.hip: randperm_kernel``).
 * ``save`` / ``load`` write and read a ``.pt`` of tensors (the reference ``load`` opened its file with
   ``"wb"`` and truncated it, ``shared_buffer.py:106`` — fixed).
 """
@@ -88,7 +89,11 @@ class RolloutBuffer:
     def minibatch_indices(self, num_mini_batch, generator=None):
         n = self.T * self.E
         mb = n // num_mini_batch
-        perm = torch.randperm(n, device=self.obs.device, generator=generator)
+        from ..ops import kernels
+        if kernels.use_hip(self.obs):   # one keyed-Feistel launch instead of torch's ~10-launch radix sort
+            perm = kernels.randperm(n, self.obs.device, generator)
+        else:
+            perm = torch.randperm(n, device=self.obs.device, generator=generator)
         return [perm[i * mb:(i + 1) * mb] for i in range(num_mini_batch)]
 
     def flat(self, name):

@@ -252,6 +252,7 @@ class MATTrainer:
         acc = torch.zeros(len(keys), device=self.device)
         if self.fused:
             self.loss_fused.out.zero_()
+            pol.optimizer.clear_grad_norm_sum()
         T, E = buffer.T, buffer.E
         obs_f = buffer.flat("obs")
         act_f = buffer.flat("actions")
@@ -283,7 +284,7 @@ class MATTrainer:
                 else:
                     mb = {k: v[idx] for k, v in src.items()}
                 if self.fused:
-                    acc[3:5] += self.ppo_update_fused(mb, None if pre is None else pre[m])
+                    self.ppo_update_fused(mb, None if pre is None else pre[m])   # norm summed in the Adam kernel
                     continue
                 self._vn_pre = None if pre is None else (pre[m, :n_obj], pre[m, n_obj:2 * n_obj], pre[m, 2 * n_obj])
                 vl, gn, pl, ent, ratio = self.ppo_update(mb)
@@ -292,6 +293,7 @@ class MATTrainer:
         if self.fused:   # loss scalars accumulated on device by the loss kernel: [policy, value, entropy, ratio]
             o = self.loss_fused.out
             acc[0], acc[1], acc[2], acc[5] = o[1], o[0], o[2], o[3]
+            acc[3] = acc[4] = pol.optimizer.grad_norm_sum
         acc /= self.ppo_epoch * self.num_mini_batch
         return dict(zip(keys, acc))
 

@@ -207,7 +207,8 @@ MDL_API int mdl_ppo_finish(const PPOArgs* a, hipStream_t st) {
 struct AdamArgs {
   int n;
   float* p; const float* g; float* m; float* v;
-  float* sumsq;       // [1] grad norm (logging), [2] skipped steps, [4 .. 4 + ADAM_NB) per-workgroup Σ g² partials
+  float* sumsq;       // [1] grad norm (logging), [2] skipped steps, [3] Σ of the norms since the trainer cleared it,
+                      // [4 .. 4 + ADAM_NB) per-workgroup Σ g² partials
   float lr, beta1, beta2, eps, wd, t, max_norm;   // t = optimizer steps attempted so far, this one included
   int clip;
 };
@@ -243,14 +244,14 @@ __global__ __launch_bounds__(256) void adam_step_kernel(AdamArgs a) {
   __syncthreads();
   const float norm = snorm;
   const float skipped = a.sumsq[2];   // read by every workgroup before workgroup 0 may bump it below
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    a.sumsq[1] = norm;
+    a.sumsq[3] += norm;   // per-iteration logging sum (the eager path adds every step's norm, finite or not)
+  }
   if (!isfinite(norm)) {   // non-finite guard: skip the whole step (params and moments untouched)
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-      a.sumsq[1] = norm;
-      a.sumsq[2] = skipped + 1.f;   // skipped-step counter
-    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.sumsq[2] = skipped + 1.f;   // skipped-step counter
     return;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) a.sumsq[1] = norm;
   const float scale = a.clip ? fminf(1.f, a.max_norm / (norm + 1e-6f)) : 1.f;
   // bias corrections from the APPLIED step count (attempted minus skipped non-finite steps, both on device), as
   // torch.optim.Adam, which never sees a skipped step; nobody writes sumsq[2] on a non-skipped step

@@ -59,6 +59,41 @@ MDL_API int mdl_philox_fill(int64_t* out, int n, uint32_t c1, uint32_t c2, uint3
   return 0;
 }
 
+// Random permutation of [0, n) in ONE launch (the per-epoch minibatch shuffle; torch.randperm on the device is a
+// radix sort of ~10 launches).  A keyed 6-round Feistel network on [0, 2^(2h)) (2^(2h) >= n, round function =
+// Philox4x32-10 of (half, round)) is a bijection; cycle walking (re-apply until the value lands below n) restricts
+// it to a bijection of [0, n) — each lane walks its own cycle, which returns below n after < 4 steps on average.
+__device__ __forceinline__ uint32_t feistel_perm(uint32_t x, int h, uint32_t k0, uint32_t k1) {
+  const uint32_t mask = (1u << h) - 1u;
+  uint32_t l = x >> h, r = x & mask;
+#pragma unroll
+  for (int rd = 0; rd < 6; ++rd) {
+    const uint32_t f = mdl::philox4x32_10(r, (uint32_t)rd, 0x5EEDu, 0u, k0, k1).x;
+    const uint32_t nr = (l ^ f) & mask;
+    l = r;
+    r = nr;
+  }
+  return (l << h) | r;
+}
+
+__global__ __launch_bounds__(256) void randperm_kernel(int64_t* out, int n, int h, uint32_t k0, uint32_t k1) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t x = (uint32_t)i;
+  do { x = feistel_perm(x, h, k0, k1); } while (x >= (uint32_t)n);
+  out[i] = (int64_t)x;
+}
+
+MDL_API int mdl_randperm(int64_t* out, int n, uint32_t k0, uint32_t k1, hipStream_t s) {
+  if (n <= 0 || n > (1 << 30)) return -1;
+  int bits = 2;
+  while ((1ll << bits) < (long long)n) ++bits;
+  const int h = (bits + 1) / 2;
+  hipLaunchKernelGGL(randperm_kernel, dim3((n + 255) / 256), dim3(256), 0, s, out, n, h, k0, k1);
+  MDL_CHECK_LAUNCH();
+  return 0;
+}
+
 // Repack fp32 Linear weights (64 x 64, [out][in]) into the MFMA fragment orders used by the fused kernels, for W
 // (forward) and W^T (backward) — all matrices of the model in ONE launch after each optimizer step.
 //  * B fragments (decode kernel, round-1 row-layout tiles):

@@ -119,6 +119,19 @@ def philox_fill(n, c1, c2, c3, k0, k1, device):
     return out
 
 
+sig("mdl_randperm", vp, i32, u32, u32, vp)
+
+
+def randperm(n, device, generator=None):
+    """Random permutation of [0, n) (int64, on ``device``) by one keyed-Feistel launch (csrc/rl_ops.hip); the
+    64-bit key is drawn from the CPU generator (``torch.manual_seed`` seeds it), so no device RNG launch either."""
+    g = generator if generator is not None and generator.device.type == "cpu" else None
+    k = torch.randint(0, 2 ** 31 - 1, (2,), generator=g).tolist()
+    out = torch.empty(n, dtype=torch.int64, device=device)
+    check(lib().mdl_randperm(P(out), int(n), int(k[0]), int(k[1]), _stream()), "randperm")
+    return out
+
+
 # ----------------------------------------------------------------------------------------- minibatch / adv stats
 sig("mdl_masked_sums", vp, vp, i32, i32, vp, vp, vp)
 _SUMS_WS = {}

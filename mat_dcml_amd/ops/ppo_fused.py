@@ -109,7 +109,7 @@ class FlatAdam:
         self.p, self.g = flat_params, flat_grads
         self.m = torch.zeros_like(flat_params)
         self.v = torch.zeros_like(flat_params)
-        # [1] grad norm, [2] skipped steps, [4:] per-workgroup Σ g² partials of the norm pass (csrc/ppo.hip)
+        # [1] grad norm, [2] skipped steps, [3] Σ norms (logging), [4:] per-workgroup Σ g² partials (csrc/ppo.hip)
         self.scratch = torch.zeros(_adam_scratch_floats(), dtype=torch.float32, device=flat_params.device)
         self.param_groups = [{"lr": lr, "betas": betas, "eps": eps, "weight_decay": weight_decay}]
         self.max_grad_norm = max_grad_norm
@@ -119,6 +119,14 @@ class FlatAdam:
     @property
     def grad_norm(self):
         return self.scratch[1]
+
+    @property
+    def grad_norm_sum(self):
+        """Σ of the step norms since ``clear_grad_norm_sum`` (accumulated in-kernel: no add launch per step)."""
+        return self.scratch[3]
+
+    def clear_grad_norm_sum(self):
+        self.scratch[3:4].zero_()
 
     @property
     def skipped_steps(self):

@@ -158,3 +158,25 @@ def test_rollout_insert_matches_torch(gpu, n_obj):
     for name in ("_ep_reward", "_ep_delay", "_ep_pay"):
         torch.testing.assert_close(getattr(a, name), getattr(b, name), rtol=1e-6, atol=1e-4, msg=name)
     torch.testing.assert_close(a._done_stats, b._done_stats, rtol=1e-9, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_feistel_randperm_is_a_permutation(gpu):
+    """One-launch minibatch shuffle (csrc/rl_ops.hip randperm_kernel): a bijection of [0, n) for every n, different
+    per key, reproducible under torch.manual_seed, and not close to the identity."""
+    from mat_dcml_amd.ops import kernels
+    dev = torch.device("cuda")
+    for n in (1, 2, 7, 100, 3200, 12800, 40000):
+        p = kernels.randperm(n, dev).cpu()
+        assert torch.equal(torch.sort(p).values, torch.arange(n)), n
+    torch.manual_seed(3)
+    a = kernels.randperm(12800, dev)
+    torch.manual_seed(3)
+    b = kernels.randperm(12800, dev)
+    c = kernels.randperm(12800, dev)
+    assert torch.equal(a, b) and not torch.equal(a, c)
+    fixed = (a.cpu() == torch.arange(12800)).float().mean().item()
+    assert fixed < 0.01
+    # the first minibatch's rows spread evenly over the buffer (the T·E rows are time-major)
+    first = a[:3200].cpu().float()
+    assert abs(first.mean().item() / 12800 - 0.5) < 0.03
