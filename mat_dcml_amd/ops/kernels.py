@@ -122,11 +122,15 @@ def philox_fill(n, c1, c2, c3, k0, k1, device):
 sig("mdl_randperm", vp, i32, u32, u32, vp)
 
 
-def randperm(n, device, generator=None):
-    """Random permutation of [0, n) (int64, on ``device``) by one keyed-Feistel launch (csrc/rl_ops.hip); the
-    64-bit key is drawn from the CPU generator (``torch.manual_seed`` seeds it), so no device RNG launch either."""
-    g = generator if generator is not None and generator.device.type == "cpu" else None
-    k = torch.randint(0, 2 ** 31 - 1, (2,), generator=g).tolist()
+def randperm(n, device, generator=None, key=None):
+    """Random permutation of [0, n) (int64, on ``device``) by one keyed-Feistel launch (csrc/rl_ops.hip; reference
+    ``utils/philox.feistel_randperm``); the key is drawn from the CPU generator (``torch.manual_seed`` seeds it),
+    so no device RNG launch either."""
+    if key is None:
+        g = generator if generator is not None and generator.device.type == "cpu" else None
+        k = torch.randint(0, 2 ** 31 - 1, (2,), generator=g).tolist()
+    else:
+        k = [int(key[0]), int(key[1])]
     out = torch.empty(n, dtype=torch.int64, device=device)
     check(lib().mdl_randperm(P(out), int(n), int(k[0]), int(k[1]), _stream()), "randperm")
     return out

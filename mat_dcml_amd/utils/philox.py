@@ -66,3 +66,29 @@ def u01_open(u: torch.Tensor) -> torch.Tensor:
 def seed_key(seed: int):
     s = int(seed) & 0xFFFFFFFFFFFFFFFF
     return s & MASK32, (s >> 32) ^ 0x5EED5EED
+
+
+def feistel_randperm(n: int, k0: int, k1: int) -> torch.Tensor:
+    """Reference of ``randperm_kernel`` (csrc/rl_ops.hip): a 6-round Feistel network on [0, 2^(2h)) with round
+    function Philox4x32-10(r, round, 0x5EED, 0; k0, k1).x, cycle-walked until the value is below n.  A bijection of
+    [0, n); the kernel's output is bit-identical."""
+    bits = 2
+    while (1 << bits) < n:
+        bits += 1
+    h = (bits + 1) // 2
+    mask = (1 << h) - 1
+
+    def feistel(x):
+        lo, r = x >> h, x & mask
+        for rd in range(6):
+            f = philox4x32(r, rd, 0x5EED, 0, k0, k1)[0]
+            lo, r = r, (lo ^ f) & mask
+        return (lo << h) | r
+
+    x = feistel(torch.arange(n, dtype=torch.int64))
+    out = x.clone()
+    todo = out >= n
+    while bool(todo.any()):
+        out[todo] = feistel(out[todo])
+        todo = out >= n
+    return out

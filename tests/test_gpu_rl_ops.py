@@ -180,3 +180,6 @@ def test_feistel_randperm_is_a_permutation(gpu):
     # the first minibatch's rows spread evenly over the buffer (the T·E rows are time-major)
     first = a[:3200].cpu().float()
     assert abs(first.mean().item() / 12800 - 0.5) < 0.03
+    from mat_dcml_amd.utils.philox import feistel_randperm
+    for n, key in ((12800, (12345, 678)), (3200, (1, 2)), (777, (2 ** 31 - 2, 99))):
+        assert torch.equal(kernels.randperm(n, dev, key=key).cpu(), feistel_randperm(n, *key)), n

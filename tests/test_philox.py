@@ -33,3 +33,15 @@ def test_device_philox_matches_torch(gpu):
     ref = torch.stack(px.philox4x32(c0, 5, 9, 3, 123, 456), -1)
     dev = kernels.philox_fill(4096, 5, 9, 3, 123, 456, gpu).cpu()
     assert torch.equal(dev, ref)
+
+
+def test_feistel_randperm_reference_is_a_permutation():
+    """utils/philox.feistel_randperm (the reference of the HIP minibatch shuffle): a bijection of [0, n) for awkward
+    n, key-dependent, far from the identity."""
+    from mat_dcml_amd.utils.philox import feistel_randperm
+    for n in (1, 2, 3, 5, 64, 1000, 12800):
+        p = feistel_randperm(n, 7, 11)
+        assert torch.equal(torch.sort(p).values, torch.arange(n)), n
+    a, b = feistel_randperm(12800, 7, 11), feistel_randperm(12800, 8, 11)
+    assert not torch.equal(a, b)
+    assert (a == torch.arange(12800)).float().mean() < 0.01
