@@ -20,6 +20,18 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=
          "-Wno-unused-result", "-fvisibility=hidden"] + os.environ.get("MAT_DCML_EXTRA_FLAGS", "").split()
 
 
+# Per-translation-unit scheduler choices, each measured on the 1-GPU bench (rocprofv3 kernel stats,
+# scripts/ab_flags2.sh): the AMDGPU register-pressure trackers cut the decoder backward's VGPR spills 76 -> 6 and
+# its time 676 -> 635 us per minibatch, but slow the decode kernel (323 -> 333 us), so only that unit uses them.
+PER_FILE_FLAGS = {
+    "mat_dec_ct_bwd.hip": ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"],
+}
+
+
+def _flags(src):
+    return FLAGS + PER_FILE_FLAGS.get(os.path.basename(src), [])
+
+
 def _sources():
     return sorted(os.path.join(HERE, f) for f in os.listdir(HERE) if f.endswith(".hip"))
 
@@ -30,7 +42,7 @@ def _hash(path):
     for p in [path] + deps:
         with open(p, "rb") as f:
             h.update(f.read())
-    h.update(" ".join(FLAGS).encode())
+    h.update(" ".join(_flags(path)).encode())
     return h.hexdigest()[:16]
 
 
@@ -38,7 +50,7 @@ def _compile(src):
     os.makedirs(os.path.join(OUT_DIR, "obj"), exist_ok=True)
     obj = os.path.join(OUT_DIR, "obj", os.path.basename(src) + "." + _hash(src) + ".o")
     if not os.path.exists(obj):
-        cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj + ".tmp"]
+        cmd = [HIPCC, *_flags(src), "-c", src, "-o", obj + ".tmp"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
