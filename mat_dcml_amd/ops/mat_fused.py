@@ -217,6 +217,12 @@ def evaluate_actions(model, obs, actions, ava=None):
     if mat_train.supported(model):
         return mat_train.evaluate_actions(model, obs, actions, ava)
     from ..models import act as act_mod
+    if mat_train.encoder_supported(model) and not model.encoder.encode_state:
+        # hybrid: fused encoder fwd/bwd kernels, eager decoder (its gates rejected the model)
+        v, rep = mat_train.encode_train(model, obs)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            logp, ent = act_mod.parallel_act(model, rep, obs, actions, ava)
+        return v, logp.float(), ent.float()
     with torch.autocast("cuda", dtype=torch.bfloat16):
         v, rep = model.encoder(None, obs)
         logp, ent = act_mod.parallel_act(model, rep, obs, actions, ava)

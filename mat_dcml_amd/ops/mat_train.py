@@ -611,6 +611,38 @@ def evaluate_actions(model, obs, actions, ava=None):
     return v, logp, ent
 
 
+class _EncFusedFn(torch.autograd.Function):
+    """(anchor, obs) -> (values, rep) through the fused encoder kernels; backward runs ``mat_enc_bwd`` with the
+    rep gradient the eager decoder hands back.  The hybrid training path for models whose decoder is outside the
+    fused gates (Available_Continuous, dec_actor, wide action heads): the encoder — the obs embedding and every
+    encoder block — stays on the HIP kernels, only the decoder runs in autograd."""
+
+    @staticmethod
+    def forward(ctx, anchor, obs, enc):
+        v, rep = enc.forward(obs, save=True)
+        ctx.enc = enc
+        return v, rep
+
+    @staticmethod
+    def backward(ctx, dv, drep):
+        enc = ctx.enc
+        v, rep = enc.ctx[2], enc.ctx[1]
+        enc.backward(drep if drep is not None else torch.zeros_like(rep),
+                     dv if dv is not None else torch.zeros_like(v))
+        enc.ctx = None
+        return torch.zeros((), device=rep.device), None, None
+
+
+def encode_train(model, obs):
+    """Fused encoder forward with autograd: (values, rep) whose backward writes the encoder's parameter gradients
+    straight into ``.grad`` (they are created zero-filled here when missing)."""
+    enc, _, anchor = _state(model, obs.device)
+    for p_ in model.encoder.parameters():
+        if p_.grad is None:
+            p_.grad = torch.zeros_like(p_)
+    return _EncFusedFn.apply(anchor, obs, enc)
+
+
 @torch.no_grad()
 def encode(model, obs):
     """Inference-only fused encoder: (values, rep)."""

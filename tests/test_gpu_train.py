@@ -250,3 +250,65 @@ def test_mujoco_runner_uses_fused_trainer(gpu):
     torch.cuda.synchronize()
     assert all(torch.isfinite(torch.as_tensor(float(v))) for v in infos.values())
     assert kernel_report(r)["train"].startswith("hip:")
+
+
+@pytest.mark.parametrize("L,B,A", [(6, 40, 4), (33, 12, 3)])
+def test_hybrid_available_continuous_grads(gpu, L, B, A):
+    """Available_Continuous (transformer_act.py:285-322) is outside the fused decoder's gates: training runs the
+    fused encoder fwd/bwd kernels under autograd with the decoder eager (ops/mat_fused.evaluate_actions).  Every
+    parameter gradient — encoder ones written by mat_enc_bwd — vs fp32 autograd of the same model."""
+    from mat_dcml_amd.ops import mat_fused, paths
+    torch.manual_seed(4)
+    od = 9
+    m = MultiAgentTransformer(L + 1, od, A, L, 2, 64, 2, action_type="Available_Continuous").to(gpu)
+    g0 = torch.Generator().manual_seed(4)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if "ln" in n or "head.2" in n or "obs_encoder.0" in n:
+                p.copy_((1.0 + 0.1 * torch.randn(p.shape, generator=g0)).to(gpu) if n.endswith("weight")
+                        else (0.1 * torch.randn(p.shape, generator=g0)).to(gpu))
+            elif n.endswith("log_std"):
+                p.copy_((0.3 * torch.randn(p.shape, generator=g0)).to(gpu))
+            else:
+                p.copy_((torch.randn(p.shape, generator=g0) * 0.2).to(gpu))
+    assert mat_train.encoder_supported(m) and not mat_train.decoder_supported(m)
+    assert paths.gate_reasons(m)["train"]
+    g = torch.Generator(device=gpu).manual_seed(9)
+    obs = torch.rand(B, L, od, device=gpu, generator=g)
+    pick = torch.randint(0, 2, (B, L), device=gpu, generator=g)
+    actions = torch.cat([torch.nn.functional.one_hot(pick, 2).float(),
+                         torch.randn(B, L, A - 2, device=gpu, generator=g) * 0.5], -1)
+    ava = torch.ones(B, L, A, device=gpu)
+    m.zero_grad()
+    lp_r, v_r, ent_r = m(None, obs, actions, ava)
+    w1, w3 = torch.randn(lp_r.shape, device=gpu, generator=g), torch.randn(ent_r.shape, device=gpu, generator=g)
+    w2 = torch.randn(v_r.shape, device=gpu, generator=g)
+    ((lp_r * w1).sum() + (v_r * w2).sum() + (ent_r * w3).sum()).backward()
+    ref = {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
+    m.zero_grad()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        lp_b, v_b, ent_b = m(None, obs, actions, ava)
+        ((lp_b.float() * w1).sum() + (v_b.float() * w2).sum() + (ent_b.float() * w3).sum()).backward()
+    refb = {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
+    m.zero_grad(set_to_none=True)
+    v_k, lp_k, ent_k = mat_fused.evaluate_actions(m, obs, actions, ava)
+    assert m._mdl_train_state[0].ctx is not None   # the fused encoder ran (its saves wait for the backward)
+    tol = lambda a, b: max(3e-2, 2.5 * rel(a.float(), b))  # noqa: E731
+    assert lp_k.shape == lp_r.shape and ent_k.shape == ent_r.shape and v_k.shape == v_r.shape
+    assert rel(lp_k, lp_r) < tol(lp_b, lp_r) and rel(v_k, v_r) < tol(v_b, v_r), (rel(lp_k, lp_r), rel(v_k, v_r))
+    ((lp_k * w1).sum() + (v_k * w2).sum() + (ent_k * w3).sum()).backward()
+    torch.cuda.synchronize()
+    assert m._mdl_train_state[0].ctx is None      # ... and its backward consumed them
+    bad = []
+    params = dict(m.named_parameters())
+    for n, r in ref.items():
+        gg = params[n].grad
+        if "key.bias" in n:
+            e = (gg - r).abs().max().item() / (ref[n.replace("key.bias", "key.weight")].abs().max().item() + 1e-6)
+            lim = 8e-2
+        else:
+            e = rel(gg, r)
+            lim = max(6e-2, 2.5 * rel(refb[n], r))
+        if e > lim:
+            bad.append((n, round(e, 4), round(rel(refb[n], r), 4)))
+    assert not bad, bad

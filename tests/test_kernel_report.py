@@ -58,3 +58,13 @@ def test_runner_report_on_cpu_names_the_reason():
     r = DCMLRunner({"all_args": args, "device": torch.device("cpu"), "run_dir": None})
     rep = kernel_report(r)
     assert rep["train"] == "torch (cpu device)" and rep["decode"].startswith("torch (")
+
+
+def test_available_continuous_takes_the_hybrid_gates():
+    """Available_Continuous: the fused encoder and decode kernels run; the fused decoder training kernels do not
+    (so ops/mat_fused.evaluate_actions trains with the fused encoder under autograd and an eager decoder)."""
+    _need_lib()
+    from mat_dcml_amd.ops.paths import gate_reasons
+    g = gate_reasons(_mat(7, 4, 9, "Available_Continuous"))
+    assert g["encoder"] == [] and g["decode"] == [], g
+    assert any("Available_Continuous" in r for r in g["train"]), g
