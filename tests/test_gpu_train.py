@@ -312,3 +312,38 @@ def test_hybrid_available_continuous_grads(gpu, L, B, A):
         if e > lim:
             bad.append((n, round(e, 4), round(rel(refb[n], r), 4)))
     assert not bad, bad
+
+
+def test_policy_available_continuous_trains_through_the_hybrid_path(gpu):
+    """TransformerPolicy with the reference's ``Available_Continous_Space`` (transformer_policy.py:36): fused decode,
+    hybrid evaluate_actions (fused encoder under autograd), Adam step, and the repacked weights change the values."""
+    from mat_dcml_amd.config import get_config, parse_args
+    from mat_dcml_amd.algos.policy import TransformerPolicy
+
+    class Available_Continous_Space:
+        def __init__(self, n):
+            self.shape = (n,)
+
+    L, B, od, A = 7, 24, 10, 4
+    args = parse_args(["--env_name", "DCML", "--n_block", "2"], get_config(), warn=False)
+    pol = TransformerPolicy(args, [od], [od], Available_Continous_Space(A), L, device=gpu)
+    assert pol._fused()
+    g = torch.Generator(device=gpu).manual_seed(5)
+    obs = torch.rand(B, L, od, device=gpu, generator=g)
+    ava = torch.ones(B, L, A, device=gpu)
+    v0, a, lp = pol.get_actions(obs, obs, ava)
+    assert a.shape == (B, L, A) and lp.shape == (B, L, A - 1)
+    pol.optimizer.zero_grad()
+    v, logp, ent = pol.evaluate_actions(obs, obs, a, ava)
+    assert pol.transformer._mdl_train_state[0].ctx is not None
+    (-(logp.sum(-1, keepdim=True) * torch.randn(B, L, 1, device=gpu, generator=g)).mean() + (v ** 2).mean()
+     - 0.01 * ent).backward()
+    enc_g = [p.grad for p in pol.transformer.encoder.parameters()]
+    assert all(x is not None and torch.isfinite(x).all() for x in enc_g)
+    assert sum(float(x.abs().sum()) for x in enc_g) > 0
+    pol.optimizer.step()
+    from mat_dcml_amd.ops import mat_fused
+    mat_fused.bump_version(pol.transformer)
+    v1 = pol.get_values(obs, obs)
+    torch.cuda.synchronize()
+    assert torch.isfinite(v1).all() and not torch.equal(v0, v1)
