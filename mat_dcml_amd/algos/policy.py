@@ -16,7 +16,7 @@ import torch
 from ..models import act as act_mod
 from ..models.mat import MultiAgentTransformer
 from ..models.variants import build_variant
-from ..ops import mat_fused
+from ..ops import kernels, mat_fused
 
 
 def action_type_of(act_space):
@@ -90,6 +90,15 @@ class TransformerPolicy:
         return (self.kernels != "torch" and self.device.type == "cuda" and self._is_mat()
                 and mat_fused.supports(self.transformer))
 
+    def _enc_fused(self):
+        """Hybrid path for MAT configs the fused decode rejects (``dec_actor`` / mat_dec, ...): the encoder still
+        runs on the fused HIP kernels (inference and, under autograd, training); only the decoder runs eager."""
+        if self.kernels == "torch" or self.device.type != "cuda" or not self._is_mat() or not kernels.available():
+            return False
+        from ..ops import mat_train
+        m = self.transformer
+        return not m.encoder.encode_state and mat_train.encoder_supported(m)
+
     def _is_mat(self):
         return isinstance(self.transformer, MultiAgentTransformer)
 
@@ -106,6 +115,11 @@ class TransformerPolicy:
             with self._autocast():
                 a, lp, v = m.get_actions(cent_obs, obs, available_actions, deterministic, stride, rand)
             return v.float(), a, lp
+        if self._enc_fused():
+            v, rep = mat_fused.get_values_rep(m, obs)
+            with torch.autocast("cuda", dtype=self.amp_dtype, enabled=self.amp_dtype is not None):
+                a, lp = act_mod.autoregressive_act(m, rep, obs, available_actions, deterministic, stride, rand)
+            return v, a, lp
         with torch.autocast("cuda", dtype=self.amp_dtype, enabled=self.amp_dtype is not None):
             v, rep = m.encoder(cent_obs, obs)
             a, lp = act_mod.autoregressive_act(m, rep, obs, available_actions, deterministic, stride, rand)
@@ -114,7 +128,7 @@ class TransformerPolicy:
     @torch.no_grad()
     def get_values(self, cent_obs, obs, available_actions=None):
         m = self.transformer
-        if self._fused():
+        if self._fused() or self._enc_fused():
             return mat_fused.get_values(m, obs)
         if not self._is_mat():
             with self._autocast():
@@ -126,7 +140,7 @@ class TransformerPolicy:
     def evaluate_actions(self, cent_obs, obs, actions, available_actions=None, active_masks=None):
         """Returns values (B,A,n_obj), log-probs (B,A,p), scalar entropy (active-masked mean)."""
         m = self.transformer
-        if self._fused():
+        if self._fused() or self._enc_fused():   # fully fused, or hybrid (fused encoder + eager decoder)
             values, logp, ent = mat_fused.evaluate_actions(m, obs, actions, available_actions)
         elif not self._is_mat():
             with self._autocast():

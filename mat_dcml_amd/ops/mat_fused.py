@@ -208,6 +208,12 @@ def get_actions(model, obs, ava=None, deterministic=False, stride=1, rand=None):
 
 
 @torch.no_grad()
+def get_values_rep(model, obs):
+    """(values, rep) from the fused encoder (eager fallback when its gates reject the model)."""
+    return _encode(model, obs)
+
+
+@torch.no_grad()
 def get_values(model, obs):
     return _encode(model, obs)[0]
 

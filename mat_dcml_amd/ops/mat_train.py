@@ -180,6 +180,8 @@ def _gptr(t):
 def decoder_linears(model):
     dec = model.decoder
     out = []
+    if dec.dec_actor:   # MAT-Dec: per-agent MLP actors, no transformer blocks to pack (hybrid path: eager decoder)
+        return out
     for blk in dec.blocks:
         a1, a2 = blk.attn1, blk.attn2
         out += [a1.query, a1.key, a1.value, a1.proj, a2.query, a2.key, a2.value, a2.proj, blk.mlp[0], blk.mlp[2]]
@@ -244,8 +246,10 @@ def _ln(ln):
 
 
 def _grad_sig(model):
-    p = next(model.parameters())
-    return p.grad.data_ptr() if p.grad is not None else 0
+    """Gradient-pointer signature the packed kernel arguments were built against: the first encoder AND decoder
+    parameter (the hybrid path creates encoder gradients separately from the decoder's autograd ones)."""
+    ps = (next(model.encoder.parameters()), next(model.decoder.parameters()))
+    return tuple(p.grad.data_ptr() if p.grad is not None else 0 for p in ps)
 
 
 # ------------------------------------------------------------------------------------------------- support

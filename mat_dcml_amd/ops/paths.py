@@ -63,8 +63,7 @@ def kernel_report(runner) -> dict:
         tr = getattr(runner, "trainer", None)
         if tr is not None and getattr(tr, "fused", False):
             out["train"] = "hip:mat_enc_fwd/bwd+mat_dec_fwd/bwd+ppo_loss+adam"
-        elif not reason and getattr(pol, "_fused", lambda: False)() and not mat_train.encoder_unsupported_reasons(m) \
-                and not m.encoder.encode_state and mat_train.decoder_unsupported_reasons(m):
+        elif not reason and getattr(pol, "_enc_fused", lambda: False)() and mat_train.decoder_unsupported_reasons(m):
             # ops/mat_fused.evaluate_actions: fused encoder kernels under autograd, eager decoder
             out["train"] = "hybrid: hip:mat_enc_fwd/bwd + torch decoder (" + \
                 "; ".join(mat_train.decoder_unsupported_reasons(m)) + ")"

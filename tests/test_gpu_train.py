@@ -347,3 +347,24 @@ def test_policy_available_continuous_trains_through_the_hybrid_path(gpu):
     v1 = pol.get_values(obs, obs)
     torch.cuda.synchronize()
     assert torch.isfinite(v1).all() and not torch.equal(v0, v1)
+
+
+def test_mat_dec_runner_trains_through_the_hybrid_path(gpu):
+    """MAT-Dec (``dec_actor``, DCML_MAT_Train.py's mat_dec): no autoregressive decode to fuse, so rollout values /
+    rep and the training encoder fwd/bwd run on the fused HIP encoder kernels and only the decoder MLPs run eager."""
+    from mat_dcml_amd.config import get_config, parse_args
+    from mat_dcml_amd.ops.paths import kernel_report
+    from mat_dcml_amd.runner.dcml_runner import DCMLRunner
+    args = parse_args(["--env_name", "DCML", "--algorithm_name", "mat_dec", "--n_workers", "8", "--n_rollout_threads",
+                       "4", "--episode_length", "4", "--ppo_epoch", "2", "--num_mini_batch", "2", "--use_valuenorm"],
+                      get_config(), warn=False)
+    args.dec_actor, args.share_actor = True, True
+    r = DCMLRunner({"all_args": args, "device": gpu, "run_dir": None})
+    assert not r.policy._fused() and r.policy._enc_fused()
+    rep = kernel_report(r)
+    assert rep["train"].startswith("hybrid: hip:mat_enc_fwd/bwd"), rep
+    r.warmup()
+    infos = r.train_iteration()
+    torch.cuda.synchronize()
+    assert all(torch.isfinite(torch.as_tensor(float(v))) for v in infos.values()), infos
+    assert r.policy.transformer._mdl_train_state[0].ctx is None   # every fused encoder forward got its backward
