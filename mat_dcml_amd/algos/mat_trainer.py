@@ -295,6 +295,8 @@ class MATTrainer:
             acc[0], acc[1], acc[2], acc[5] = o[1], o[0], o[2], o[3]
             acc[3] = acc[4] = pol.optimizer.grad_norm_sum
         acc /= self.ppo_epoch * self.num_mini_batch
+        if self.comm is not None and self.comm.world_size > 1:
+            self.comm.poll_errors()
         return dict(zip(keys, acc))
 
     def prep_training(self):

@@ -152,7 +152,10 @@ class TransformerPolicy:
                 logp, ent = act_mod.parallel_act(m, rep, obs, actions, available_actions)
             values = v.float()
         if self._use_policy_active_masks and active_masks is not None:
-            am = active_masks.expand_as(ent) if active_masks.shape != ent.shape else active_masks
+            # (N, A) entropies times (N, 1) masks (transformer_policy.py:212-213): summed over the action dims,
+            # divided by the active-token count
+            am = active_masks.reshape(ent.shape[:-1] + (1,)) if active_masks.numel() * ent.shape[-1] == ent.numel() \
+                else active_masks.expand_as(ent)
             entropy = (ent * am).sum() / am.sum()
         else:
             entropy = ent.mean()

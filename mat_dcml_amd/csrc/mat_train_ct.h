@@ -387,11 +387,7 @@ __device__ __forceinline__ void wgrad_g(const bf16_t* Y, const bf16_t* X, int KP
       for (int r = 0; r < 4; ++r) {
         const int n = 16 * rb + 4 * g + r, k = 16 * ct + c16;
         const bool ok = bj < 16 && ct < nct && n < nrows && k < ncols;
-#ifdef MDL_ABLATE_WGRAD_ATOMIC   // timing experiment only: plain stores instead of the fp32 atomics (wrong sums)
-        if (ok) dW[n * ld + k] = acc[j][r];
-#else
         if (ok) atomicAdd(dW + n * ld + k, acc[j][r]);
-#endif
       }
     }
   }
@@ -489,9 +485,6 @@ __device__ __forceinline__ void split8v(const float* x, bf16x8& hi, bf16x8& lo) 
 // forward: O (CT, the wave's query tiles rt = wave + NW k, both heads) = softmax(scale Q Kᵀ) V
 __device__ __forceinline__ void attn_fwd_ct(const bf16_t* Q, const bf16_t* K, const bf16_t* V, bool causal, float* lse_g,
                                             CT* O, const Ctx& c) {
-#ifdef MDL_ABLATE_ATTN
-  return;
-#endif
   const int lane = c.lane, g = lane >> 4, c16 = lane & 15;
 #pragma unroll
   for (int k = 0; k < MAXRT; ++k) {
@@ -556,9 +549,6 @@ __device__ __forceinline__ void st_lds_head(bf16_t* buf, int rt, int h, f32x4 a,
 // the backward kernels' code and register pressure).
 __device__ __forceinline__ void attn_bwd_q_ct(const bf16_t* Q, const bf16_t* K, const bf16_t* V, const bf16_t* DA,
                                               bf16_t* DQ, bool causal, const Ctx& c) {
-#ifdef MDL_ABLATE_ATTN
-  return;
-#endif
   const int lane = c.lane, g = lane >> 4, c16 = lane & 15;
   for (int item = c.wave; item < 2 * c.NT; item += NW) {
     const int rt = item >> 1, h = item & 1;
@@ -599,9 +589,6 @@ __device__ __forceinline__ void attn_bwd_q_ct(const bf16_t* Q, const bf16_t* K, 
 // backward, by (key tile, head) item: dV = Pᵀ dO, dK = scale dSᵀ Q, written over the item's own K / V head columns
 __device__ __forceinline__ void attn_bwd_kv_ct(const bf16_t* Q, bf16_t* K, bf16_t* V, const bf16_t* DA, bool causal,
                                                const Ctx& c) {
-#ifdef MDL_ABLATE_ATTN
-  return;
-#endif
   const int lane = c.lane, g = lane >> 4, c16 = lane & 15;
   for (int item = c.wave; item < 2 * c.NT; item += NW) {
     const int rt = item >> 1, h = item & 1;

@@ -108,9 +108,11 @@ __global__ __launch_bounds__(256) void ppo_grad_kernel(PPOArgs a) {
     // policy: -min(r A, clip(r) A)
     // multi-objective MAT (momat / dmomat): one advantage per objective, the surrogate summed over objectives
     // (mat_trainer.py:129-139 on (B, A, n_obj) advantages: min(...).sum(-1))
-    // continuous action type: one ratio per action dimension, the surrogate summed over dimensions; the entropy is
-    // the mean over every (token, dimension) entry (transformer_policy.py:212-215 with (B, L, A) entropies)
+    // continuous action type: one ratio per action dimension, the surrogate summed over dimensions.  Entropy
+    // (transformer_policy.py:212-215 on (N, A) entropies): with policy active masks Σ(ent * active) / Σ active —
+    // summed over the dimensions, per active token; without, the mean over every (token, dimension) entry.
     const float wp = a.use_pam ? act * inv_pa : inv_pa;
+    const float we = a.use_pam ? wp : wp / (float)a.n_lp;
     const float inv_lp = 1.f / (float)a.n_lp;
     for (int k = 0; k < a.n_lp; ++k) {
       const size_t q = (size_t)i * a.n_lp + k;
@@ -127,8 +129,8 @@ __global__ __launch_bounds__(256) void ppo_grad_kernel(PPOArgs a) {
       pl -= sm_ * wp;
       a.dlogp[q] = -wp * dm;
       // entropy bonus
-      a.dent[q] = -a.coef_e * wp * inv_lp;
-      el += a.ent[q] * wp * inv_lp;
+      a.dent[q] = -a.coef_e * we;
+      el += a.ent[q] * we;
       rl += imp * inv_lp;
     }
     // value

@@ -18,7 +18,8 @@
 // Two buffer halves alternate by epoch parity: a rank can only overwrite half (e & 1) at epoch e + 2 after every
 // peer signalled epoch e + 1 for the slice, i.e. after every peer's epoch-e kernel (same stream) has finished
 // reading it.  Waits are bounded: a missing peer sets the local error word and the kernel exits (never a hang);
-// the host checks the word (`mdl_ar_error`).  All cross-GPU traffic uses vector-memory loads / stores / atomics.
+// the host checks the word (`mdl_ar_error`) and the
+// workgroup writes NaN over its output slice (the optimizer's non-finite guard then skips that step).  All cross-GPU traffic uses vector-memory loads / stores / atomics.
 #include "common.h"
 #include <cstring>
 
@@ -62,6 +63,9 @@ __global__ __launch_bounds__(AR_THREADS) void oneshot_allreduce_kernel(ArArgs a)
   __threadfence_system();
   __syncthreads();
   // 2. signal every peer, then wait for every peer's signal for this slice
+  __shared__ int timed_out;
+  if (tid == 0) timed_out = 0;
+  __syncthreads();
   if (tid < a.world) {
     unsigned* f = reinterpret_cast<unsigned*>(a.region[tid] + a.flag_off) + (long long)a.rank * G + b;
     __hip_atomic_store(f, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -69,13 +73,18 @@ __global__ __launch_bounds__(AR_THREADS) void oneshot_allreduce_kernel(ArArgs a)
     const long long t0 = clock64();
     while (__hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.epoch) {
       __builtin_amdgcn_s_sleep(4);
-      if (clock64() - t0 > a.wait_cycles) {   // a peer never arrived: flag the error and leave (garbage results)
+      if (clock64() - t0 > a.wait_cycles) {   // a peer never arrived: flag the error, poison the slice
         atomicOr(reinterpret_cast<unsigned*>(a.region[a.rank] + a.err_off), 1u << (tid & 31));
+        timed_out = 1;
         break;
       }
     }
   }
   __syncthreads();
+  if (timed_out) {   // NaN output: FlatAdam's non-finite guard skips the step instead of applying a partial sum
+    for (long long i = (a.vec ? 4 * lo : lo) + tid; i < (a.vec ? 4 * hi : hi); i += AR_THREADS) a.dst[i] = __int_as_float(0x7fc00000);
+    return;
+  }
   // 3. reduce the slice over ranks in a fixed order
   if (a.vec) {
     float4* d4 = reinterpret_cast<float4*>(a.dst);
@@ -166,4 +175,11 @@ MDL_API int mdl_ar_run(void* const* regions, int world, int rank, const float* s
 // this rank's error word (synchronous read): nonzero = some peer never signalled within wait_cycles
 MDL_API int mdl_ar_error(void* region, long long n, int G, unsigned* out) {
   return (int)hipMemcpy(out, static_cast<float*>(region) + err_off_of(n, G), sizeof(unsigned), hipMemcpyDeviceToHost);
+}
+
+// the same word copied asynchronously on `st` into host-visible memory (pinned): the trainer polls it once per
+// iteration without a device synchronisation (parallel/oneshot.OneShotAllReduce.poll)
+MDL_API int mdl_ar_error_async(void* region, long long n, int G, unsigned* out_host, hipStream_t st) {
+  return (int)hipMemcpyAsync(out_host, static_cast<float*>(region) + err_off_of(n, G), sizeof(unsigned),
+                             hipMemcpyDeviceToHost, st);
 }

@@ -57,21 +57,9 @@ class DecP(ctypes.Structure):
                [("cont", ctypes.c_int), ("ba", VP), ("d_ba", VP)]
 
 
-# builds of the training kernels, by name suffix (csrc/mat_train_common.h MDL_VARIANT_SUFFIX).  Only the base build
-# (three 16-row tiles per wave, one workgroup per CU, L <= 192) ships: an occupancy-2 build (one tile per wave, two
-# workgroups per CU) measured 1.6x / 2.9x slower backward kernels (register spills, 5x more weight-gradient atomics;
-# profiles/r1_occupancy_ab.md).
-#
-# Round 2 ("ct", csrc/mat_train_ct.h): token-on-lane tiles, weight A fragments in permuted k order, register-
-# chained linears; the default.  MAT_DCML_TRAIN_KERNELS=v1 selects the round-1 row-layout kernels (A/B runs).
-TRAIN_KERNELS = os.environ.get("MAT_DCML_TRAIN_KERNELS", "ct").lower()
-VARIANTS = ("_ct",) if TRAIN_KERNELS == "ct" else ("",)
-for _v in ("",):
-    sig("mdl_mat_train_geometry" + _v, ctypes.c_int)
-    sig("mdl_mat_enc_fwd" + _v, ctypes.POINTER(EncP), ctypes.c_int, ctypes.c_int, VP)
-    sig("mdl_mat_enc_bwd" + _v, ctypes.POINTER(EncP), ctypes.c_int, VP)
-    sig("mdl_mat_dec_fwd" + _v, ctypes.POINTER(DecP), ctypes.c_int, ctypes.c_int, VP)
-    sig("mdl_mat_dec_bwd" + _v, ctypes.POINTER(DecP), ctypes.c_int, VP)
+# Training kernels (csrc/mat_train_ct.h): token-on-lane tiles, weight A fragments in permuted k order, register-
+# chained linears.  The forward kernels run 4 waves x 2 workgroups per CU, the backward 8 waves x 1 (its own
+# translation units); the tile geometry comes from mdl_mat_train_geometry_ct.
 sig("mdl_mat_train_geometry_ct", ctypes.c_int)
 sig("mdl_mat_enc_fwd_ct", ctypes.POINTER(EncP), VP, ctypes.c_int, ctypes.c_int, VP)
 sig("mdl_mat_enc_bwd_ct", ctypes.POINTER(EncP), VP, VP, ctypes.c_int, VP)
@@ -134,7 +122,7 @@ class ObsEmbed:
         check(lib().mdl_obs_embed_bwd(ctypes.byref(a), kernels._stream()), "obs_embed_bwd")
 sig("mdl_pack_weights", VP, ctypes.c_int, VP)
 
-MAX_ACTION_DIM = 64 if TRAIN_KERNELS == "ct" else 8
+MAX_ACTION_DIM = 64
 
 
 def _spread(B, L, SQ, NRP, dev):
@@ -148,24 +136,18 @@ def _spread(B, L, SQ, NRP, dev):
 
 
 def geometry(L):
-    """(SQ sequences per tile, NRP padded rows, kernel-variant suffix) — the first variant whose tiling fits L."""
-    for sfx in VARIANTS:
-        v = getattr(lib(), "mdl_mat_train_geometry" + sfx)(L)
-        if v:
-            return v & 0xFFFF, v >> 16, sfx
-    return 0, 0, ""
+    """(SQ sequences per tile, NRP padded rows, kernel suffix) of the training tiling for sequence length L
+    ((0, 0, "") when L does not fit)."""
+    v = lib().mdl_mat_train_geometry_ct(L)
+    return (v & 0xFFFF, v >> 16, "_ct") if v else (0, 0, "")
 
 
 def _enc_fwd(sfx, p, pre_in, nb, save):
-    if sfx == "_ct":
-        return lib().mdl_mat_enc_fwd_ct(ctypes.byref(p), pre_in, nb, int(save), kernels._stream())
-    return getattr(lib(), "mdl_mat_enc_fwd" + sfx)(ctypes.byref(p), nb, int(save), kernels._stream())
+    return lib().mdl_mat_enc_fwd_ct(ctypes.byref(p), pre_in, nb, int(save), kernels._stream())
 
 
 def _enc_bwd(sfx, p, pre_in, dpre_out, nb):
-    if sfx == "_ct":
-        return lib().mdl_mat_enc_bwd_ct(ctypes.byref(p), pre_in, dpre_out, nb, kernels._stream())
-    return getattr(lib(), "mdl_mat_enc_bwd" + sfx)(ctypes.byref(p), nb, kernels._stream())
+    return lib().mdl_mat_enc_bwd_ct(ctypes.byref(p), pre_in, dpre_out, nb, kernels._stream())
 
 
 def _ptr(t):
@@ -207,11 +189,10 @@ class ModelPack:
         self.n_dec = len(decoder_linears(model))
         dev = lins[0].weight.device
         self.fw = torch.empty(self.n, 4096, dtype=torch.bfloat16, device=dev)
-        self.bw = torch.empty(self.n, 4096, dtype=torch.bfloat16, device=dev)
         self.fa = torch.empty(self.n, 4096, dtype=torch.bfloat16, device=dev)
         self.ba = torch.empty(self.n, 4096, dtype=torch.bfloat16, device=dev)
         self.index = {id(l): i for i, l in enumerate(lins)}
-        tab = [[l.weight.data_ptr(), self.fw[i].data_ptr(), self.bw[i].data_ptr(), self.fa[i].data_ptr(),
+        tab = [[l.weight.data_ptr(), self.fw[i].data_ptr(), 0, self.fa[i].data_ptr(),
                 self.ba[i].data_ptr()] for i, l in enumerate(lins)]
         self.table = torch.tensor(tab, dtype=torch.int64, device=dev)
         self.version = None
@@ -224,7 +205,7 @@ class ModelPack:
 
     def mat(self, lin):
         i = self.index[id(lin)]
-        return Mat(self.fw[i].data_ptr(), self.bw[i].data_ptr(), lin.bias.data_ptr(), _gptr(lin.weight),
+        return Mat(self.fw[i].data_ptr(), None, lin.bias.data_ptr(), _gptr(lin.weight),
                    _gptr(lin.bias), self.fa[i].data_ptr(), self.ba[i].data_ptr())
 
     @property
@@ -269,8 +250,6 @@ def encoder_unsupported_reasons(model):
     r = _common_reasons(model)
     if enc.encode_state:
         r.append("encode_state")
-    if enc.obs_dim > MAX_FUSED_OBS and TRAIN_KERNELS != "ct":
-        r.append(f"obs_dim {enc.obs_dim} > {MAX_FUSED_OBS} (round-1 kernels)")
     if model.n_objective > 2:
         r.append(f"n_objective {model.n_objective} > 2")
     return r
@@ -281,7 +260,7 @@ def decoder_unsupported_reasons(model):
     r = _common_reasons(model)
     if dec.dec_actor:
         r.append("dec_actor")
-    ok_types = ("Semi_Discrete", "Discrete") + (("Continuous", "Continous") if TRAIN_KERNELS == "ct" else ())
+    ok_types = ("Semi_Discrete", "Discrete", "Continuous", "Continous")
     if model.action_type not in ok_types:
         r.append(f"action_type {model.action_type}")
     if model.action_dim > MAX_ACTION_DIM:
@@ -386,7 +365,7 @@ class EncoderFused:
             check_grad_ptrs(p, m._mdl_gws_buf[1])
         dpre = torch.empty_like(pre) if pre is not None else None
         b = m.encoder.head[3].bias
-        in_kernel = sfx == "_ct" and b.grad is not None   # the CT backward sums dv into the bias gradient itself
+        in_kernel = b.grad is not None   # the backward kernel sums dv into the bias gradient itself
         p.d_bh2 = b.grad.data_ptr() if in_kernel else None
         if in_kernel and p.g_copies:
             check_grad_ptrs(p, m._mdl_gws_buf[1])
@@ -457,9 +436,6 @@ class DecoderFused:
         model_pack(m)
         self._build()
         B, L, _ = rep.shape
-        if m.action_type != "Discrete" and geometry(L)[2] != "_ct":   # the CT kernels read log_std directly
-            with torch.no_grad():
-                self.std.copy_(m.action_std())
         dev = rep.device
         n_tok = B * L
         rep = rep.float().contiguous()
@@ -496,8 +472,8 @@ class DecoderFused:
         p = self.p
         dlogp = dlogp.reshape(-1).float().contiguous()
         dent = dent.reshape(-1).float().contiguous()
-        # the CT backward writes every row of d rep (its last decoder block overwrites); round 1 accumulates
-        drep = torch.empty_like(rep) if sfx == "_ct" else torch.zeros_like(rep)
+        # the backward writes every row of d rep (its last decoder block overwrites)
+        drep = torch.empty_like(rep)
         p.act, p.ava, p.rep = act.data_ptr(), _ptr(ava_c), rep.data_ptr()
         p.dlogp, p.dent, p.drep, p.sv_head = dlogp.data_ptr(), dent.data_ptr(), drep.data_ptr(), head
         for i, s in enumerate(svs):
@@ -517,12 +493,16 @@ class _MATFusedFn(torch.autograd.Function):
     def forward(ctx, anchor, obs, actions, ava, enc, dec):
         v, rep = enc.forward(obs, save=True)
         logp, ent = dec.forward(rep, actions, ava, save=True)
-        ctx.enc, ctx.dec = enc, dec
+        # the saved activations belong to THIS forward: another fused call before backward (a second
+        # evaluate_actions, get_values) overwrites enc.ctx / dec.ctx, so they are restored from here
+        ctx.enc, ctx.dec, ctx.saved = enc, dec, (enc.ctx, dec.ctx)
         return logp, v, ent
 
     @staticmethod
     def backward(ctx, dlogp, dv, dent):
         dec, enc = ctx.dec, ctx.enc
+        enc.ctx, dec.ctx = ctx.saved
+        ctx.saved = None
         logp, ent = dec.ctx[3], dec.ctx[4]
         drep = dec.backward(dlogp if dlogp is not None else torch.zeros_like(logp),
                             dent if dent is not None else torch.zeros_like(ent))
@@ -624,12 +604,13 @@ class _EncFusedFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, anchor, obs, enc):
         v, rep = enc.forward(obs, save=True)
-        ctx.enc = enc
+        ctx.enc, ctx.saved = enc, enc.ctx   # this forward's activations (enc.ctx is shared, see _MATFusedFn)
         return v, rep
 
     @staticmethod
     def backward(ctx, dv, drep):
         enc = ctx.enc
+        enc.ctx, ctx.saved = ctx.saved, None
         v, rep = enc.ctx[2], enc.ctx[1]
         enc.backward(drep if drep is not None else torch.zeros_like(rep),
                      dv if dv is not None else torch.zeros_like(v))

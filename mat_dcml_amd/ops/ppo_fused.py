@@ -14,6 +14,7 @@
 from __future__ import annotations
 
 import ctypes
+import warnings
 
 import torch
 
@@ -162,11 +163,27 @@ class FlatAdam:
         return {"state": state, "param_groups": [grp]}
 
     def load_state_dict(self, sd):
-        if "m" in sd:   # round-1 flat format (unpadded layout): only usable if the sizes still agree
-            if sd["m"].numel() == self.m.numel():
-                self.m.copy_(sd["m"])
-                self.v.copy_(sd["v"])
-            self.t = int(sd["t"])
+        if "m" in sd:   # round-1 flat format: the parameters concatenated WITHOUT the per-parameter padding
+            m_old, v_old = sd["m"].reshape(-1), sd["v"].reshape(-1)
+            self.m.zero_()
+            self.v.zero_()
+            if m_old.numel() == self.m.numel():
+                self.m.copy_(m_old)
+                self.v.copy_(v_old)
+                self.t = int(sd["t"])
+            elif self.layout is not None and m_old.numel() == sum(p.numel() for p, _ in self.layout):
+                o = 0   # remap the unpadded moments through the padded layout
+                for p, off in self.layout:
+                    n = p.numel()
+                    self.m[off:off + n].copy_(m_old[o:o + n].to(self.m.device))
+                    self.v[off:off + n].copy_(v_old[o:o + n].to(self.v.device))
+                    o += n
+                self.t = int(sd["t"])
+            else:   # moments unusable: restart them AND the bias-correction step count (a large t with zero
+                warnings.warn("FlatAdam: legacy optimizer state does not match the parameter layout; "   # moments
+                              "Adam moments and step count reset")                                     # = 3x steps)
+                self.t = 0
+            self.scratch[2] = 0.0
             self.param_groups[0].update({k: v for k, v in sd["param_groups"][0].items() if k != "params"})
             return
         st = sd.get("state", {})

@@ -123,6 +123,12 @@ class Comm:
         self.oneshot = ar
         return "oneshot" if chosen == "oneshot" else self.backend
 
+    def poll_errors(self):
+        """Once per training iteration, without a device sync: raise if a one-shot all-reduce peer wait timed out
+        (its NaN output already made the optimizer skip that step; see ``OneShotAllReduce.poll``)."""
+        if self.oneshot is not None:
+            self.oneshot.poll()
+
     def all_reduce_sum_async(self, t: torch.Tensor):
         """Start a SUM all-reduce of ``t``; returns a work handle (``wait()`` makes the current stream wait) or None.
         With the nccl (RCCL) backend the collective runs on the process group's own HIP stream, ordered after the

@@ -36,6 +36,7 @@ def _declare(lib):
         "mdl_ar_close": [_vp],
         "mdl_ar_run": [ctypes.POINTER(_vp), _i32, _i32, _vp, _vp, _i64, _i32, _u32, _f32, _i64, _vp],
         "mdl_ar_error": [_vp, _i64, _i32, ctypes.POINTER(_u32)],
+        "mdl_ar_error_async": [_vp, _i64, _i32, _vp, _vp],
     }.items():
         fn = getattr(lib, name)
         fn.argtypes = args
@@ -117,6 +118,24 @@ class OneShotAllReduce:
         v = _u32(0)
         kernels.check(self.lib.mdl_ar_error(self.own, self.n, self.G, ctypes.byref(v)), "mdl_ar_error")
         return int(v.value)
+
+    def poll(self):
+        """Asynchronous error check, once per training iteration: raise if the error word copied by the PREVIOUS
+        poll (on the current stream, into pinned memory) is set, then queue the next copy.  A timed-out wait also
+        wrote NaN over its output slice, so the optimizer has already skipped that step; this turns it into a
+        loud failure one iteration later without a device synchronisation."""
+        if getattr(self, "_err_host", None) is None:
+            self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            self._err_ev = None
+        if self._err_ev is not None and self._err_ev.query() and int(self._err_host[0]):
+            raise RuntimeError(f"rank {self.comm.rank}: one-shot all-reduce peer wait timed out "
+                               f"(mask {int(self._err_host[0]) & 0xffffffff:#x})")
+        if self._err_ev is None or self._err_ev.query():
+            st = torch.cuda.current_stream()
+            kernels.check(self.lib.mdl_ar_error_async(self.own, self.n, self.G, _vp(self._err_host.data_ptr()),
+                                                      _vp(st.cuda_stream)), "mdl_ar_error_async")
+            self._err_ev = torch.cuda.Event()
+            self._err_ev.record(st)
 
     def check(self):
         """Synchronous: raise if any wait inside the kernel timed out since the region was created."""

@@ -66,7 +66,7 @@ int main(int argc, char** argv) {
       }
 
   // training geometry
-  auto tr_geom = sym<int (*)(int)>(h, "mdl_mat_train_geometry");
+  auto tr_geom = sym<int (*)(int)>(h, "mdl_mat_train_geometry_ct");
   int n_fit = 0;
   for (int L = 1; L <= 320; ++L) {
     const int g = tr_geom(L);
@@ -81,10 +81,12 @@ int main(int argc, char** argv) {
   std::vector<unsigned char> zeros(1 << 14, 0);
   auto decode = sym<int (*)(const void*, int, void*)>(h, "mdl_mat_decode");
   CHECK(decode(zeros.data(), 2, nullptr) < 0, "decode accepted epw = 0");
-  auto enc_fwd = sym<int (*)(const void*, int, int, void*)>(h, "mdl_mat_enc_fwd");
-  CHECK(enc_fwd(zeros.data(), 2, 1, nullptr) < 0, "enc_fwd accepted od = 0");
-  auto enc_bwd = sym<int (*)(const void*, int, void*)>(h, "mdl_mat_enc_bwd");
-  CHECK(enc_bwd(zeros.data(), 2, nullptr) < 0, "enc_bwd accepted od = 0");
+  auto enc_fwd = sym<int (*)(const void*, const float*, int, int, void*)>(h, "mdl_mat_enc_fwd_ct");
+  CHECK(enc_fwd(zeros.data(), nullptr, 2, 1, nullptr) < 0, "enc_fwd accepted od = 0");
+  auto enc_bwd = sym<int (*)(const void*, const float*, float*, int, void*)>(h, "mdl_mat_enc_bwd_ct");
+  CHECK(enc_bwd(zeros.data(), nullptr, nullptr, 2, nullptr) < 0, "enc_bwd accepted od = 0");
+  auto dec_bwd = sym<int (*)(const void*, int, void*)>(h, "mdl_mat_dec_bwd_ct");
+  CHECK(dec_bwd(zeros.data(), 2, nullptr) < 0, "dec_bwd accepted A = 0");
 
   std::printf("host checks: %d decode geometries, %d trainable agent counts, %d failures\n", n_dec, n_fit, g_fail);
   dlclose(h);

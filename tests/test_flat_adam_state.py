@@ -43,3 +43,28 @@ def test_fused_state_loads_into_torch_adam_and_back():
         mask[off:off + p.numel()] = True
     assert torch.equal(fb.m[mask], fa.m[mask]) and torch.equal(fb.v[mask], fa.v[mask])
     assert fb.m[~mask].abs().sum() == 0         # padding stays zero
+
+
+def test_legacy_unpadded_state_is_remapped_or_reset():
+    """Round-1 flat checkpoints ('m'/'v'/'t', parameters concatenated without padding): remapped through the padded
+    layout; a state of any other size resets the moments AND t (zero moments with a large t would make the first
+    steps ~3x too large: the bias corrections would be ~1)."""
+    import pytest
+    m = _model()
+    flat = m._mdl_flat_params
+    lay = param_offsets(m)
+    n_raw = sum(p.numel() for p, _ in lay)
+    raw_m, raw_v = torch.randn(n_raw), torch.rand(n_raw)
+    fa = FlatAdam(flat, torch.zeros_like(flat), layout=lay)
+    fa.load_state_dict({"m": raw_m, "v": raw_v, "t": 11, "param_groups": [{"lr": 1e-4}]})
+    assert fa.t == 11 and fa.param_groups[0]["lr"] == 1e-4
+    o = 0
+    for p, off in lay:
+        n = p.numel()
+        assert torch.equal(fa.m[off:off + n], raw_m[o:o + n]) and torch.equal(fa.v[off:off + n], raw_v[o:o + n])
+        o += n
+    fb = FlatAdam(flat, torch.zeros_like(flat), layout=lay)
+    with pytest.warns(UserWarning):
+        fb.load_state_dict({"m": torch.randn(n_raw - 5), "v": torch.rand(n_raw - 5), "t": 11,
+                            "param_groups": [{"lr": 1e-4}]})
+    assert fb.t == 0 and fb.m.abs().sum() == 0 and fb.v.abs().sum() == 0

@@ -105,3 +105,38 @@ def test_dp_fused_trainer_with_oneshot_gradients(gpu):
     assert a[0][3] == pytest.approx(b[0][3], rel=1e-4, abs=1e-6)   # statistics path is unchanged
     assert abs(a[0][0] - b[0][0]) <= 1e-4 * max(1.0, abs(b[0][0]))
     assert abs(a[0][1] - b[0][1]) <= 1e-4 * max(1.0, abs(b[0][1]))
+
+
+def _timeout_case(comm):
+    """Rank 1 never joins the all-reduce: rank 0's bounded peer wait times out, its output is NaN (so the
+    optimizer's non-finite guard skips the step), and both the synchronous check and the per-iteration poll raise."""
+    from mat_dcml_amd.parallel.oneshot import OneShotAllReduce
+    n = 4096
+    ar = OneShotAllReduce(comm, n, wait_s=0.02)
+    dev = comm.device
+    res = (None, None, None)
+    if comm.rank == 0:
+        x = torch.ones(n, device=dev)
+        y = ar(x, out=torch.empty_like(x))
+        ar.poll()                       # queues the first asynchronous error-word copy
+        torch.cuda.synchronize(dev)
+        try:
+            ar.poll()
+            polled = False
+        except RuntimeError:
+            polled = True
+        try:
+            ar.check()
+            raised = False
+        except RuntimeError:
+            raised = True
+        res = (bool(torch.isnan(y).all()), raised, polled)
+    comm.barrier()
+    ar.close()
+    return res
+
+
+@pytest.mark.gpu
+def test_oneshot_missing_peer_poisons_output_and_raises(gpu):
+    out = spawn(_timeout_case, world=2, gpu=True)
+    assert out[0] == (True, True, True), out[0]

@@ -130,3 +130,40 @@ def test_fused_trainer_step_matches_autograd_step(gpu, n_obj):
     cos = torch.nn.functional.cosine_similarity(d_f, d_t, dim=0)
     assert cos > 0.999, float(cos)
     assert torch.allclose(d_f.norm(), d_t.norm(), rtol=1e-2)
+
+
+@pytest.mark.parametrize("pam", [True, False])
+def test_ppo_loss_continuous_multi_dim_matches_reference_formula(gpu, pam):
+    """Continuous action type with A = 3 action dimensions: (N, 3) log-probs / entropies, (N, 1) advantages and
+    active masks.  Reference formulas (mat_trainer.py:129-139, transformer_policy.py:212-215): the surrogate and,
+    under policy active masks, the entropy are SUMMED over the dimensions and divided by the active-token count;
+    without the masks both are means over the tokens (entropy: over every (token, dim) entry)."""
+    from mat_dcml_amd.ops.ppo_fused import PPOLossFused
+    g = torch.Generator(device=gpu).manual_seed(7)
+    N, A = 3000, 3
+    r = lambda *s: torch.randn(*s, device=gpu, generator=g)  # noqa: E731
+    v, lp, ent = r(N, 1), r(N, A) * 0.3 - 0.7, r(N, A).abs()
+    mb = {"old_logp": lp + 0.3 * r(N, A), "adv": r(N, 1), "value_preds": v + 0.3 * r(N, 1), "returns": 3 * r(N, 1) + 1,
+          "active": (torch.rand(N, 1, device=gpu, generator=g) > 0.2).float()}
+    tr = _args(_use_policy_active_masks=pam)
+    tr.value_normalizer = None
+    fused = PPOLossFused(tr, gpu)
+    fused.out.zero_()
+    dv, dlp, dent = fused.run(v, lp, ent, mb)
+    ll, ee = lp.clone().requires_grad_(), ent.clone().requires_grad_()
+    imp = torch.exp(ll - mb["old_logp"])
+    s1, s2 = imp * mb["adv"], imp.clamp(1 - tr.clip_param, 1 + tr.clip_param) * mb["adv"]
+    act = mb["active"]
+    if pam:
+        pl = (-torch.sum(torch.min(s1, s2) * act, dim=-1, keepdim=True)).sum() / act.sum()
+        e = (ee * act).sum() / act.sum()
+    else:
+        pl = -torch.sum(torch.min(s1, s2), dim=-1, keepdim=True).mean()
+        e = ee.mean()
+    (pl - e * tr.entropy_coef).backward()
+    torch.cuda.synchronize()
+    assert torch.allclose(dlp, ll.grad, atol=1e-8, rtol=1e-4), (dlp - ll.grad).abs().max()
+    assert torch.allclose(dent, ee.grad, atol=1e-10, rtol=1e-4), (dent[:2], ee.grad[:2])
+    o = fused.out
+    assert torch.allclose(o[0], pl.detach(), rtol=1e-4, atol=1e-5), (o[0], pl)
+    assert torch.allclose(o[2], e.detach(), rtol=1e-4, atol=1e-5), (o[2], e)
