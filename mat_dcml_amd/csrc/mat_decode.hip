@@ -61,17 +61,19 @@ struct DecParams {
                          // with one row per pass (stride 1, token inputs) the head phase writes the NEXT row's
                          // block-0 query / K / V / residual straight from this table and block 0's projection
                          // phase (one MFMA GEMM + barrier per agent step) disappears
+  uint32_t genv0;        // global id of batch row 0: the noise of row b is keyed by env genv0 + b, so the rollout of a
+                         // global env does not depend on how envs are split over ranks
 };
 
-// in-kernel sampling noise: one Philox block per (env, row, purpose); purpose 0 = the categorical uniform (x) and
+// in-kernel sampling noise: one Philox block per (global env, row, call counter, purpose); purpose 0 = the categorical uniform (x) and
 // the Normal draws of dims 0, 1 (Box-Muller of y, z); purpose 1 + k = dims 2 + 2k, 3 + 2k
 __device__ __forceinline__ float draw_u(const DecParams& p, int env, int row) {
-  const u4 r = philox4x32_10((uint32_t)env, (uint32_t)row, p.rctr, (uint32_t)P_POLICY, p.rk0, p.rk1);
+  const u4 r = philox4x32_10(p.genv0 + (uint32_t)env, (uint32_t)row, p.rctr, (uint32_t)P_POLICY, p.rk0, p.rk1);
   return u01_open_f(r.x);
 }
 __device__ __forceinline__ float draw_n(const DecParams& p, int env, int row, int a) {
   const int k = a >> 1;
-  const u4 r = philox4x32_10((uint32_t)env, (uint32_t)row, p.rctr, (uint32_t)(P_POLICY + k), p.rk0, p.rk1);
+  const u4 r = philox4x32_10(p.genv0 + (uint32_t)env, (uint32_t)row, p.rctr, (uint32_t)(P_POLICY + k), p.rk0, p.rk1);
   const uint32_t b0 = k == 0 ? r.y : r.x, b1 = k == 0 ? r.z : r.y;
   const float rad = sqrtf(-2.f * __logf(u01_open_f(b0))), th = 6.283185307179586f * u01_open_f(b1);
   return (a & 1) ? rad * __sinf(th) : rad * __cosf(th);

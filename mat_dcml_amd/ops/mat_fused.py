@@ -28,7 +28,7 @@ class DecParams(ctypes.Structure):
                                             "tok_start", "tok_zero", "stage", "cont")] + \
                [(n, ctypes.c_void_p) for n in ("wa", "ba", "lnd")] + \
                [("gen", ctypes.c_int)] + [(n, ctypes.c_uint32) for n in ("rk0", "rk1", "rctr")] + \
-               [("avail_cont", ctypes.c_int), ("qkv0", ctypes.c_void_p)]
+               [("avail_cont", ctypes.c_int), ("qkv0", ctypes.c_void_p), ("genv0", ctypes.c_uint32)]
 
 
 sig("mdl_mat_decode", ctypes.POINTER(DecParams), i32, vp)
@@ -152,6 +152,29 @@ def decoder_pack(model):
     return pack
 
 
+def set_sampling_key(model, seed: int, env0: int = 0):
+    """Key the rollout's exploration noise by (seed, GLOBAL env id, decode-call counter): row b of a decode batch draws
+    from env ``env0 + b``.  Every rank uses the same key and counter, and the runner passes its env-id offset, so a
+    1-GPU run over 2E envs and a 2-GPU run over E envs each produce identical rollouts (the reference
+    is irreproducible, DCML_MAT_Train.py:35).  The same draws feed the eager decode (``models/act.philox_rand``)."""
+    from ..utils import philox as px
+    k0, k1 = px.seed_key((int(seed) * 0x9E3779B1 + 0x51A3) & 0xFFFFFFFFFFFF)
+    model._mdl_draw_key = [k0, k1 & 0xFFFFFFFF, 0]
+    model._mdl_env0 = int(env0)
+
+
+def next_draw_key(model):
+    """(k0, k1, counter) for the next stochastic decode call; advances the counter.  Without ``set_sampling_key``
+    the key comes from torch's CPU generator on first use (torch.manual_seed reproducible)."""
+    key = getattr(model, "_mdl_draw_key", None)
+    if key is None:
+        key = [int(x) for x in torch.randint(0, 2 ** 31 - 1, (2,))] + [0]
+        model._mdl_draw_key = key
+    k0, k1, c = key
+    key[2] = (c + 1) & 0xFFFFFFFF
+    return k0, k1, c
+
+
 def decode(model, rep, ava=None, deterministic=False, stride=1, rand=None):
     """rep (B, L, 64) f32 -> actions (B, L, 1), log-probs (B, L, 1)."""
     B, L, D = rep.shape
@@ -159,17 +182,11 @@ def decode(model, rep, ava=None, deterministic=False, stride=1, rand=None):
     pk = decoder_pack(model)
     rep = rep.float().contiguous()
     dev = rep.device
-    # sampling noise: explicit draws (tests) or in-kernel Philox keyed by a per-model key taken from torch's CPU
-    # generator on first use (torch.manual_seed reproducible; per-rank after Comm.seed_sampling_rng) and a call counter
+    # sampling noise: explicit draws (tests) or in-kernel Philox keyed by (model key, global env id, call counter)
     gen = rand is None and not deterministic
     rk0 = rk1 = rctr = 0
     if gen:
-        key = getattr(model, "_mdl_draw_key", None)
-        if key is None:
-            key = [int(x) for x in torch.randint(0, 2 ** 31 - 1, (2,))] + [0]
-            model._mdl_draw_key = key
-        rk0, rk1, rctr = key
-        key[2] = (key[2] + 1) & 0xFFFFFFFF
+        rk0, rk1, rctr = next_draw_key(model)
     u = rand["u"].float().contiguous() if rand is not None else None
     n = rand["n"].float().contiguous() if rand is not None else None
     ava_c = ava.float().contiguous() if ava is not None else None
@@ -186,7 +203,7 @@ def decode(model, rep, ava=None, deterministic=False, stride=1, rand=None):
                     B, L, A, _n_disc(model, L), int(stride if deterministic else 1), int(bool(deterministic)), epw, rmax,
                     pk["n_tok"], pk["tok_start"], pk["tok_zero"], 0, cont,
                     P(pk.get("wa")).value, P(pk.get("ba")).value, P(pk.get("lnd")).value, int(gen), rk0, rk1, rctr,
-                    avail, P(pk.get("qkv0")).value)
+                    avail, P(pk.get("qkv0")).value, int(getattr(model, "_mdl_env0", 0)) & 0xFFFFFFFF)
     check(lib().mdl_mat_decode(ctypes.byref(prm), model.n_block, kernels._stream()), "mat_decode")
     return out_a, out_lp
 

@@ -81,6 +81,10 @@ class DCMLRunner:
                                         act_space, self.num_agents, device=self.device)
         self.comm.broadcast_module_(self.policy.transformer)
         self.comm.seed_sampling_rng(a.seed)
+        # exploration noise keyed by the GLOBAL env id (same key and call counter on every rank): the rollout of the
+        # global env set is the same at any rank count
+        from ..ops import mat_fused
+        mat_fused.set_sampling_key(self.policy.transformer, a.seed, env0=rank * E)
         # every .grad is a view of ONE flat fp32 buffer: one memset to zero, one all-reduce under DP, and the fused
         # backward kernels accumulate straight into it
         self.comm.attach_flat_grads(self.policy.transformer.parameters())

@@ -265,3 +265,69 @@ def test_gradient_allreduce_mode_falls_back_to_the_backend_on_cpu():
     for r in (0, 1):
         path, none, v = out[r]
         assert path == "gloo" and none and v == 1.5
+
+
+# ------------------------------------------------------------------------------------------ rank-count invariance
+def _rollout_case(comm, E, gpu_fused=False):
+    """One rollout (T steps, no update) of E envs per rank; the buffer as CPU tensors."""
+    from mat_dcml_amd.config import get_config, parse_args
+    from mat_dcml_amd.runner.dcml_runner import DCMLRunner
+    args = parse_args(["--n_workers", "32" if gpu_fused else "4", "--n_rollout_threads", str(E), "--episode_length",
+                       "6", "--env_name", "DCML", "--use_valuenorm"], get_config(), warn=False)
+    r = DCMLRunner({"all_args": args, "device": comm.device, "run_dir": None, "comm": comm})
+    r.warmup()
+    for _ in range(2):   # two rollouts: the noise counter and the env task counters advance identically
+        r.rollout()
+    b = r.buffer
+    out = {k: getattr(b, k).detach().cpu().numpy().copy() for k in ("obs", "actions", "action_log_probs", "value_preds",
+                                                                "rewards", "masks", "available_actions")}
+    out["fused"] = bool(r.policy._fused()) if hasattr(r.policy, "_fused") else False
+    return out
+
+
+def _rollout_e2(comm):
+    return _rollout_case(comm, 2)
+
+
+def _rollout_e4(comm):
+    return _rollout_case(comm, 4)
+
+
+def _assert_rank_split_equal(single, parts, exact_model_outputs=True):
+    import numpy as np
+    for k, v in single.items():
+        if k == "fused":
+            continue
+        joined = np.concatenate([parts[r][k] for r in sorted(parts)], axis=1)
+        if k in ("action_log_probs", "value_preds") and not exact_model_outputs:
+            # CPU BLAS picks its GEMM kernel by batch size: model outputs may differ in the last bit
+            assert np.allclose(joined, v, rtol=1e-6, atol=1e-6), (k, np.abs(joined - v).max())
+        else:
+            assert np.array_equal(joined, v), (k, np.abs(joined - v).max())
+
+
+def test_rollout_is_identical_at_one_and_two_ranks():
+    """the same global env set (4 envs) split over 2 ranks (gloo, CPU) or run by 1 rank produces
+    identical rollouts — env draws AND policy sampling noise are keyed by the global env id: observations, actions,
+    rewards, masks bit-identical (model outputs to the last bit of CPU BLAS)."""
+    one = spawn(_rollout_e4, world=1)[0]
+    two = spawn(_rollout_e2, world=2)
+    _assert_rank_split_equal(one, two, exact_model_outputs=False)
+
+
+def _rollout_gpu_e8(comm):
+    return _rollout_case(comm, 8, gpu_fused=True)
+
+
+def _rollout_gpu_e16(comm):
+    return _rollout_case(comm, 16, gpu_fused=True)
+
+
+@pytest.mark.gpu
+def test_rollout_is_identical_at_one_and_two_ranks_gpu(gpu):
+    """The fused HIP rollout (encoder kernel, decode kernel with in-kernel Philox noise, env kernel, fused insert)
+    at 2 ranks sharing the GPU vs 1 rank with twice the envs: bit-identical buffers."""
+    one = spawn(_rollout_gpu_e16, world=1, gpu=True)[0]
+    two = spawn(_rollout_gpu_e8, world=2, gpu=True)
+    assert one["fused"] and two[0]["fused"]
+    _assert_rank_split_equal(one, two)
