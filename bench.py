@@ -130,10 +130,12 @@ def main():
     sync()
     comm.barrier()
     sync()
+    comm.enable_timing(True)   # hipEvents around the critical-path collectives (grad average, epoch statistics)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         runner.train_iteration()
     sync()
+    t_rank = time.perf_counter() - t0      # this rank's own time, before waiting for the others
     comm.barrier()
     sync()
     dt = time.perf_counter() - t0
@@ -141,6 +143,14 @@ def main():
     comm.all_reduce_max_(t)
     dt = float(t)
     n = comm.world_size
+    comm_ms = comm.timing_ms()
+    comm.enable_timing(False)
+    per_rank = comm.all_gather_object((round(t_rank / a.steps * 1e3, 3), comm_ms))
+    diag = {"rank_ms_per_step": [r[0] for r in per_rank],
+            "comm_ms_per_step": {k: round(max(r[1].get(k, 0.0) for r in per_rank) / a.steps, 4)
+                                 for k in ("grad_allreduce", "stats_allreduce")},
+            "collectives_per_step": {k: max(r[1].get(k + "_calls", 0) for r in per_rank) // max(a.steps, 1)
+                                     for k in ("grad_allreduce", "stats_allreduce")}}
     env_steps = a.steps * a.episode_length * a.envs * n
     value = env_steps / dt
     eval_info = None
@@ -166,6 +176,9 @@ def main():
             "ranks": n, "backend": topo["backend"], "rank_devices": topo["devices"], "hosts": topo["hosts"],
             "kernels": paths, "grad_allreduce": getattr(runner.trainer, "grad_allreduce", topo["backend"]) if n > 1 else None,
             "grad_allreduce_probe": comm.oneshot_probe,
+            # scaling diagnostics: each rank's own ms per step (max = ms_per_step up to the closing barrier) and the
+            # critical-path collective time per step (hipEvents on the compute stream, max over ranks)
+            **diag,
             "eval": eval_info,
         }), flush=True)
     comm.destroy()

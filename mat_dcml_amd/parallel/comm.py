@@ -16,9 +16,11 @@ hard-coded to ``cuda:0``).  This module is the new DP layer:
 """
 from __future__ import annotations
 
+import contextlib
 import datetime
 import os
 import socket
+import time
 
 import torch
 import torch.distributed as dist
@@ -33,6 +35,39 @@ class Comm:
         self.backend = "none"
         self.oneshot = None          # OneShotAllReduce of the flat gradient (opt-in)
         self.oneshot_probe = None    # start-up check / timing of the one-shot path (mode "auto")
+        self._timing = None          # {name: [event pairs | seconds]} while enable_timing(True)
+
+    # -------------------------------------------------------------------------------- timing (bench.py)
+    def enable_timing(self, on: bool = True):
+        """Time every critical-path collective (flat-gradient average, statistics all-reduces) on the current
+        stream: hipEvents before / after, so the time includes waiting for the slowest rank."""
+        self._timing = {} if on else None
+
+    @contextlib.contextmanager
+    def _timed(self, name):
+        if self._timing is None or self.world_size == 1:
+            yield
+            return
+        if self.device.type == "cuda":
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            yield
+            b.record()
+            self._timing.setdefault(name, []).append((a, b))
+        else:
+            t0 = time.perf_counter()
+            yield
+            self._timing.setdefault(name, []).append(time.perf_counter() - t0)
+
+    def timing_ms(self, reset: bool = True) -> dict:
+        """{name: total ms, name + "_calls": count} since the last reset (synchronise the device first)."""
+        out = {}
+        for k, v in (self._timing or {}).items():
+            out[k] = round(sum(x[0].elapsed_time(x[1]) if isinstance(x, tuple) else x * 1e3 for x in v), 4)
+            out[k + "_calls"] = len(v)
+        if reset and self._timing is not None:
+            self._timing = {}
+        return out
 
     @property
     def is_main(self):
@@ -41,7 +76,8 @@ class Comm:
     # -------------------------------------------------------------------------------- collectives
     def all_reduce_sum_(self, t: torch.Tensor):
         if self.world_size > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+            with self._timed("stats_allreduce"):
+                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
         return t
 
     def all_reduce_max_(self, t: torch.Tensor):
@@ -99,10 +135,11 @@ class Comm:
         all-reduce when enabled for this buffer size (the 1/world scale is applied in-kernel), else RCCL."""
         if self.world_size == 1:
             return buf
-        if self.oneshot is not None and buf.numel() == self.oneshot.n and buf.is_cuda:
-            return self.oneshot(buf, scale=1.0 / self.world_size)
-        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
-        return buf.mul_(1.0 / self.world_size)
+        with self._timed("grad_allreduce"):
+            if self.oneshot is not None and buf.numel() == self.oneshot.n and buf.is_cuda:
+                return self.oneshot(buf, scale=1.0 / self.world_size)
+            dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
+            return buf.mul_(1.0 / self.world_size)
 
     def maybe_enable_oneshot(self, n: int, mode: str | None = None):
         """Collective: pick the flat-gradient all-reduce for n-float gradients.  ``MAT_DCML_ALLREDUCE`` (or ``mode``):

@@ -225,22 +225,40 @@ class DCMLRunner:
             if self.use_eval and episode % self.eval_interval == 0:
                 self.eval(total)
             last_infos = infos
+        self._log_flush()
         return last_infos
 
     def log(self, episode, episodes, total, start, infos):
-        stats = self._done_stats.clone()
-        self.comm.all_reduce_sum_(stats)
-        avg_step_reward = self.buffer.rewards.mean((0, 1, 2)).double()    # per objective
-        self.comm.all_reduce_mean_(avg_step_reward)
+        """Queue this log's statistics: ONE packed asynchronous all-reduce (episode sums + per-objective average step
+        reward) started here and overlapped with the next rollout; it is waited on, and the scalars are read back
+        and printed, at the next ``log`` (or at the end of ``run``), so logging never drains the GPU queue or
+        blocks a rank on the collective inside the training loop."""
+        self._log_flush()
+        packed = torch.cat([self._done_stats, self.buffer.rewards.mean((0, 1, 2)).double()])
+        self._done_stats.zero_()
+        work = self.comm.all_reduce_sum_async(packed)
+        infos = {k: (v.detach().clone() if torch.is_tensor(v) else v) for k, v in infos.items()}
+        self._pending_log = (work, packed, episode, episodes, total, time.time() - start, infos)
+
+    def _log_flush(self):
+        pend = getattr(self, "_pending_log", None)
+        if pend is None:
+            return
+        self._pending_log = None
+        work, packed, episode, episodes, total, elapsed, infos = pend
+        if work is not None:
+            work.wait()
+        stats = packed[:4]
+        avg_step_reward = packed[4:] / self.comm.world_size    # per objective
         infos = {k: float(v) for k, v in infos.items()}
         infos["average_step_rewards"] = float(avg_step_reward.sum())
         if avg_step_reward.numel() > 1:   # dcml_runner.py:306-309
             for i in range(avg_step_reward.numel()):
                 infos[f"average_step_objective_{i}"] = float(avg_step_reward[i])
-        self._done_stats.zero_()
+        self.last_log = infos
         if not self.comm.is_main:
             return
-        fps = int(total / max(time.time() - start, 1e-9))
+        fps = int(total / max(elapsed, 1e-9))
         print(f"\n Scenario {self.all_args.scenario} Algo {self.algorithm_name} Exp {self.experiment_name} "
               f"updates {episode}/{episodes} episodes, total num timesteps {total}/{self.num_env_steps}, FPS {fps}.\n")
         print(f"average_step_rewards is {infos['average_step_rewards']}.")
@@ -256,7 +274,8 @@ class DCMLRunner:
             print(self.timers.summary())
 
     def save(self, episode):
-        self.comm.barrier()
+        """Checkpoint (reference layout).  No collective when nothing is written (bench / no run dir); otherwise ONE
+        barrier after the writes, so a resume never sees rank 0's model without every rank's env counters."""
         if not self.save_dir:
             return
         if getattr(self.all_args, "save_trainer_state", True) and hasattr(self.envs, "task_ctr"):   # per-rank env counters

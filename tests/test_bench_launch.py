@@ -35,6 +35,14 @@ def test_bench_self_launches_two_ranks():
     assert out["backend"] == "gloo" and len(set(out["rank_devices"])) == 2
     assert out["config"]["global_batch"] == 8
     assert set(out["kernels"]) >= {"env", "encoder", "decode", "train", "gae"}
+    # scaling diagnostics: per-rank ms per step and critical-path collective time per step
+    assert len(out["rank_ms_per_step"]) == 2 and all(t > 0 for t in out["rank_ms_per_step"])
+    assert max(out["rank_ms_per_step"]) <= out["ms_per_step"] * 1.001
+    cm = out["comm_ms_per_step"]
+    assert cm["grad_allreduce"] > 0 and cm["stats_allreduce"] > 0
+    assert cm["grad_allreduce"] + cm["stats_allreduce"] < out["ms_per_step"]
+    # SMALL = 1 epoch x 1 minibatch: one gradient average and one epoch-statistics all-reduce per step
+    assert out["collectives_per_step"] == {"grad_allreduce": 1, "stats_allreduce": 1}
 
 
 def test_bench_rejects_world_size_mismatch():
