@@ -48,6 +48,8 @@ struct EnvState {
 struct StepOut {
   const float* actions;  // (E, A)
   float* reward; bool* done; float* delay; float* payment;  // (E)
+  double* dbg;           // optional (E, 6 + 3W) parity record: N, K, standalone, final delay, payment, reward, then
+                         // per worker the transmission count n, the consumed slots and the worker's delay
 };
 
 #define MAXW 256
@@ -274,6 +276,12 @@ __global__ __launch_bounds__(MAXW) void dcml_env_step_kernel(EnvCfg c, EnvState 
     }
     const double upload = up_unit * n + 0.02;
     delay = arrive_slot + nslots - arrive - (availability - need) + upload;
+    if (out.dbg) {
+      double* d = out.dbg + (size_t)e * (6 + 3 * W) + 6;
+      d[w] = n;
+      d[W + w] = nslots;
+      d[2 * W + w] = delay;
+    }
   }
   // K-th order statistic of the selected workers' delays (ties broken by index)
   const bool sel = valid && strat > 0.5;
@@ -322,6 +330,10 @@ __global__ __launch_bounds__(MAXW) void dcml_env_step_kernel(EnvCfg c, EnvState 
     out.done[e] = u01_open(udn.x) < c.continue_prob;
     out.delay[e] = (float)final_delay;
     out.payment[e] = (float)pay;
+    if (out.dbg) {
+      double* d = out.dbg + (size_t)e * (6 + 3 * W);
+      d[0] = N; d[1] = K; d[2] = standalone ? 1.0 : 0.0; d[3] = final_delay; d[4] = pay; d[5] = rew;
+    }
   }
   __syncthreads();
   env_reset(c, s, e);  // every step starts a new task (ENV_SingleProcess.py:139)

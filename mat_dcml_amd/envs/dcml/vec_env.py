@@ -264,6 +264,14 @@ class DeviceDCMLEnv:
         k = torch.floor(torch.log(U) / torch.log(safe))
         return torch.where(pr > 0, k, torch.zeros_like(k))
 
+    def _near_int(self, u, pr, tol=1e-6):
+        """Geometric draws whose log U / log pr lies within ``tol`` of an integer: there the floor may legitimately
+        differ between two correct implementations (libm vs device log)."""
+        U = px.u01_open(u)
+        safe = pr.clamp(min=1e-300, max=1 - 1e-12)
+        x = torch.log(U) / torch.log(safe)
+        return (pr > 0) & ((x - torch.round(x)).abs() < tol)
+
     def _step_torch(self, actions):
         cfg, E, W, P = self.cfg, self.E, self.W, self.P
         dev = self.device
@@ -290,6 +298,8 @@ class DeviceDCMLEnv:
         need = torch.ceil((9 * rr - 3) * cc) / cfg.frequency                   # SECOND_TO_CENTSEC * ceil(.)/freq
         ud = px.philox4x32(ctr.view(E, 1), self.gid.view(E, 1), wi, px.P_DOWNLOAD, self.k0, self.k1)
         n = 1 + self._geom(ud[0], pr)
+        rec = getattr(self, "record_debug", False)
+        near = self._near_int(ud[0], pr) if rec else None
         rate = self.rate                                       # Worker.process uses the download rate for both legs
         transmit = ((torch.ceil((rr + 1) * cc) * cfg.bit_to_byte) / rate + 0.001) * n
         price0 = torch.floor(transmit) * 0.1
@@ -309,6 +319,8 @@ class DeviceDCMLEnv:
             a = 1.0 - torch.gather(lw, 2, tp.unsqueeze(-1)).squeeze(-1)
             uu = px.philox4x32(ctr.view(E, 1), self.gid.view(E, 1), wi + (it << 16), px.P_UPLOAD, self.k0, self.k1)
             g = self._geom(uu[0], pr)
+            if rec:
+                near = near | (active & self._near_int(uu[0], pr))
             availability = torch.where(active, availability + a, availability)
             nslots = torch.where(active, nslots + 1, nslots)
             n = torch.where(active, n + g, n)
@@ -339,6 +351,10 @@ class DeviceDCMLEnv:
         reward = torch.where(standalone, reward * cfg.standalone_penalty, reward)
         udn = px.philox4x32(ctr, self.gid, 0, px.P_DONE, self.k0, self.k1)
         done = px.u01_open(udn[0]) < cfg.continue_prob
+        if rec:   # the kernel's parity record (csrc/dcml_env.hip StepOut.dbg) + which envs had a borderline draw
+            self.last_debug = torch.cat([torch.stack([N, K, standalone.to(f64), final, payment, reward], 1),
+                                         n, nslots, delay], 1)
+            self.last_near_int = near.any(1)
         self._reset(torch.ones(E, dtype=torch.bool, device=dev))
         return (self.obs, self.share_view(), reward.to(torch.float32), done, final.to(torch.float32),
                 payment.to(torch.float32), self.ava)

@@ -260,7 +260,7 @@ class EnvState(ctypes.Structure):
 
 
 class StepOut(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_void_p) for n in ("actions", "reward", "done", "delay", "payment")]
+    _fields_ = [(n, ctypes.c_void_p) for n in ("actions", "reward", "done", "delay", "payment", "dbg")]
 
 
 sig("mdl_dcml_env_reset", ctypes.POINTER(EnvCfg), ctypes.POINTER(EnvState), vp)
@@ -302,7 +302,12 @@ def dcml_env_step(env, actions):
     rew, done, delay, pay = env._out
     actions = actions.contiguous()
     ec, es = _env_structs(env)
-    so = StepOut(actions.data_ptr(), rew.data_ptr(), done.data_ptr(), delay.data_ptr(), pay.data_ptr())
+    dbg = None
+    if getattr(env, "record_debug", False):   # parity record (tests/test_gpu_env.py)
+        dbg = torch.zeros(env.E, 6 + 3 * env.W, dtype=torch.float64, device=env.device)
+        env.last_debug = dbg
+    so = StepOut(actions.data_ptr(), rew.data_ptr(), done.data_ptr(), delay.data_ptr(), pay.data_ptr(),
+                 dbg.data_ptr() if dbg is not None else None)
     check(lib().mdl_dcml_env_step(ctypes.byref(ec), ctypes.byref(es), ctypes.byref(so), _stream()), "dcml_env_step")
     return env.obs, env.share_view(), rew, done, delay, pay, env.ava
 
