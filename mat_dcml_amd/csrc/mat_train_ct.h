@@ -25,6 +25,8 @@
 
 // The backward kernels build in their own translation units (mat_enc_ct_bwd.hip / mat_dec_ct_bwd.hip: 8 waves per
 // workgroup); per-TU exported names (the phase-profiler readers) carry this suffix.
+#define MDL_CAT2(a, b) a##b
+#define MDL_CAT(a, b) MDL_CAT2(a, b)
 #ifdef MDL_CT_BWD_TU
 #define MDL_CT_TU_SUFFIX _bwd
 #else

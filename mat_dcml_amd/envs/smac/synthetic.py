@@ -14,11 +14,17 @@ dead agents inactive, episode limit 180, reward scaled by ``max_reward / 20`` an
 
 It reproduces shapes, masking, episode structure and the compute of the MAT/PPO stack on SMAC, NOT SC2 dynamics:
 learning-curve parity for SMAC needs a host with StarCraft II (``envs/smac/adapter.py``).
+
+Randomness: every battle reset draws from Philox keyed by (seed, battles started, global env id, unit), so the
+GPU kernel (``csrc/smac_env.hip``: the whole step + reset + observation build as ONE launch) and this torch path
+produce identical battles; ``backend="auto"`` takes the kernel on a GPU.  Distances are ``sqrt(dx*dx + dy*dy)``
+with every product / sum rounded separately on both paths.
 """
 from __future__ import annotations
 
 import torch
 
+from ...utils import philox as px
 from .maps import N_NO_ATTACK, SMACSpec, get_map
 
 MAP_SIZE, SIGHT, SHOOT = 32.0, 9.0, 6.0
@@ -29,14 +35,14 @@ DIRS = ((0.0, 1.0), (0.0, -1.0), (1.0, 0.0), (-1.0, 0.0))
 
 class SyntheticSMACEnv:
     def __init__(self, n_envs: int, map_name: str = "27m_vs_30m", device="cpu", seed: int = 1,
-                 reward_scale_rate: float = 20.0, state_per_agent: bool = True, random_agent_order: bool = False):
+                 reward_scale_rate: float = 20.0, state_per_agent: bool = True, random_agent_order: bool = False,
+                 env_id_offset: int = 0, backend: str = "auto"):
         self.spec: SMACSpec = get_map(map_name)
         s = self.spec
         self.E, self.A, self.N = int(n_envs), s.n_agents, s.n_enemies
         self.n_actions = s.n_actions
         self.device = torch.device(device)
-        self.gen = torch.Generator(device=self.device)
-        self.gen.manual_seed(int(seed))
+        self.k0, self.k1 = px.seed_key(int(seed))
         self.reward_scale = s.max_reward / reward_scale_rate
         self.state_per_agent = state_per_agent
         E, A, N, dev = self.E, self.A, self.N, self.device
@@ -48,6 +54,8 @@ class SyntheticSMACEnv:
         self.last = torch.zeros(E, A, dtype=torch.long, device=dev)
         self.battles_won = torch.zeros(E, device=dev)
         self.battles_game = torch.zeros(E, device=dev)
+        self.gid = torch.arange(E, dtype=torch.long, device=dev) + int(env_id_offset)
+        self.ep_ctr = torch.zeros(E, dtype=torch.long, device=dev)   # battles started per env (reset draw counter)
         idx = torch.arange(A, device=dev)
         self.others = torch.stack([torch.cat([idx[:i], idx[i + 1:]]) for i in range(A)]) if A > 1 else \
             torch.zeros(1, 0, dtype=torch.long, device=dev)
@@ -56,6 +64,13 @@ class SyntheticSMACEnv:
         # incoming actions are mapped back with the inverse (agent_recovery, :483-484)
         self.random_agent_order = bool(random_agent_order)
         self.perm = torch.arange(A, device=dev).expand(E, A).clone()
+        self._kern = None
+        if backend in ("auto", "hip") and self.device.type == "cuda":
+            from ...ops import kernels
+            if kernels.available() and A <= 64 and N <= 64:
+                self._kern = kernels
+            elif backend == "hip":
+                raise RuntimeError("SMAC env kernel unavailable (HIP library not loaded or > 64 units)")
 
     # ------------------------------------------------------------------------------------- spaces
     @property
@@ -75,13 +90,21 @@ class SyntheticSMACEnv:
         return [Discrete(self.n_actions)] * self.A
 
     # ------------------------------------------------------------------------------------- core
-    def _rand(self, *shape):
-        return torch.rand(*shape, device=self.device, generator=self.gen)
+    def _dist(self, dx, dy):
+        return torch.sqrt(dx * dx + dy * dy)
 
     def _reset_where(self, m):
-        E, A, N = self.E, self.A, self.N
-        ap = torch.stack([8.0 + 3.0 * self._rand(E, A), 16.0 + 6.0 * (self._rand(E, A) - 0.5)], -1)
-        ep = torch.stack([22.0 + 3.0 * self._rand(E, N), 16.0 + 6.0 * (self._rand(E, N) - 0.5)], -1)
+        """Battle reset of the envs in ``m``: Philox draws (ep_ctr, gid, unit, P_SMAC) — ally i unit i, enemy j
+        unit 64 + j; words x, y = position, z = the agent-order key (stable argsort)."""
+        E, A, N, dev = self.E, self.A, self.N, self.device
+        ctr, gid = self.ep_ctr.view(E, 1), self.gid.view(E, 1)
+        ua = px.philox4x32(ctr, gid, torch.arange(A, device=dev).view(1, A), px.P_SMAC, self.k0, self.k1)
+        ue = px.philox4x32(ctr, gid, 64 + torch.arange(N, device=dev).view(1, N), px.P_SMAC, self.k0, self.k1)
+
+        def f(u):
+            return px.u01_open(u).float()
+        ap = torch.stack([8.0 + 3.0 * f(ua[0]), 16.0 + 6.0 * (f(ua[1]) - 0.5)], -1)
+        ep = torch.stack([22.0 + 3.0 * f(ue[0]), 16.0 + 6.0 * (f(ue[1]) - 0.5)], -1)
         mm = m.view(E, 1)
         self.apos = torch.where(mm.unsqueeze(-1), ap, self.apos)
         self.epos = torch.where(mm.unsqueeze(-1), ep, self.epos)
@@ -90,8 +113,9 @@ class SyntheticSMACEnv:
         self.t = torch.where(m, torch.zeros_like(self.t), self.t)
         self.last = torch.where(mm, torch.zeros_like(self.last), self.last)
         if self.random_agent_order:
-            p = torch.argsort(self._rand(E, A), dim=1)
+            p = torch.sort(ua[2], dim=1, stable=True).indices
             self.perm = torch.where(mm, p, self.perm)
+        self.ep_ctr = torch.where(m, self.ep_ctr + 1, self.ep_ctr)
 
     def _rows(self, x, perm):
         if not self.random_agent_order:
@@ -103,6 +127,8 @@ class SyntheticSMACEnv:
         return tuple(self._rows(x, self.perm) for x in self._observe())
 
     def reset(self):
+        if self._kern is not None:
+            return self._kern.smac_env(self, None)[:3]
         self._reset_where(torch.ones(self.E, dtype=torch.bool, device=self.device))
         return self._observe_perm()
 
@@ -110,6 +136,9 @@ class SyntheticSMACEnv:
         """actions (E, A[, 1]) ints.  Returns obs, state, reward (E, A, 1), dones (E, A), info dict of (E,)
         tensors, available actions."""
         E, A, N = self.E, self.A, self.N
+        if self._kern is not None:   # csrc/smac_env.hip: step + battle reset + observation build in one launch
+            obs, state, ava, reward, dones, info = self._kern.smac_env(self, actions)
+            return obs, state, reward.view(E, 1, 1).expand(E, A, 1), dones, info, ava
         a = actions.reshape(E, A).long()
         if self.random_agent_order:   # row j of the policy output belongs to agent perm[j]
             a = torch.empty_like(a).scatter_(1, self.perm, a)
@@ -122,7 +151,8 @@ class SyntheticSMACEnv:
         step = dirs[(a - 2).clamp(0, 3)] * MOVE * mv.unsqueeze(-1)
         self.apos = (self.apos + step).clamp(0.0, MAP_SIZE)
         # ally attacks
-        d_ae = (self.apos[:, :, None] - self.epos[:, None]).norm(dim=-1)           # (E, A, N) (no GEMM path)
+        rel = self.epos[:, None] - self.apos[:, :, None]
+        d_ae = self._dist(rel[..., 0], rel[..., 1])                                  # (E, A, N)
         tgt = (a - N_NO_ATTACK).clamp(0, N - 1)
         att = (a >= N_NO_ATTACK) & alive
         in_rng = torch.gather(d_ae, 2, tgt.unsqueeze(-1)).squeeze(-1) <= SHOOT
@@ -141,7 +171,7 @@ class SyntheticSMACEnv:
         walk = e_alive & (dist > SHOOT) & torch.isfinite(dist)
         tp = torch.gather(self.apos, 1, near.unsqueeze(-1).expand(E, N, 2))
         vec = tp - self.epos
-        vec = vec / vec.norm(dim=-1, keepdim=True).clamp(min=1e-6)
+        vec = vec / self._dist(vec[..., 0], vec[..., 1]).unsqueeze(-1).clamp(min=1e-6)
         self.epos = self.epos + vec * ENEMY_MOVE * walk.unsqueeze(-1)
         admg = torch.zeros(E, A, device=self.device).scatter_add_(1, near, shoot.float() * ENEMY_DMG)
         self.ahp = (self.ahp - admg).clamp(min=0.0)
@@ -178,7 +208,7 @@ class SyntheticSMACEnv:
         move = (((nxt >= 0) & (nxt <= MAP_SIZE)).all(-1).float()) * alive.unsqueeze(-1)
         # enemies
         rel_e = self.epos.unsqueeze(1) - self.apos.unsqueeze(2)                      # (E, A, N, 2)
-        d_e = rel_e.norm(dim=-1)
+        d_e = self._dist(rel_e[..., 0], rel_e[..., 1])
         vis_e = (d_e <= SIGHT).float() * e_alive.unsqueeze(1) * alive.unsqueeze(-1)
         attackable = (d_e <= SHOOT).float() * vis_e
         ef = torch.stack([attackable, d_e / SIGHT, rel_e[..., 0] / SIGHT, rel_e[..., 1] / SIGHT,
@@ -188,7 +218,7 @@ class SyntheticSMACEnv:
         # allies (others)
         oth = self.others
         rel_a = self.apos[:, oth] - self.apos.unsqueeze(2)                           # (E, A, A-1, 2)
-        d_a = rel_a.norm(dim=-1)
+        d_a = self._dist(rel_a[..., 0], rel_a[..., 1])
         vis_a = (d_a <= SIGHT).float() * alive[:, oth] * alive.unsqueeze(-1)
         af = torch.cat([torch.stack([vis_a, d_a / SIGHT, rel_a[..., 0] / SIGHT, rel_a[..., 1] / SIGHT,
                                      self.ahp[:, oth]], -1), tb_a[:, oth], last1h[:, oth]], -1) * vis_a.unsqueeze(-1)

@@ -332,3 +332,63 @@ def planar_step(consts, scal, act, p, th, v, w, q, qd, tau, f_end, f_root):
     assert consts.is_contiguous() and consts.dtype == torch.float32
     check(lib().mdl_planar_step(ctypes.byref(c), P(consts), consts.numel(), P(act), P(p), P(th), P(v), P(w), P(q),
                                 P(qd), P(tau), P(f_end), P(f_root), _stream()), "planar_step")
+
+
+# ----------------------------------------------------------------------------------------- SMAC-shaped env
+class SmacCfg(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("E", "A", "N", "nA", "u", "limit", "obs_dim", "state_dim", "rao",
+                                            "mode")] + \
+               [("k0", ctypes.c_uint32), ("k1", ctypes.c_uint32), ("reward_scale", ctypes.c_float)]
+
+
+class SmacState(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("gid", "ep_ctr", "apos", "ahp", "epos", "ehp", "t", "last",
+                                               "battles_won", "battles_game", "perm")]
+
+
+class SmacOut(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("actions", "obs", "state", "ava", "reward", "dones", "won", "lost",
+                                               "timeout", "dead_allies", "dead_enemies", "battles_won_out",
+                                               "battles_game_out")]
+
+
+sig("mdl_smac_env", ctypes.POINTER(SmacCfg), ctypes.POINTER(SmacState), ctypes.POINTER(SmacOut), vp)
+
+
+def smac_env(env, actions):
+    """One launch of csrc/smac_env.hip: the step (``actions`` (E, A) policy rows) or, with ``actions=None``, the
+    reset of every env; returns (obs, state, ava, reward (E,), dones (E, A) bool, info)."""
+    E, A, N, sp = env.E, env.A, env.N, env.spec
+    dev = env.device
+    for name in ("apos", "ahp", "epos", "ehp"):
+        t = getattr(env, name)
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            setattr(env, name, t.float().contiguous())
+    for name in ("t", "last", "perm", "ep_ctr", "gid"):
+        t = getattr(env, name)
+        if t.dtype != torch.int64 or not t.is_contiguous():
+            setattr(env, name, t.long().contiguous())
+    c = SmacCfg(E=E, A=A, N=N, nA=env.n_actions, u=sp.unit_type_bits, limit=sp.limit, obs_dim=sp.obs_dim,
+                state_dim=sp.state_dim, rao=int(env.random_agent_order), mode=0 if actions is not None else 1,
+                k0=env.k0, k1=env.k1, reward_scale=env.reward_scale)
+    s = SmacState(*[getattr(env, n).data_ptr() for n in ("gid", "ep_ctr", "apos", "ahp", "epos", "ehp", "t", "last",
+                                                        "battles_won", "battles_game", "perm")])
+    f32 = dict(device=dev, dtype=torch.float32)
+    obs = torch.empty(E, A, sp.obs_dim, **f32)
+    state = torch.empty(E, A, sp.state_dim, **f32)
+    ava = torch.empty(E, A, env.n_actions, **f32)
+    reward = torch.empty(E, **f32)
+    dones = torch.empty(E, A, dtype=torch.bool, device=dev)
+    flags = torch.empty(3, E, dtype=torch.bool, device=dev)
+    scal = torch.empty(4, E, **f32)
+    act = None
+    if actions is not None:
+        act = actions.reshape(E, A)
+        act = act if (act.dtype == torch.float32 and act.is_contiguous()) else act.float().contiguous()
+    o = SmacOut(act.data_ptr() if act is not None else None, obs.data_ptr(), state.data_ptr(), ava.data_ptr(),
+                reward.data_ptr(), dones.data_ptr(), flags[0].data_ptr(), flags[1].data_ptr(), flags[2].data_ptr(),
+                scal[0].data_ptr(), scal[1].data_ptr(), scal[2].data_ptr(), scal[3].data_ptr())
+    check(lib().mdl_smac_env(ctypes.byref(c), ctypes.byref(s), ctypes.byref(o), _stream()), "smac_env")
+    info = {"won": flags[0], "lost": flags[1], "bad_transition": flags[2], "battles_won": scal[2],
+            "battles_game": scal[3], "dead_allies": scal[0], "dead_enemies": scal[1]}
+    return obs, state, ava, reward, dones, info

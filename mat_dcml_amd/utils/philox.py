@@ -31,6 +31,7 @@ P_UPLOAD = 7        # per-worker upload retries, sub = slot iteration
 P_DONE = 8          # per-env done draw
 P_SHANNON = 9       # Shannon link draws (distance, worker power; sub 0xFFFF = master power)
 P_POLICY = 16       # policy sampling streams (decode kernel)
+P_SMAC = 32         # SMAC-shaped env battle resets (csrc/smac_env.hip)
 
 
 def _mulhilo(a: int, b: torch.Tensor):
