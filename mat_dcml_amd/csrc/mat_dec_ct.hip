@@ -161,7 +161,7 @@ __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, C
       flush_vec(dlg, c.g(ln.dg), lane);
       flush_vec(dlb, c.g(ln.db), lane);
     }
-    {   // pass 2 (Wpᵀ): dO = Wpᵀ ds -> DA
+    {   // pass 2 (Wpᵀ): dO = Wpᵀ ds -> DA; delta = rowsum(dO O) -> DEL (O = X of Wp, in XB)
       AFr Wpb;
       loadA(Wpb, m[7].ba, lane);
 #pragma unroll
@@ -171,7 +171,9 @@ __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, C
           CT da;
           ct_zero(da);
           mm(da, Wpb, ld_lds(c.DQ, rt, lane));
-          st_lds(c.DA, rt, ct_pack(da), tok_ok(rt, c), lane);
+          const bool ok = tok_ok(rt, c);
+          st_lds(c.DA, rt, ct_pack(da), ok, lane);
+          attn_delta_ct(ld_lds(c.XB, rt, lane), da, rt, ok, c);
         }
       }
     }

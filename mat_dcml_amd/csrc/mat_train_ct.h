@@ -546,9 +546,26 @@ __device__ __forceinline__ void st_lds_head(bf16_t* buf, int rt, int h, f32x4 a,
   *(uint2*)(buf + tmo(row, 32 * h + 16 + 4 * g)) = ub;
 }
 
-// backward, by (query tile, head) item: delta_q = Σ_k P dP (-> DEL), dQ = scale Σ_k dS K (-> DQ, token-major);
-// LSE in log2 units.  Items are dealt round robin (a runtime loop: the per-wave tile loop of the forward blew up
-// the backward kernels' code and register pressure).
+// delta_q = Σ_k P_qk dP_qk = Σ_d dO_qd O_qd per (query, head) (dP = dO Vᵀ, O = P V): from the saved forward output
+// O and dO in registers (CT layout, both heads) -> DEL [head][row] in LDS.  Replaces a full extra sweep over the keys
+// (scores, exp2 and dP MFMAs) in the query pass.
+__device__ __forceinline__ void attn_delta_ct(const CTr& o, const CT& dO, int rt, bool ok, const Ctx& c) {
+  const CT ov = ct_unpack(o);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float d = 0.f;
+#pragma unroll
+    for (int mt = 2 * h; mt < 2 * h + 2; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) d += ov.v[mt][r] * dO.v[mt][r];
+    d = cross_row_sum(d);
+    if ((c.lane >> 4) == 0) c.DEL[h * c.NRP + rt * 16 + (c.lane & 15)] = ok ? d : 0.f;
+  }
+}
+
+// backward, by (query tile, head) item: dQ = scale Σ_k dS K (-> DQ, token-major), dS = P (dP - delta) with delta from
+// DEL (attn_delta_ct); LSE in log2 units.  Items are dealt round robin (a runtime loop: the per-wave tile loop of the
+// forward blew up the backward kernels' code and register pressure).
 __device__ __forceinline__ void attn_bwd_q_ct(const bf16_t* Q, const bf16_t* K, const bf16_t* V, const bf16_t* DA,
                                               bf16_t* DQ, bool causal, const Ctx& c) {
   const int lane = c.lane, g = lane >> 4, c16 = lane & 15;
@@ -559,15 +576,7 @@ __device__ __forceinline__ void attn_bwd_q_ct(const bf16_t* Q, const bf16_t* K, 
     const SeqSpan sp = tile_span(rt, c, causal);
     const bf16x8 qB = lda_tm(Q, q, 4 * h + g), dB = lda_tm(DA, q, 4 * h + g);
     const float lse = c.LSE[h * c.NRP + q];
-    float delta = 0.f;
-    for (int kb = sp.lo; kb < sp.hi; kb += 32) {
-      float sc[8], dp[8];
-      chunk_scores(K, kb, h, qB, qs, sc, lane);
-      score_chunk_T(V, kb, h, dB, dp, lane);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) delta += exp2f(sc[j] - lse) * dp[j];
-    }
-    delta = cross_row_sum(delta);
+    const float delta = c.DEL[h * c.NRP + q];
     f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
     for (int kb = sp.lo; kb < sp.hi; kb += 32) {
       float sc[8], dp[8];
@@ -584,7 +593,6 @@ __device__ __forceinline__ void attn_bwd_q_ct(const bf16_t* Q, const bf16_t* K, 
       d1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, dsl, d1, 0, 0, 0);
     }
     st_lds_head(DQ, rt, h, d0 * ATT_SCALE, d1 * ATT_SCALE, q < c.NR, lane);
-    if (g == 0) c.DEL[h * c.NRP + q] = q < c.NR ? delta : 0.f;
   }
 }
 
@@ -827,7 +835,7 @@ __device__ __forceinline__ void self_attn_bwd_ct(const Mat* m, const LNp& ln, CT
       flush_vec(dlg, c.g(ln.dg), lane);
       flush_vec(dlb, c.g(ln.db), lane);
     }
-    {   // pass 2 (Wpᵀ): dO = Wpᵀ ds -> DA
+    {   // pass 2 (Wpᵀ): dO = Wpᵀ ds -> DA; delta = rowsum(dO O) -> DEL (O = X of Wp, in XB)
       AFr Wpb;
       loadA(Wpb, m[3].ba, lane);
 #pragma unroll
@@ -837,7 +845,9 @@ __device__ __forceinline__ void self_attn_bwd_ct(const Mat* m, const LNp& ln, CT
           CT da;
           ct_zero(da);
           mm(da, Wpb, ld_lds(c.DQ, rt, lane));
-          st_lds(c.DA, rt, ct_pack(da), tok_ok(rt, c), lane);
+          const bool ok = tok_ok(rt, c);
+          st_lds(c.DA, rt, ct_pack(da), ok, lane);
+          attn_delta_ct(ld_lds(c.XB, rt, lane), da, rt, ok, c);
         }
       }
     }

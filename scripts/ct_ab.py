@@ -31,8 +31,10 @@ def main(B=3200, L=33, reps=20):
     obs = torch.rand(B, L, 7, device=dev)
     ava = torch.ones(B, L, 2, device=dev)
     actions = (torch.rand(B, L, 1, device=dev) < 0.5).float()
-    for p in m.parameters():
-        p.grad = torch.zeros_like(p)
+    from mat_dcml_amd.parallel.comm import FlatGrads
+    fg = FlatGrads(list(m.parameters()))   # the trainer's layout: .grad views of one flat buffer + 8-copy workspace
+    mat_train.attach_grad_workspace(m, fg.buf)
+    m._mdl_gws_active = True
     enc, dec = mat_train.EncoderFused(m), mat_train.DecoderFused(m)
     st = {}
     v, rep = enc.forward(obs)
@@ -44,6 +46,7 @@ def main(B=3200, L=33, reps=20):
     st["dec_fwd"] = timed(lambda: dec.forward(rep, actions, ava), reps)
     st["dec_bwd"] = timed(lambda: dec.backward(torch.ones_like(lp), torch.ones_like(ent)), reps)
     st["enc_bwd"] = timed(lambda: enc.backward(drep, torch.ones_like(v)), reps)
+    st["grad_reduce"] = timed(lambda: mat_train.reduce_grad_workspace(m), reps)
     st["total"] = sum(st.values())
     print(os.environ.get("MAT_DCML_LIBNAME", "libmatdcml.so"), " ".join(f"{k} {v:.1f}us" for k, v in st.items()))
 
