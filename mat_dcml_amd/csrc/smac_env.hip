@@ -22,12 +22,13 @@ namespace {
 constexpr int SM_MAXU = 64;          // allies and enemies per env (largest registered map: 2c_vs_64zg, 64 enemies)
 constexpr int SM_THREADS = 1024;
 constexpr uint32_t P_SMAC = 32;      // Philox purpose of the battle reset draws (utils/philox.py P_SMAC)
+constexpr float INV_SIGHT = (float)(1.0 / 9.0);   // x / SIGHT as torch computes it: x * fl(1/9)
 constexpr float MAP = 32.f, SIGHT = 9.f, SHOOT = 6.f, MOVE = 1.f, EMOVE = 0.6f, ADMG = 0.15f, EDMG = 0.06f;
 
 struct SmacCfg {
   int E, A, N, nA, u, limit, obs_dim, state_dim, rao, mode;   // mode 0: step, 1: reset every env
   uint32_t k0, k1;
-  float reward_scale;
+  float inv_reward_scale;   // fl(1 / reward_scale): reward = rw * it, as the torch path
 };
 
 struct SmacState {
@@ -167,7 +168,7 @@ __global__ __launch_bounds__(SM_THREADS) void smac_env_kernel(SmacCfg c, SmacSta
       const bool tout = t >= c.limit && !won && !lost;
       const bool done = won || lost || tout;
       const float rw = __fadd_rn(__fadd_rn(sum_dealt, __fmul_rn(10.f, (float)kills)), won ? 200.f : 0.f);
-      o.reward[e] = __fdiv_rn(rw, c.reward_scale);
+      o.reward[e] = __fmul_rn(rw, c.inv_reward_scale);
       o.won[e] = won;
       o.lost[e] = lost;
       o.timeout[e] = tout;
@@ -244,8 +245,8 @@ __global__ __launch_bounds__(SM_THREADS) void smac_env_kernel(SmacCfg c, SmacSta
       float dx, dy;
       const float d = dist2(ax[i], ay[i], ex[k], ey[k], dx, dy);
       const float vis = (d <= SIGHT ? 1.f : 0.f) * (eh[k] > 0.f ? 1.f : 0.f) * al;
-      const float fv = q == 0 ? (d <= SHOOT ? 1.f : 0.f) * vis : q == 1 ? __fdiv_rn(d, SIGHT)
-                     : q == 2 ? __fdiv_rn(dx, SIGHT) : q == 3 ? __fdiv_rn(dy, SIGHT) : q == 4 ? eh[k] : 0.f;
+      const float fv = q == 0 ? (d <= SHOOT ? 1.f : 0.f) * vis : q == 1 ? __fmul_rn(d, INV_SIGHT)
+                     : q == 2 ? __fmul_rn(dx, INV_SIGHT) : q == 3 ? __fmul_rn(dy, INV_SIGHT) : q == 4 ? eh[k] : 0.f;
       v = fv * vis;
     } else if (f < o_o) {
       const int qa = (f - o_a) / AF, q = f - o_a - qa * AF;
@@ -255,9 +256,9 @@ __global__ __launch_bounds__(SM_THREADS) void smac_env_kernel(SmacCfg c, SmacSta
       const float vis = (d <= SIGHT ? 1.f : 0.f) * (ah[oa] > 0.f ? 1.f : 0.f) * al;
       float fv;
       if (q == 0) fv = vis;
-      else if (q == 1) fv = __fdiv_rn(d, SIGHT);
-      else if (q == 2) fv = __fdiv_rn(dx, SIGHT);
-      else if (q == 3) fv = __fdiv_rn(dy, SIGHT);
+      else if (q == 1) fv = __fmul_rn(d, INV_SIGHT);
+      else if (q == 2) fv = __fmul_rn(dx, INV_SIGHT);
+      else if (q == 3) fv = __fmul_rn(dy, INV_SIGHT);
       else if (q == 4) fv = ah[oa];
       else if (q < 5 + u) fv = q == 5 ? 1.f : 0.f;
       else fv = (q - 5 - u) == lst[oa] ? 1.f : 0.f;
@@ -296,8 +297,8 @@ __global__ __launch_bounds__(SM_THREADS) void smac_env_kernel(SmacCfg c, SmacSta
       const float d = dist2(ax[i], ay[i], ex[k], ey[k], dx, dy);
       const float ea = eh[k] > 0.f ? 1.f : 0.f;
       const float vis = (d <= SIGHT ? 1.f : 0.f) * ea * al;
-      v = q == 0 ? (d <= SHOOT ? 1.f : 0.f) * vis : q == 1 ? __fdiv_rn(d, SIGHT) : q == 2 ? __fdiv_rn(dx, SIGHT)
-        : q == 3 ? __fdiv_rn(dy, SIGHT) : q == 4 ? eh[k] : q == 5 ? __fdiv_rn(ex[k], MAP)
+      v = q == 0 ? (d <= SHOOT ? 1.f : 0.f) * vis : q == 1 ? __fmul_rn(d, INV_SIGHT) : q == 2 ? __fmul_rn(dx, INV_SIGHT)
+        : q == 3 ? __fmul_rn(dy, INV_SIGHT) : q == 4 ? eh[k] : q == 5 ? __fdiv_rn(ex[k], MAP)
         : q == 6 ? __fdiv_rn(ey[k], MAP) : q == 7 ? ea : 0.f;
     } else if (f < s_o) {
       const int qa = (f - s_a) / SA, q = f - s_a - qa * SA;
@@ -306,9 +307,9 @@ __global__ __launch_bounds__(SM_THREADS) void smac_env_kernel(SmacCfg c, SmacSta
       const float d = dist2(ax[i], ay[i], ax[oa], ay[oa], dx, dy);
       const float aa = ah[oa] > 0.f ? 1.f : 0.f;
       if (q == 0) v = (d <= SIGHT ? 1.f : 0.f) * aa * al;
-      else if (q == 1) v = __fdiv_rn(d, SIGHT);
-      else if (q == 2) v = __fdiv_rn(dx, SIGHT);
-      else if (q == 3) v = __fdiv_rn(dy, SIGHT);
+      else if (q == 1) v = __fmul_rn(d, INV_SIGHT);
+      else if (q == 2) v = __fmul_rn(dx, INV_SIGHT);
+      else if (q == 3) v = __fmul_rn(dy, INV_SIGHT);
       else if (q == 4) v = ah[oa];
       else if (q == 5) v = __fdiv_rn(ax[oa], MAP);
       else if (q == 6) v = __fdiv_rn(ay[oa], MAP);

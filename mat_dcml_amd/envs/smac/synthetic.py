@@ -28,6 +28,7 @@ from ...utils import philox as px
 from .maps import N_NO_ATTACK, SMACSpec, get_map
 
 MAP_SIZE, SIGHT, SHOOT = 32.0, 9.0, 6.0
+INV_SIGHT = 1.0 / SIGHT   # multiply by the reciprocal: torch's own tensor / scalar does, the kernel matches it
 MOVE, ENEMY_MOVE = 1.0, 0.6
 ALLY_DMG, ENEMY_DMG = 0.15, 0.06
 DIRS = ((0.0, 1.0), (0.0, -1.0), (1.0, 0.0), (-1.0, 0.0))
@@ -181,7 +182,7 @@ class SyntheticSMACEnv:
         lost = (self.ahp <= 0).all(1) & ~won
         timeout = (self.t >= self.spec.limit) & ~won & ~lost
         done = won | lost | timeout
-        reward = (dealt + 10.0 * kills + 200.0 * won.float()) / self.reward_scale
+        reward = (dealt + 10.0 * kills + 200.0 * won.float()) * (1.0 / self.reward_scale)
         self.battles_game += done.float()
         self.battles_won += won.float()
         dones = (self.ahp <= 0) | done.view(E, 1)
@@ -211,7 +212,7 @@ class SyntheticSMACEnv:
         d_e = self._dist(rel_e[..., 0], rel_e[..., 1])
         vis_e = (d_e <= SIGHT).float() * e_alive.unsqueeze(1) * alive.unsqueeze(-1)
         attackable = (d_e <= SHOOT).float() * vis_e
-        ef = torch.stack([attackable, d_e / SIGHT, rel_e[..., 0] / SIGHT, rel_e[..., 1] / SIGHT,
+        ef = torch.stack([attackable, d_e * INV_SIGHT, rel_e[..., 0] * INV_SIGHT, rel_e[..., 1] * INV_SIGHT,
                           self.ehp.unsqueeze(1).expand(E, A, N)], -1) * vis_e.unsqueeze(-1)
         if u:
             ef = torch.cat([ef, torch.zeros(E, A, N, u, device=dev)], -1)
@@ -220,7 +221,7 @@ class SyntheticSMACEnv:
         rel_a = self.apos[:, oth] - self.apos.unsqueeze(2)                           # (E, A, A-1, 2)
         d_a = self._dist(rel_a[..., 0], rel_a[..., 1])
         vis_a = (d_a <= SIGHT).float() * alive[:, oth] * alive.unsqueeze(-1)
-        af = torch.cat([torch.stack([vis_a, d_a / SIGHT, rel_a[..., 0] / SIGHT, rel_a[..., 1] / SIGHT,
+        af = torch.cat([torch.stack([vis_a, d_a * INV_SIGHT, rel_a[..., 0] * INV_SIGHT, rel_a[..., 1] * INV_SIGHT,
                                      self.ahp[:, oth]], -1), tb_a[:, oth], last1h[:, oth]], -1) * vis_a.unsqueeze(-1)
         own = torch.cat([torch.stack([self.ahp, self.apos[..., 0] / MAP_SIZE, self.apos[..., 1] / MAP_SIZE,
                                       torch.zeros_like(self.ahp), alive], -1), tb_a, last1h], -1)
@@ -228,13 +229,13 @@ class SyntheticSMACEnv:
         ids = self.agent_id.expand(E, A, A)
         obs = torch.cat([move, ef.reshape(E, A, -1), af.reshape(E, A, -1), own, ids], -1)
         # per-agent state: absolute positions added to every entity
-        esf = torch.cat([torch.stack([attackable, d_e / SIGHT, rel_e[..., 0] / SIGHT, rel_e[..., 1] / SIGHT,
+        esf = torch.cat([torch.stack([attackable, d_e * INV_SIGHT, rel_e[..., 0] * INV_SIGHT, rel_e[..., 1] * INV_SIGHT,
                                       self.ehp.unsqueeze(1).expand(E, A, N),
                                       self.epos[..., 0].unsqueeze(1).expand(E, A, N) / MAP_SIZE,
                                       self.epos[..., 1].unsqueeze(1).expand(E, A, N) / MAP_SIZE,
                                       e_alive.unsqueeze(1).expand(E, A, N)], -1),
                          torch.zeros(E, A, N, u, device=dev)], -1)
-        asf = torch.cat([torch.stack([vis_a, d_a / SIGHT, rel_a[..., 0] / SIGHT, rel_a[..., 1] / SIGHT,
+        asf = torch.cat([torch.stack([vis_a, d_a * INV_SIGHT, rel_a[..., 0] * INV_SIGHT, rel_a[..., 1] * INV_SIGHT,
                                       self.ahp[:, oth], self.apos[:, oth][..., 0] / MAP_SIZE,
                                       self.apos[:, oth][..., 1] / MAP_SIZE, alive[:, oth]], -1),
                          tb_a[:, oth], last1h[:, oth]], -1)

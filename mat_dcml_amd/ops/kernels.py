@@ -338,7 +338,7 @@ def planar_step(consts, scal, act, p, th, v, w, q, qd, tau, f_end, f_root):
 class SmacCfg(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in ("E", "A", "N", "nA", "u", "limit", "obs_dim", "state_dim", "rao",
                                             "mode")] + \
-               [("k0", ctypes.c_uint32), ("k1", ctypes.c_uint32), ("reward_scale", ctypes.c_float)]
+               [("k0", ctypes.c_uint32), ("k1", ctypes.c_uint32), ("inv_reward_scale", ctypes.c_float)]
 
 
 class SmacState(ctypes.Structure):
@@ -370,7 +370,7 @@ def smac_env(env, actions):
             setattr(env, name, t.long().contiguous())
     c = SmacCfg(E=E, A=A, N=N, nA=env.n_actions, u=sp.unit_type_bits, limit=sp.limit, obs_dim=sp.obs_dim,
                 state_dim=sp.state_dim, rao=int(env.random_agent_order), mode=0 if actions is not None else 1,
-                k0=env.k0, k1=env.k1, reward_scale=env.reward_scale)
+                k0=env.k0, k1=env.k1, inv_reward_scale=1.0 / env.reward_scale)
     s = SmacState(*[getattr(env, n).data_ptr() for n in ("gid", "ep_ctr", "apos", "ahp", "epos", "ehp", "t", "last",
                                                         "battles_won", "battles_game", "perm")])
     f32 = dict(device=dev, dtype=torch.float32)
