@@ -61,6 +61,8 @@ struct DecParams {
                          // with one row per pass (stride 1, token inputs) the head phase writes the NEXT row's
                          // block-0 query / K / V / residual straight from this table and block 0's projection
                          // phase (one MFMA GEMM + barrier per agent step) disappears
+  int q2pre;             // 1: the cross-attention queries W_q2 rep_i + b of every row are precomputed into LDS
+                         // before the agent loop (they depend only on the encoder output, ma_transformer.py:114)
   uint32_t genv0;        // global id of batch row 0: the noise of row b is keyed by env genv0 + b, so the rollout of a
                          // global env does not depend on how envs are split over ranks
 };
@@ -189,13 +191,13 @@ __device__ __forceinline__ float xrow_max(float x) {   // max over the 4 lane ro
 // Single-pass online softmax in log2 units; P enters as a hi/lo bf16 pair (fp32-like P·V).  O (bf16) -> XA rows.
 // Masked keys (j > i, or rows of other caches beyond the chunk) get P = 0; every cache row is finite (zeroed at
 // kernel start, plus 32 zero rows after the last cache) so 0 · V stays 0.
-__device__ __forceinline__ void attention_mfma(const bf16_t* KV, int rowK, int rowV, const bf16_t* QT, bf16_t* XA,
-                                               int plo, int R, int imax, int wave, int lane) {
+__device__ __forceinline__ void attention_mfma(const bf16_t* KV, int rowK, int rowV, const bf16_t* QT, int qrow0,
+                                               bf16_t* XA, int plo, int R, int imax, int wave, int lane) {
   if (wave >= 2) return;
   const int h = wave, g = lane >> 4, c = lane & 15;
   constexpr float SL2 = 0.17677669529663687f * 1.4426950408889634f;   // 1/sqrt(32) * log2(e)
   const int iq = c < R ? plo + c : -1;
-  const bf16x8 qB = lda_tm(QT, c, 4 * h + g);
+  const bf16x8 qB = lda_tm(QT, qrow0 + c, 4 * h + g);
   float m = -INFINITY, l = 0.f;
   f32x4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
   for (int kb = 0; kb <= imax; kb += 32) {
@@ -483,6 +485,9 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
   float* XR = (float*)ptr;  ptr += 16 * SP * 4;
   bf16_t* XA = (bf16_t*)ptr; ptr += 16 * XP * 2;
   bf16_t* QT = (bf16_t*)ptr; ptr += 16 * 64 * 2;   // attention queries, token-major swizzled (tile.h tmo)
+  const bool q2pre = p.q2pre != 0;
+  bf16_t* Q2T = (bf16_t*)ptr;                        // [NB][L + 16] precomputed cross-attention queries (q2pre)
+  if (q2pre) ptr += (size_t)NB * (L + 16) * 64 * 2;
   float* LNP = (float*)ptr; ptr += NLN * 128 * 4;
   int* TOK = (int*)ptr;     ptr += ((EPW * L * 4 + 15) & ~15);
   int* PEND = (int*)ptr;    ptr += ((EPW * L * 4 + 15) & ~15);
@@ -524,6 +529,8 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
   for (int i = tid; i < 16 * XP; i += 256) XA[i] = 0;   // dead tile rows keep finite A-operand rows
   for (size_t i = (size_t)tid * 8; i < kv_elems; i += 256 * 8) *(uint4*)(KV + i) = make_uint4(0, 0, 0, 0);
   for (int i = tid; i < 16 * 64; i += 256) QT[i] = 0;
+  if (q2pre)
+    for (size_t i = (size_t)tid * 8; i < (size_t)NB * (L + 16) * 64; i += 256 * 8) *(uint4*)(Q2T + i) = make_uint4(0, 0, 0, 0);
   if (stage) {   // the workgroup's envs are contiguous in every input
     const int nrow = n_env * L;
     const float4* src = (const float4*)(p.rep + (size_t)env0 * L * 64);
@@ -546,6 +553,25 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
   const float* bh2 = stage ? WH2 + AD * 64 : p.bh2;
   const float* qkv0 = stage ? QKV0S : p.qkv0;
   __syncthreads();
+  if (q2pre) {   // q2 of every agent row, every block: one MFMA pass over 16-row tiles of rep before the agent loop
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      for (int t0 = 0; t0 < L; t0 += 16) {
+        bf16x8 a[2];
+        float xf[16];
+        const int ri = t0 + c16;
+        const float* rrow = ri >= L ? nullptr : stage ? REP + (size_t)ri * 64 : p.rep + ((size_t)env0 * L + ri) * 64;
+        afrag_rowf(rrow, lane, a, xf);
+        const f32x4 q2 = mfma2(a, wb[b * 10 + 4], f32x4{0, 0, 0, 0});
+        const int col = 16 * wave + c16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = t0 + 4 * g4 + r;
+          if (row < L) Q2T[(size_t)b * (L + 16) * 64 + tmo(row, col)] = f2bf(q2[r] + bcol[b * 10 + 4]);
+        }
+      }
+    }
+  }
   if (fast0 && tid < 64) {   // row 0 (the start token): block-0 query / K / V / residual x from the table
     const float* tq = qkv0 + (size_t)p.tok_start * 192;
     QT[tmo(0, tid)] = f2bf(tq[tid]);
@@ -607,7 +633,7 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
         }
         MDL_PROF_MARK(1);
         // ---------------- [B] causal self-attention over cached rows 0..i
-        attention_mfma(KV, kv_row(b, 0, 0, L), kv_row(b, 1, 0, L), QT, XA, plo, R, imax, wave, lane);
+        attention_mfma(KV, kv_row(b, 0, 0, L), kv_row(b, 1, 0, L), QT, 0, XA, plo, R, imax, wave, lane);
         __syncthreads();
         MDL_PROF_MARK(2);
         // ---------------- [C] proj1 + bias + residual x -> S
@@ -626,20 +652,22 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
         // ---------------- [D] x1 = LN1(S); k2, v2 from x1; q2 from rep_i
         afrag_ln(S, LNP + (3 * b + 0) * 128, LNP + (3 * b + 0) * 128 + 64, lane, a, xf);
         {
-          bf16x8 ar[2];
-          float rf[16];
-          const float* rrow = arow_i < 0 ? nullptr
-                              : stage ? REP + ((size_t)arow_m * L + arow_i) * 64
-                                      : p.rep + ((size_t)(env0 + arow_m) * L + arow_i) * 64;
-          afrag_rowf(rrow, lane, ar, rf);
           f32x4 k2 = mfma2(a, wb[b * 10 + 5], f32x4{0, 0, 0, 0});
           f32x4 v2 = mfma2(a, wb[b * 10 + 6], f32x4{0, 0, 0, 0});
-          f32x4 q2 = mfma2(ar, wb[b * 10 + 4], f32x4{0, 0, 0, 0});
+          if (!q2pre) {
+            bf16x8 ar[2];
+            float rf[16];
+            const float* rrow = arow_i < 0 ? nullptr
+                                : stage ? REP + ((size_t)arow_m * L + arow_i) * 64
+                                        : p.rep + ((size_t)(env0 + arow_m) * L + arow_i) * 64;
+            afrag_rowf(rrow, lane, ar, rf);
+            const f32x4 q2 = mfma2(ar, wb[b * 10 + 4], f32x4{0, 0, 0, 0});
+#pragma unroll
+            for (int r = 0; r < 4; ++r) QT[tmo(4 * g4 + r, 16 * wave + c16)] = f2bf(q2[r] + bcol[b * 10 + 4]);
+          }
           const int col = 16 * wave + c16;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int row = 4 * g4 + r;
-            QT[tmo(row, col)] = f2bf(q2[r] + bcol[b * 10 + 4]);
             if (crow_i[r] >= 0) {
               KV[kv_off(b, 2, crow_i[r], col, L)] = f2bf(k2[r] + bcol[b * 10 + 5]);
               KV[kv_off(b, 3, crow_i[r], col, L)] = f2bf(v2[r] + bcol[b * 10 + 6]);
@@ -649,7 +677,8 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
         __syncthreads();
         MDL_PROF_MARK(4);
         // ---------------- [E] causal cross-attention (q = rep rows, k/v = x1 rows)
-        attention_mfma(KV, kv_row(b, 2, 0, L), kv_row(b, 3, 0, L), QT, XA, plo, R, imax, wave, lane);
+        attention_mfma(KV, kv_row(b, 2, 0, L), kv_row(b, 3, 0, L), q2pre ? Q2T + (size_t)b * (L + 16) * 64 : QT,
+                       q2pre ? plo : 0, XA, plo, R, imax, wave, lane);
         __syncthreads();
         MDL_PROF_MARK(5);
         // ---------------- [F] proj2 + bias + rep_i -> S
@@ -838,6 +867,11 @@ MDL_API int mdl_mat_decode(const DecParams* p, int NB, hipStream_t st) {
   const size_t sb = mat_decode_stage_bytes(epw, p->L, p->act_dim, p->n_tok);
   q.stage = stage_ok && lds + sb <= 160 * 1024 && (p->rep != nullptr);
   if (q.stage) lds += sb;
+  // precomputed cross-attention queries (MAT_DCML_DECODE_Q2PRE=0 disables) when they fit as well
+  static const bool q2_ok = [] { const char* e = getenv("MAT_DCML_DECODE_Q2PRE"); return !(e && e[0] == '0'); }();
+  const size_t q2b = (size_t)NB * (p->L + 16) * 64 * 2;
+  q.q2pre = q2_ok && lds + q2b <= 160 * 1024 && p->rep != nullptr;
+  if (q.q2pre) lds += q2b;
   p = &q;
   switch (NB) {
     case 1:

@@ -28,7 +28,8 @@ class DecParams(ctypes.Structure):
                                             "tok_start", "tok_zero", "stage", "cont")] + \
                [(n, ctypes.c_void_p) for n in ("wa", "ba", "lnd")] + \
                [("gen", ctypes.c_int)] + [(n, ctypes.c_uint32) for n in ("rk0", "rk1", "rctr")] + \
-               [("avail_cont", ctypes.c_int), ("qkv0", ctypes.c_void_p), ("genv0", ctypes.c_uint32)]
+               [("avail_cont", ctypes.c_int), ("qkv0", ctypes.c_void_p), ("q2pre", ctypes.c_int),
+                ("genv0", ctypes.c_uint32)]
 
 
 sig("mdl_mat_decode", ctypes.POINTER(DecParams), i32, vp)
@@ -203,7 +204,7 @@ def decode(model, rep, ava=None, deterministic=False, stride=1, rand=None):
                     B, L, A, _n_disc(model, L), int(stride if deterministic else 1), int(bool(deterministic)), epw, rmax,
                     pk["n_tok"], pk["tok_start"], pk["tok_zero"], 0, cont,
                     P(pk.get("wa")).value, P(pk.get("ba")).value, P(pk.get("lnd")).value, int(gen), rk0, rk1, rctr,
-                    avail, P(pk.get("qkv0")).value, int(getattr(model, "_mdl_env0", 0)) & 0xFFFFFFFF)
+                    avail, P(pk.get("qkv0")).value, 0, int(getattr(model, "_mdl_env0", 0)) & 0xFFFFFFFF)
     check(lib().mdl_mat_decode(ctypes.byref(prm), model.n_block, kernels._stream()), "mat_decode")
     return out_a, out_lp
 

@@ -15,3 +15,7 @@ bash scripts/kstats.sh || exit 3
 rm -f gpurun_out/ct_ab.txt
 bash scripts/ct_ab.sh || exit 4
 if [ -f mat_dcml_amd/_lib/libmatdcml_ctprof.so ]; then bash scripts/ct_prof.sh > /dev/null || exit 5; cat gpurun_out/ct_prof.txt | head -80; fi
+if [ -f mat_dcml_amd/_lib/libmatdcml_prof.so ]; then
+  MAT_DCML_LIBNAME=libmatdcml_prof.so timeout -k 10 200 python -u scripts/decode_prof.py > gpurun_out/decode_prof.txt 2>&1 || { tail -20 gpurun_out/decode_prof.txt; exit 6; }
+  grep -v amdgpu gpurun_out/decode_prof.txt | head -16
+fi
