@@ -650,7 +650,51 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
     self_attn_bwd_ct(B.m, B.ln[0], dx, p.sv[bb].xin, p.sv[bb].a1, p.sv[bb].lse1, true, cc);
   }
   // ---------------- embedding backward: dW_a[:, token] += d pre ; LN_dec params
-  {
+  if (!CONT) {
+    // discrete tokens: dW_a (64 x (A+1)) = Σ_rows d pre ⊗ onehot(token) — a weight-gradient GEMM on MFMA with the
+    // one-hot rows as X (wgrad_g), d pre as a hi/lo bf16 pair; replaces per-element LDS atomics that collided on
+    // the (A+1) token rows (16-way address conflicts per wave instruction)
+    CT dlg, dlb;
+    ct_zero(dlg);
+    ct_zero(dlb);
+    const CT gam = ld_vec(p.lnd_g, lane), bet = ld_vec(p.lnd_b, lane);
+    const int g = lane >> 4;
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + NW * k;
+      if (rt < c.NT) {
+        const bool ok = tok_ok(rt, c);
+        int tk;
+        const CT pre = dec_embed_pre_ct<CONT>(p, rt, tk, c);
+        CT e = pre, xh, yy, de;
+        gelu_ct(e);
+        const float rs = ln_fwd_ct(e, xh, yy, gam, bet);
+        ln_bwd_ct(dx[k], xh, rs, gam, ok, de, dlg, dlb);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) de.v[mt][r] = ok ? de.v[mt][r] * gelu_erf_grad(pre.v[mt][r]) : 0.f;
+        CTr dh, dl, oh;
+        ct_split(de, dh, dl);
+        CT onehot;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) onehot.v[mt][r] = (ok && 16 * mt + 4 * g + r == tk) ? 1.f : 0.f;
+        oh = ct_pack(onehot);
+        st_lds(c.DA, rt, dh, ok, lane);   // dY (hi)
+        st_lds(c.DQ, rt, dl, ok, lane);   // dY (lo)
+        st_lds(c.XB, rt, oh, ok, lane);   // X = one-hot token rows
+      }
+    }
+    flush_vec(dlg, c.g(p.d_lnd_g), lane);
+    flush_vec(dlb, c.g(p.d_lnd_b), lane);
+    __syncthreads();
+    if (p.d_wa) {
+      wgrad_g(c.DA, c.XB, c.NRP, c.g(p.d_wa), p.A + 1, 64, p.A + 1, nullptr, c.wave, lane);
+      wgrad_g(c.DQ, c.XB, c.NRP, c.g(p.d_wa), p.A + 1, 64, p.A + 1, nullptr, c.wave, lane);
+    }
+  } else {
     float* EMB = (float*)c.QB;   // [(A+1)][64] f32 accumulators (QB + KB: 2 NRP x 128 B >= 65 x 256 B)
     for (int i = c.tid; i < (p.A + 1) * 64; i += NTHR) EMB[i] = 0.f;
     __syncthreads();
@@ -670,7 +714,7 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
         gelu_ct(e);
         const float rs = ln_fwd_ct(e, xh, yy, gam, bet);
         ln_bwd_ct(dx[k], xh, rs, gam, ok, de, dlg, dlb);
-        if (ok && CONT) {   // EMB[k][f] += d pre_f * a_prev_k (k < A), EMB[A][f] += d pre_f (bias)
+        if (ok) {   // EMB[k][f] += d pre_f * a_prev_k (k < A), EMB[A][f] += d pre_f (bias)
           const int row = rt * 16 + (lane & 15);
           const bool first = row % c.L == 0;
           const float* prev = p.act + (size_t)(c.tok0 + (first ? 0 : row - 1)) * p.A;
@@ -684,29 +728,17 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
               if (!first)
                 for (int kk = 0; kk < p.A; ++kk) atomicAdd(EMB + kk * 64 + f, dp * prev[kk]);
             }
-        } else if (ok) {
-#pragma unroll
-          for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              atomicAdd(EMB + tk * 64 + 16 * mt + 4 * g + r, de.v[mt][r] * gelu_erf_grad(pre.v[mt][r]));
         }
       }
     }
     flush_vec(dlg, c.g(p.d_lnd_g), lane);
     flush_vec(dlb, c.g(p.d_lnd_b), lane);
     __syncthreads();
-    if (CONT) {   // W_a [64][A] and b_a
-      for (int i = c.tid; i < (p.A + 1) * 64; i += NTHR) {
-        const int t = i / 64, col = i % 64;
-        if (t < p.A) { if (p.d_wa) atomicAdd(c.g(p.d_wa) + col * p.A + t, EMB[i]); }
-        else if (p.d_ba) atomicAdd(c.g(p.d_ba) + col, EMB[i]);
-      }
-    } else if (p.d_wa)
-      for (int i = c.tid; i < (p.A + 1) * 64; i += NTHR) {
-        const int t = i / 64, col = i % 64;
-        atomicAdd(c.g(p.d_wa) + col * (p.A + 1) + t, EMB[i]);
-      }
+    for (int i = c.tid; i < (p.A + 1) * 64; i += NTHR) {   // W_a [64][A] and b_a
+      const int t = i / 64, col = i % 64;
+      if (t < p.A) { if (p.d_wa) atomicAdd(c.g(p.d_wa) + col * p.A + t, EMB[i]); }
+      else if (p.d_ba) atomicAdd(c.g(p.d_ba) + col, EMB[i]);
+    }
   }
   CP_MARK(30);
 }

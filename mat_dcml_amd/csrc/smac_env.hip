@@ -60,7 +60,7 @@ struct SmacOut {
 __device__ __forceinline__ float dist2(float ax, float ay, float bx, float by, float& dx, float& dy) {
   dx = __fsub_rn(bx, ax);
   dy = __fsub_rn(by, ay);
-  return __fsqrt_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)));
+  return (float)__dsqrt_rn((double)__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)));   // as the torch path
 }
 
 __device__ __forceinline__ float u01f(uint32_t u) { return (float)u01_open(u); }

@@ -92,7 +92,9 @@ class SyntheticSMACEnv:
 
     # ------------------------------------------------------------------------------------- core
     def _dist(self, dx, dy):
-        return torch.sqrt(dx * dx + dy * dy)
+        # fp32 squares and sum, the square root in fp64 rounded once to fp32: identical on every backend (fp32 sqrt
+        # is not correctly rounded everywhere; the kernel does the same)
+        return torch.sqrt((dx * dx + dy * dy).double()).float()
 
     def _reset_where(self, m):
         """Battle reset of the envs in ``m``: Philox draws (ep_ctr, gid, unit, P_SMAC) — ally i unit i, enemy j
