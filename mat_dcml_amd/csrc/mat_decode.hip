@@ -65,6 +65,8 @@ struct DecParams {
                          // before the agent loop (they depend only on the encoder output, ma_transformer.py:114)
   uint32_t genv0;        // global id of batch row 0: the noise of row b is keyed by env genv0 + b, so the rollout of a
                          // global env does not depend on how envs are split over ranks
+  const float* hfold;    // [act_dim][64] W_h2 diag(gamma_h), then G[act_dim] = Σ_c W_h2 gamma_h, C[act_dim] = W_h2 beta_h
+                         // + b_h2: the head LayerNorm folded into the logit GEMV (fused head of one-row passes)
 };
 
 // in-kernel sampling noise: one Philox block per (global env, row, call counter, purpose); purpose 0 = the categorical uniform (x) and
@@ -253,6 +255,7 @@ __device__ __forceinline__ void attention_mfma(const bf16_t* KV, int rowK, int r
 // categorical sample over <= 4 register logits (every lane of the row computes it alike): availability mask,
 // inverse-CDF draw (argmax when deterministic); returns the action, its masked logit and the log-sum-exp
 constexpr int SMALL_AD = 4;
+#define SMALL_AD_ 4
 __device__ __forceinline__ int sample_small(const float* lgr, int AD, const float* av, float uu, bool det, float& la,
                                             float& lse) {
   float l[SMALL_AD];
@@ -514,16 +517,15 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
   float bcol[NG];
 #pragma unroll
   for (int gi = 0; gi < NG; ++gi) bcol[gi] = p.bias[gi * 64 + 16 * wave + c16];
-  // head1's other three column slices + biases (the fused head of one-row passes runs head1 whole in wave 0)
-  bf16x8 wh1x[3][2];
-  float bh1x[4];
+  // folded head (one-row discrete passes, <= 4 actions): this lane's column 16 wave + c16 of W_h2 diag(gamma_h)
+  float hw[SMALL_AD_], hG[SMALL_AD_], hC[SMALL_AD_];
 #pragma unroll
-  for (int ct = 1; ct < 4; ++ct)
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-      wh1x[ct - 1][ks] = *(const bf16x8*)(p.wpack + ((size_t)(((NG - 1) * 4 + ct) * 2 + ks) * 64 + lane) * 8);
-#pragma unroll
-  for (int ct = 0; ct < 4; ++ct) bh1x[ct] = p.bias[(NG - 1) * 64 + 16 * ct + c16];
+  for (int a = 0; a < SMALL_AD_; ++a) {
+    const bool in = p.hfold && a < AD;
+    hw[a] = in ? p.hfold[a * 64 + 16 * wave + c16] : 0.f;
+    hG[a] = in ? p.hfold[AD * 64 + a] : 0.f;
+    hC[a] = in ? p.hfold[AD * 65 + a] : 0.f;
+  }
   for (int i = tid; i < NLN * 128; i += 256) LNP[i] = p.lnp[i];
   for (int i = tid; i < EPW * L; i += 256) { TOK[i] = (i % L == 0) ? p.tok_start : p.tok_zero; PEND[i] = -1; }
   for (int i = tid; i < 16 * XP; i += 256) XA[i] = 0;   // dead tile rows keep finite A-operand rows
@@ -727,55 +729,62 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
         __syncthreads();
         MDL_PROF_MARK(8);
       }
-      // ---------------- [I+J fused] one discrete row per pass, <= 4 actions: wave 0 runs head1 for all 64
-      // columns, the head LayerNorm, the logits and the sampling from registers — no Q staging, one barrier
-      if (fast0 && AD <= SMALL_AD && plo < p.n_disc) {
-        if (wave == 0) {
+      // ---------------- [I+J fused] one discrete row per pass, <= 4 actions, head LayerNorm folded into the logit
+      // weights (p.hfold).  J1, every wave: head1 of its 16 columns for the row, GELU, and the partial sums
+      // Σx, Σx², Σ_c (W_h2 γ)[a, c] x_c of those columns -> LDS; J2, every wave alike: combine the 4 partials,
+      // logits = rstd (P_a - mean G_a) + C_a, sample, and write its slice of the next row's block-0 operands.
+      // (Round 2 ran the whole head in wave 0: 8 MFMAs, 4 GELUs and serial reductions per lane; 4.3k cycles.)
+      if (fast0 && AD <= SMALL_AD && plo < p.n_disc && p.hfold) {
+        float* PART = Q;   // [4 waves][8] partial sums (the head1 staging buffer is unused on this path)
+        {
           bf16x8 a[2];
           float xf[16];
           afrag_ln(S, LNP + (3 * (NB - 1) + 2) * 128, LNP + (3 * (NB - 1) + 2) * 128 + 64, lane, a, xf);
-          f32x4 acc[4];
-          acc[0] = mfma2(a, wb[NG - 1], f32x4{0, 0, 0, 0});
+          const f32x4 acc = mfma2(a, wb[NG - 1], f32x4{0, 0, 0, 0});
+          if (g4 == 0) {   // lanes 0..15: tile row 0 (element r = 0), column 16 wave + c16
+            const float x = gelu_erf(acc[0] + bcol[NG - 1]);
+            const float s1 = group_sum<16>(x), s2 = group_sum<16>(x * x);
+            float pa[SMALL_AD];
 #pragma unroll
-          for (int ct = 1; ct < 4; ++ct) acc[ct] = mfma2(a, wh1x[ct - 1], f32x4{0, 0, 0, 0});
-          if (g4 == 0) {   // lanes 0..15 hold tile row 0 (element r = 0): column 16 ct + c16
-            const float* lnh = LNP + 3 * NB * 128;
-            float x[4];
-#pragma unroll
-            for (int ct = 0; ct < 4; ++ct) x[ct] = gelu_erf(acc[ct][0] + bh1x[ct]);
-            const float sm = group_sum<16>((x[0] + x[1]) + (x[2] + x[3]));
-            const float sq = group_sum<16>((x[0] * x[0] + x[1] * x[1]) + (x[2] * x[2] + x[3] * x[3]));
-            const float mean = sm * (1.f / 64.f);
-            const float rstd = rsqrtf(fmaxf(sq * (1.f / 64.f) - mean * mean, 0.f) + 1e-5f);
-            float xn[4];
-#pragma unroll
-            for (int ct = 0; ct < 4; ++ct) {
-              const int col = 16 * ct + c16;
-              xn[ct] = (x[ct] - mean) * rstd * lnh[col] + lnh[64 + col];
-            }
-            float lgr[SMALL_AD];
-#pragma unroll
-            for (int aa = 0; aa < SMALL_AD; ++aa) {
-              float part = 0.f;
-              if (aa < AD) {
-#pragma unroll
-                for (int ct = 0; ct < 4; ++ct) part += xn[ct] * wh2[aa * 64 + 16 * ct + c16];
-              }
-              lgr[aa] = group_sum<16>(part) + (aa < AD ? bh2[aa] : 0.f);
-            }
-            const int i = plo;
-            const size_t oi = (size_t)env0 * L + i, li = (size_t)i;
-            const float* av = p.ava ? (stage ? AVA + li * AD : p.ava + oi * AD) : nullptr;
-            const float uu = p.deterministic ? 0.f : stage ? RU[li] : p.gen ? draw_u(p, env0, i) : p.rnd_u[oi];
-            float la, lse;
-            const int act = sample_small(lgr, AD, av, uu, p.deterministic != 0, la, lse);
+            for (int aa = 0; aa < SMALL_AD; ++aa) pa[aa] = aa < AD ? group_sum<16>(x * hw[aa]) : 0.f;
             if (c16 == 0) {
-              p.out_a[oi] = (float)act;
-              p.out_lp[oi] = la - lse;
-              PEND[i] = act;
+              PART[wave * 8 + 0] = s1;
+              PART[wave * 8 + 1] = s2;
+#pragma unroll
+              for (int aa = 0; aa < SMALL_AD; ++aa) PART[wave * 8 + 2 + aa] = pa[aa];
             }
-            if (i + 1 < L) write_next_row0(qkv0, emb, 1 + act, i + 1, L, c16, QT, KV, XR);
           }
+        }
+        __syncthreads();
+        MDL_PROF_MARK(9);
+        if (g4 == 0) {
+          float s1 = 0.f, s2 = 0.f, pa[SMALL_AD];
+#pragma unroll
+          for (int aa = 0; aa < SMALL_AD; ++aa) pa[aa] = 0.f;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {   // fixed order: every wave computes bit-identical logits
+            s1 += PART[w * 8 + 0];
+            s2 += PART[w * 8 + 1];
+#pragma unroll
+            for (int aa = 0; aa < SMALL_AD; ++aa) pa[aa] += PART[w * 8 + 2 + aa];
+          }
+          const float mean = s1 * (1.f / 64.f);
+          const float rstd = rsqrtf(fmaxf(s2 * (1.f / 64.f) - mean * mean, 0.f) + 1e-5f);
+          float lgr[SMALL_AD];
+#pragma unroll
+          for (int aa = 0; aa < SMALL_AD; ++aa) lgr[aa] = rstd * (pa[aa] - mean * hG[aa]) + hC[aa];
+          const int i = plo;
+          const size_t oi = (size_t)env0 * L + i, li = (size_t)i;
+          const float* av = p.ava ? (stage ? AVA + li * AD : p.ava + oi * AD) : nullptr;
+          const float uu = p.deterministic ? 0.f : stage ? RU[li] : p.gen ? draw_u(p, env0, i) : p.rnd_u[oi];
+          float la, lse;
+          const int act = sample_small(lgr, AD, av, uu, p.deterministic != 0, la, lse);
+          if (wave == 0 && c16 == 0) {
+            p.out_a[oi] = (float)act;
+            p.out_lp[oi] = la - lse;
+            PEND[i] = act;
+          }
+          if (i + 1 < L && c16 < 4) write_next_row0(qkv0, emb, 1 + act, i + 1, L, 4 * wave + c16, QT, KV, XR);
         }
         __syncthreads();
         MDL_PROF_MARK(10);

@@ -29,7 +29,7 @@ class DecParams(ctypes.Structure):
                [(n, ctypes.c_void_p) for n in ("wa", "ba", "lnd")] + \
                [("gen", ctypes.c_int)] + [(n, ctypes.c_uint32) for n in ("rk0", "rk1", "rctr")] + \
                [("avail_cont", ctypes.c_int), ("qkv0", ctypes.c_void_p), ("q2pre", ctypes.c_int),
-                ("genv0", ctypes.c_uint32)]
+                ("genv0", ctypes.c_uint32), ("hfold", ctypes.c_void_p)]
 
 
 sig("mdl_mat_decode", ctypes.POINTER(DecParams), i32, vp)
@@ -136,6 +136,13 @@ def decoder_pack(model):
                 wh2=dec.head[3].weight.detach().float().contiguous(), bh2=dec.head[3].bias.detach().float().contiguous(),
                 stdv=std.contiguous(), n_tok=toks.shape[0], tok_start=tok_start, tok_zero=tok_zero,
                 cont=int(cont or avail), avail=int(avail))
+    if not (cont or avail) and A <= 4:
+        # head LayerNorm folded into the logit GEMV of the fused one-row head: W_h2 diag(gamma), Σ_c W_h2 gamma,
+        # W_h2 beta + b_h2 (csrc/mat_decode.hip DecParams.hfold)
+        w2, b2 = dec.head[3].weight.detach().float(), dec.head[3].bias.detach().float()
+        gam, bet = dec.head[2].weight.detach().float(), dec.head[2].bias.detach().float()
+        w2g = w2 * gam.view(1, -1)
+        pack["hfold"] = torch.cat([w2g.reshape(-1), w2g.sum(1), w2 @ bet + b2]).contiguous()
     if not (cont or avail):
         # block-0 q / k / v of every token row (the decode's first projection depends only on the previous action)
         a1 = dec.blocks[0].attn1
@@ -204,7 +211,8 @@ def decode(model, rep, ava=None, deterministic=False, stride=1, rand=None):
                     B, L, A, _n_disc(model, L), int(stride if deterministic else 1), int(bool(deterministic)), epw, rmax,
                     pk["n_tok"], pk["tok_start"], pk["tok_zero"], 0, cont,
                     P(pk.get("wa")).value, P(pk.get("ba")).value, P(pk.get("lnd")).value, int(gen), rk0, rk1, rctr,
-                    avail, P(pk.get("qkv0")).value, 0, int(getattr(model, "_mdl_env0", 0)) & 0xFFFFFFFF)
+                    avail, P(pk.get("qkv0")).value, 0, int(getattr(model, "_mdl_env0", 0)) & 0xFFFFFFFF,
+                    P(pk.get("hfold")).value)
     check(lib().mdl_mat_decode(ctypes.byref(prm), model.n_block, kernels._stream()), "mat_decode")
     return out_a, out_lp
 
