@@ -104,7 +104,7 @@ class MATTrainer:
         self.loss_fused = ppo_fused.PPOLossFused(self, self.device)
         if self.comm.world_size > 1:
             self.grad_allreduce = self.comm.maybe_enable_oneshot(flat.buf.numel())
-        copies = int(os.environ.get("MAT_DCML_GRAD_COPIES", "8"))
+        copies = int(os.environ.get("MAT_DCML_GRAD_COPIES", "32"))
         if copies > 0:
             mat_train.attach_grad_workspace(m, flat.buf, copies=copies)
         pol.optimizer = ppo_fused.FlatAdam(fp, flat.buf, lr=pol.optimizer.param_groups[0]["lr"], eps=args.opti_eps,

@@ -126,6 +126,7 @@ __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, C
                                                   const bf16_t* sv_x1, const bf16_t* sv_a, const float* sv_lse,
                                                   bool first, const Ctx& c) {
   const int lane = c.lane;
+  const LseR lse = lse_fetch(sv_lse, c);   // consumed after the recompute phase (latency hidden by passes 1-2)
   CT dres[MAXRT];
   {
     CT dlg, dlb;
@@ -184,7 +185,7 @@ __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, C
   __syncthreads();
   CP_MARK(5);
   cross_proj<false>(m, nullptr, sv_x1, rep, nullptr, c);
-  load_lse(sv_lse, c);
+  lse_store(lse, c);
   __syncthreads();
   CP_MARK(6);
   attn_bwd_q_ct(c.QB, c.KB, c.VB, c.DA, c.DQ, true, c);
@@ -634,7 +635,7 @@ template <int NB, int MA, bool CONT>
 __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0, int nseq) {
   const Ctx c = make_ctx(p, smem, seq0, nseq);
   if (c.nseq <= 0) return;
-  zero_lds(smem, mat_train_lds_bytes(p.NRP, p.SQ, p.L), c.tid);
+  zero_pad_rows(c);
   __syncthreads();
   CP_MARK(0);
   const int lane = c.lane;

@@ -176,7 +176,7 @@ template <int NB>
 __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char* smem, int seq0, int nseq) {
   const Ctx c = make_ctx(p, smem, seq0, nseq);
   if (c.nseq <= 0) return;
-  zero_lds(smem, mat_train_lds_bytes(p.NRP, p.SQ, p.L), c.tid);
+  zero_pad_rows(c);
   __syncthreads();
   CP_MARK(0);
   const int lane = c.lane;

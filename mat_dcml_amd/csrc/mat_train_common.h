@@ -144,6 +144,42 @@ __device__ __forceinline__ void load_lse(const float* sv_lse, const Ctx& c) {
   }
 }
 
+// the same in two halves: issue the global loads early (lse_fetch, registers), store them to LDS later (lse_store),
+// so the load latency hides under the work in between instead of stalling right before a barrier
+struct LseR { float v[2]; };
+__device__ __forceinline__ LseR lse_fetch(const float* sv_lse, const Ctx& c) {
+  LseR r;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int i = c.tid + j * NTHR;
+    const int h = i / c.NRP, row = i - h * c.NRP;
+    r.v[j] = (i < 2 * c.NRP && row < c.NR) ? sv_lse[(size_t)(c.tok0 + row) * 2 + h] : 0.f;
+  }
+  return r;
+}
+__device__ __forceinline__ void lse_store(const LseR& r, const Ctx& c) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int i = c.tid + j * NTHR;
+    if (i < 2 * c.NRP) c.LSE[i] = r.v[j];
+  }
+}
+
+// Backward tile start: zero only what no phase rewrites before reading — the padded rows [16 NT, NRP) of the six
+// token-major buffers and of delta.  Rows below 16 NT are always written (zeros for rows >= NR) by the phase that
+// produces them before any phase reads them; LSE is fully rewritten per attention.  (Round 2 zeroed all ~150 KB.)
+__device__ __forceinline__ void zero_pad_rows(const Ctx& c) {
+  const int r0 = c.NT * 16, nr = c.NRP - r0;
+  if (nr <= 0) return;
+  bf16_t* bufs[6] = {c.QB, c.KB, c.VB, c.DA, c.DQ, c.XB};
+  const int per = nr * 8;   // 16-byte pieces per buffer
+  for (int i = c.tid; i < 6 * per; i += NTHR) {
+    const int b = i / per, o = i - b * per;
+    *(uint4*)(bufs[b] + (size_t)r0 * 64 + (size_t)o * 8) = make_uint4(0, 0, 0, 0);
+  }
+  for (int i = c.tid; i < 2 * nr; i += NTHR) c.DEL[(i / nr) * c.NRP + r0 + (i % nr)] = 0.f;
+}
+
 __device__ __forceinline__ void zero_lds(char* smem, size_t bytes, int tid) {
   for (size_t i = (size_t)tid * 16; i < bytes; i += NTHR * 16) *(uint4*)(smem + i) = make_uint4(0, 0, 0, 0);
 }

@@ -800,6 +800,7 @@ __device__ __forceinline__ void mlp_bwd_ct(const Mat& m1, const Mat& m2, const L
 __device__ __forceinline__ void self_attn_bwd_ct(const Mat* m, const LNp& ln, CT* dx, const bf16_t* sv_xin,
                                                  const bf16_t* sv_a, const float* sv_lse, bool causal, const Ctx& c) {
   const int lane = c.lane;
+  const LseR lse = lse_fetch(sv_lse, c);   // consumed after the recompute phase (latency hidden by passes 1-2)
   CTr xin[MAXRT];
   {
     CT dlg, dlb;
@@ -863,7 +864,7 @@ __device__ __forceinline__ void self_attn_bwd_ct(const Mat* m, const LNp& ln, CT
     const int rt = c.wave + NW * k;
     if (rt < c.NT) st_lds(c.XB, rt, xin[k], tok_ok(rt, c), lane);   // X of dWq / dWk / dWv
   }
-  load_lse(sv_lse, c);
+  lse_store(lse, c);
   __syncthreads();
   CP_MARK(13);
   attn_bwd_q_ct(c.QB, c.KB, c.VB, c.DA, c.DQ, causal, c);

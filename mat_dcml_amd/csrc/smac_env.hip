@@ -63,6 +63,12 @@ __device__ __forceinline__ float dist2(float ax, float ay, float bx, float by, f
   return (float)__dsqrt_rn((double)__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)));   // as the torch path
 }
 
+__device__ __forceinline__ float sq2(float ax, float ay, float bx, float by) {   // squared distance, torch order
+  const float dx = __fsub_rn(bx, ax), dy = __fsub_rn(by, ay);
+  return __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy));
+}
+constexpr float SHOOT2 = 36.f, SIGHT2 = 81.f;
+
 __device__ __forceinline__ float u01f(uint32_t u) { return (float)u01_open(u); }
 
 __device__ __forceinline__ float dir_x(int k) { return k == 2 ? 1.f : (k == 3 ? -1.f : 0.f); }   // N, S, E, W
@@ -114,9 +120,7 @@ __global__ __launch_bounds__(SM_THREADS) void smac_env_kernel(SmacCfg c, SmacSta
       const int a = act[tid];
       if (a >= 6 && ah[tid] > 0.f) {
         const int tg = min(max(a - 6, 0), N - 1);
-        float dx, dy;
-        const float d = dist2(ax[tid], ay[tid], ex[tg], ey[tg], dx, dy);
-        if (d <= SHOOT && eh[tg] > 0.f) atomicAdd(&dmg[tg], ADMG);   // equal addends: order-free sum
+        if (sq2(ax[tid], ay[tid], ex[tg], ey[tg]) <= SHOOT2 && eh[tg] > 0.f) atomicAdd(&dmg[tg], ADMG);   // equal addends
       }
     }
     __syncthreads();
@@ -131,11 +135,10 @@ __global__ __launch_bounds__(SM_THREADS) void smac_env_kernel(SmacCfg c, SmacSta
         int near = 0;
         for (int i = 0; i < A; ++i) {
           if (!(ah[i] > 0.f)) continue;
-          float dx, dy;
-          const float d = dist2(ex[tid], ey[tid], ax[i], ay[i], dx, dy);
+          const float d = sq2(ax[i], ay[i], ex[tid], ey[tid]);   // squared: no square root in the dynamics
           if (d < best) { best = d; near = i; }
         }
-        if (best <= SHOOT) {
+        if (best <= SHOOT2) {
           atomicAdd(&admg[near], EDMG);
         } else if (best < INFINITY) {
           float vx, vy;
@@ -244,8 +247,9 @@ __global__ __launch_bounds__(SM_THREADS) void smac_env_kernel(SmacCfg c, SmacSta
       const int k = (f - o_e) / EF, q = f - o_e - k * EF;
       float dx, dy;
       const float d = dist2(ax[i], ay[i], ex[k], ey[k], dx, dy);
-      const float vis = (d <= SIGHT ? 1.f : 0.f) * (eh[k] > 0.f ? 1.f : 0.f) * al;
-      const float fv = q == 0 ? (d <= SHOOT ? 1.f : 0.f) * vis : q == 1 ? __fmul_rn(d, INV_SIGHT)
+      const float d2 = sq2(ax[i], ay[i], ex[k], ey[k]);
+      const float vis = (d2 <= SIGHT2 ? 1.f : 0.f) * (eh[k] > 0.f ? 1.f : 0.f) * al;
+      const float fv = q == 0 ? (d2 <= SHOOT2 ? 1.f : 0.f) * vis : q == 1 ? __fmul_rn(d, INV_SIGHT)
                      : q == 2 ? __fmul_rn(dx, INV_SIGHT) : q == 3 ? __fmul_rn(dy, INV_SIGHT) : q == 4 ? eh[k] : 0.f;
       v = fv * vis;
     } else if (f < o_o) {
@@ -253,7 +257,7 @@ __global__ __launch_bounds__(SM_THREADS) void smac_env_kernel(SmacCfg c, SmacSta
       const int oa = qa < i ? qa : qa + 1;
       float dx, dy;
       const float d = dist2(ax[i], ay[i], ax[oa], ay[oa], dx, dy);
-      const float vis = (d <= SIGHT ? 1.f : 0.f) * (ah[oa] > 0.f ? 1.f : 0.f) * al;
+      const float vis = (sq2(ax[i], ay[i], ax[oa], ay[oa]) <= SIGHT2 ? 1.f : 0.f) * (ah[oa] > 0.f ? 1.f : 0.f) * al;
       float fv;
       if (q == 0) fv = vis;
       else if (q == 1) fv = __fmul_rn(d, INV_SIGHT);
@@ -296,8 +300,9 @@ __global__ __launch_bounds__(SM_THREADS) void smac_env_kernel(SmacCfg c, SmacSta
       float dx, dy;
       const float d = dist2(ax[i], ay[i], ex[k], ey[k], dx, dy);
       const float ea = eh[k] > 0.f ? 1.f : 0.f;
-      const float vis = (d <= SIGHT ? 1.f : 0.f) * ea * al;
-      v = q == 0 ? (d <= SHOOT ? 1.f : 0.f) * vis : q == 1 ? __fmul_rn(d, INV_SIGHT) : q == 2 ? __fmul_rn(dx, INV_SIGHT)
+      const float d2 = sq2(ax[i], ay[i], ex[k], ey[k]);
+      const float vis = (d2 <= SIGHT2 ? 1.f : 0.f) * ea * al;
+      v = q == 0 ? (d2 <= SHOOT2 ? 1.f : 0.f) * vis : q == 1 ? __fmul_rn(d, INV_SIGHT) : q == 2 ? __fmul_rn(dx, INV_SIGHT)
         : q == 3 ? __fmul_rn(dy, INV_SIGHT) : q == 4 ? eh[k] : q == 5 ? __fdiv_rn(ex[k], MAP)
         : q == 6 ? __fdiv_rn(ey[k], MAP) : q == 7 ? ea : 0.f;
     } else if (f < s_o) {
@@ -306,7 +311,7 @@ __global__ __launch_bounds__(SM_THREADS) void smac_env_kernel(SmacCfg c, SmacSta
       float dx, dy;
       const float d = dist2(ax[i], ay[i], ax[oa], ay[oa], dx, dy);
       const float aa = ah[oa] > 0.f ? 1.f : 0.f;
-      if (q == 0) v = (d <= SIGHT ? 1.f : 0.f) * aa * al;
+      if (q == 0) v = (sq2(ax[i], ay[i], ax[oa], ay[oa]) <= SIGHT2 ? 1.f : 0.f) * aa * al;
       else if (q == 1) v = __fmul_rn(d, INV_SIGHT);
       else if (q == 2) v = __fmul_rn(dx, INV_SIGHT);
       else if (q == 3) v = __fmul_rn(dy, INV_SIGHT);
@@ -346,8 +351,8 @@ __global__ __launch_bounds__(SM_THREADS) void smac_env_kernel(SmacCfg c, SmacSta
     } else {
       const int k = q - 6;
       float dx, dy;
-      const float d = k < N ? dist2(ax[i], ay[i], ex[k], ey[k], dx, dy) : INFINITY;
-      v = (k < N && d <= SHOOT && d <= SIGHT && eh[k] > 0.f) ? al : 0.f;
+      const float d2 = k < N ? sq2(ax[i], ay[i], ex[k], ey[k]) : INFINITY;
+      v = (k < N && d2 <= SHOOT2 && d2 <= SIGHT2 && eh[k] > 0.f) ? al : 0.f;
     }
     o.ava[(size_t)e * A * nA + x] = v;
   }

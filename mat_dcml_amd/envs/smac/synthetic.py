@@ -91,6 +91,10 @@ class SyntheticSMACEnv:
         return [Discrete(self.n_actions)] * self.A
 
     # ------------------------------------------------------------------------------------- core
+    @staticmethod
+    def _d2(dx, dy):
+        return dx * dx + dy * dy
+
     def _dist(self, dx, dy):
         # fp32 squares and sum, the square root in fp64 rounded once to fp32: identical on every backend (fp32 sqrt
         # is not correctly rounded everywhere; the kernel does the same)
@@ -155,10 +159,11 @@ class SyntheticSMACEnv:
         self.apos = (self.apos + step).clamp(0.0, MAP_SIZE)
         # ally attacks
         rel = self.epos[:, None] - self.apos[:, :, None]
-        d_ae = self._dist(rel[..., 0], rel[..., 1])                                  # (E, A, N)
+        d2_ae = self._d2(rel[..., 0], rel[..., 1])      # squared distances (E, A, N): range tests and the nearest
+        #                                                  ally compare them, so no square root enters the dynamics
         tgt = (a - N_NO_ATTACK).clamp(0, N - 1)
         att = (a >= N_NO_ATTACK) & alive
-        in_rng = torch.gather(d_ae, 2, tgt.unsqueeze(-1)).squeeze(-1) <= SHOOT
+        in_rng = torch.gather(d2_ae, 2, tgt.unsqueeze(-1)).squeeze(-1) <= SHOOT * SHOOT
         e_alive = self.ehp > 0
         hit = att & in_rng & torch.gather(e_alive, 1, tgt)
         dmg = torch.zeros(E, N, device=self.device).scatter_add_(1, tgt, hit.float() * ALLY_DMG)
@@ -167,11 +172,11 @@ class SyntheticSMACEnv:
         dealt = (old_ehp - self.ehp).sum(1)
         kills = ((old_ehp > 0) & (self.ehp <= 0)).float().sum(1)
         # enemy behaviour: nearest living ally, shoot if in range else approach
-        d_ea = d_ae.transpose(1, 2).masked_fill(~alive.unsqueeze(1), float("inf"))   # (E, N, A)
-        dist, near = d_ea.min(-1)
+        d_ea = d2_ae.transpose(1, 2).masked_fill(~alive.unsqueeze(1), float("inf"))  # (E, N, A)
+        dist, near = d_ea.min(-1)                        # squared distance to the nearest living ally
         e_alive = self.ehp > 0
-        shoot = e_alive & (dist <= SHOOT)
-        walk = e_alive & (dist > SHOOT) & torch.isfinite(dist)
+        shoot = e_alive & (dist <= SHOOT * SHOOT)
+        walk = e_alive & (dist > SHOOT * SHOOT) & torch.isfinite(dist)
         tp = torch.gather(self.apos, 1, near.unsqueeze(-1).expand(E, N, 2))
         vec = tp - self.epos
         vec = vec / self._dist(vec[..., 0], vec[..., 1]).unsqueeze(-1).clamp(min=1e-6)
@@ -211,9 +216,10 @@ class SyntheticSMACEnv:
         move = (((nxt >= 0) & (nxt <= MAP_SIZE)).all(-1).float()) * alive.unsqueeze(-1)
         # enemies
         rel_e = self.epos.unsqueeze(1) - self.apos.unsqueeze(2)                      # (E, A, N, 2)
+        d2_e = self._d2(rel_e[..., 0], rel_e[..., 1])
         d_e = self._dist(rel_e[..., 0], rel_e[..., 1])
-        vis_e = (d_e <= SIGHT).float() * e_alive.unsqueeze(1) * alive.unsqueeze(-1)
-        attackable = (d_e <= SHOOT).float() * vis_e
+        vis_e = (d2_e <= SIGHT * SIGHT).float() * e_alive.unsqueeze(1) * alive.unsqueeze(-1)
+        attackable = (d2_e <= SHOOT * SHOOT).float() * vis_e
         ef = torch.stack([attackable, d_e * INV_SIGHT, rel_e[..., 0] * INV_SIGHT, rel_e[..., 1] * INV_SIGHT,
                           self.ehp.unsqueeze(1).expand(E, A, N)], -1) * vis_e.unsqueeze(-1)
         if u:
@@ -222,7 +228,7 @@ class SyntheticSMACEnv:
         oth = self.others
         rel_a = self.apos[:, oth] - self.apos.unsqueeze(2)                           # (E, A, A-1, 2)
         d_a = self._dist(rel_a[..., 0], rel_a[..., 1])
-        vis_a = (d_a <= SIGHT).float() * alive[:, oth] * alive.unsqueeze(-1)
+        vis_a = (self._d2(rel_a[..., 0], rel_a[..., 1]) <= SIGHT * SIGHT).float() * alive[:, oth] * alive.unsqueeze(-1)
         af = torch.cat([torch.stack([vis_a, d_a * INV_SIGHT, rel_a[..., 0] * INV_SIGHT, rel_a[..., 1] * INV_SIGHT,
                                      self.ahp[:, oth]], -1), tb_a[:, oth], last1h[:, oth]], -1) * vis_a.unsqueeze(-1)
         own = torch.cat([torch.stack([self.ahp, self.apos[..., 0] / MAP_SIZE, self.apos[..., 1] / MAP_SIZE,

@@ -512,7 +512,7 @@ class _MATFusedFn(torch.autograd.Function):
         return torch.zeros((), device=drep.device), None, None, None, None, None
 
 
-def attach_grad_workspace(model, flat_grads: torch.Tensor, copies: int = 8):
+def attach_grad_workspace(model, flat_grads: torch.Tensor, copies: int = 32):
     """Spread the backward kernels' weight-gradient atomics over ``copies`` workspace copies of the flat gradient
     buffer (every parameter's ``.grad`` must be a view of ``flat_grads``); ``reduce_grad_workspace`` folds them
     back.  Cuts the number of workgroups adding into one 16 KB weight matrix by ``copies``."""

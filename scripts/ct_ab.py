@@ -33,7 +33,7 @@ def main(B=3200, L=33, reps=20):
     actions = (torch.rand(B, L, 1, device=dev) < 0.5).float()
     from mat_dcml_amd.parallel.comm import FlatGrads
     fg = FlatGrads(list(m.parameters()))   # the trainer's layout: .grad views of one flat buffer + 8-copy workspace
-    mat_train.attach_grad_workspace(m, fg.buf)
+    mat_train.attach_grad_workspace(m, fg.buf, copies=int(os.environ.get("MAT_DCML_GRAD_COPIES", "32")))
     m._mdl_gws_active = True
     enc, dec = mat_train.EncoderFused(m), mat_train.DecoderFused(m)
     st = {}
@@ -48,7 +48,8 @@ def main(B=3200, L=33, reps=20):
     st["enc_bwd"] = timed(lambda: enc.backward(drep, torch.ones_like(v)), reps)
     st["grad_reduce"] = timed(lambda: mat_train.reduce_grad_workspace(m), reps)
     st["total"] = sum(st.values())
-    print(os.environ.get("MAT_DCML_LIBNAME", "libmatdcml.so"), " ".join(f"{k} {v:.1f}us" for k, v in st.items()))
+    print(os.environ.get("MAT_DCML_LIBNAME", "libmatdcml.so"), f"copies={os.environ.get('MAT_DCML_GRAD_COPIES', '8')}",
+          " ".join(f"{k} {v:.1f}us" for k, v in st.items()))
 
 
 if __name__ == "__main__":

@@ -6,3 +6,6 @@ mkdir -p gpurun_out
 for lib in libmatdcml.so $(cd mat_dcml_amd/_lib && ls libmatdcml_ab_*.so 2>/dev/null); do
   MAT_DCML_LIBNAME=$lib timeout -k 10 120 python -u scripts/ct_ab.py 2>&1 | grep -v amdgpu.ids | tee -a gpurun_out/ct_ab.txt || exit 1
 done
+for cp in ${AB_COPIES:-}; do
+  MAT_DCML_GRAD_COPIES=$cp timeout -k 10 120 python -u scripts/ct_ab.py 2>&1 | grep -v amdgpu.ids | tee -a gpurun_out/ct_ab.txt || exit 1
+done

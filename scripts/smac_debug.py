@@ -10,8 +10,10 @@ for map_name, rao in (("27m_vs_30m", False), ("3m", False)):
     o1, o2 = hip.reset(), ref.reset()
     print(map_name, "state equal:", {n: bool(torch.equal(getattr(hip, n), getattr(ref, n))) for n in
                                      ("apos", "ahp", "epos", "ehp", "perm", "last", "t", "ep_ctr")})
-    if not torch.equal(hip.apos, ref.apos):
-        print(" apos", hip.apos[0, :3].tolist(), ref.apos[0, :3].tolist())
+    for nm in ("apos", "epos"):
+        a, b = getattr(hip, nm), getattr(ref, nm)
+        d = (a != b).nonzero()
+        print(f" {nm}: {len(d)} mismatches", [(tuple(i), float(a[tuple(i)]), float(b[tuple(i)])) for i in d[:6].tolist()])
     for name, a, b in zip(("obs", "state", "ava"), o1, o2):
         d = (a != b).nonzero()
         print(f" {name}: {len(d)} mismatches of {a.numel()}")
