@@ -76,7 +76,8 @@ __device__ __forceinline__ float dir_y(int k) { return k == 0 ? 1.f : (k == 1 ? 
 
 __global__ __launch_bounds__(SM_THREADS) void smac_env_kernel(SmacCfg c, SmacState s, SmacOut o) {
   __shared__ float ax[SM_MAXU], ay[SM_MAXU], ah[SM_MAXU], ex[SM_MAXU], ey[SM_MAXU], eh[SM_MAXU];
-  __shared__ float dmg[SM_MAXU], admg[SM_MAXU], dealt[SM_MAXU];
+  __shared__ int nhit[SM_MAXU], ahit[SM_MAXU];   // hit counts: damage = count x per-hit damage, one rounding
+  __shared__ float dealt[SM_MAXU];
   __shared__ int act[SM_MAXU], lst[SM_MAXU], prm[SM_MAXU];
   __shared__ uint32_t keys[SM_MAXU];
   __shared__ int s_reset;
@@ -94,7 +95,7 @@ __global__ __launch_bounds__(SM_THREADS) void smac_env_kernel(SmacCfg c, SmacSta
     ey[tid] = s.epos[((size_t)e * N + tid) * 2 + 1];
     eh[tid] = s.ehp[(size_t)e * N + tid];
   }
-  if (tid < SM_MAXU) { dmg[tid] = 0.f; admg[tid] = 0.f; dealt[tid] = 0.f; }
+  if (tid < SM_MAXU) { nhit[tid] = 0; ahit[tid] = 0; dealt[tid] = 0.f; }
   if (tid == 0) s_reset = c.mode == 1;
   __syncthreads();
   if (c.mode == 0) {
@@ -120,14 +121,14 @@ __global__ __launch_bounds__(SM_THREADS) void smac_env_kernel(SmacCfg c, SmacSta
       const int a = act[tid];
       if (a >= 6 && ah[tid] > 0.f) {
         const int tg = min(max(a - 6, 0), N - 1);
-        if (sq2(ax[tid], ay[tid], ex[tg], ey[tg]) <= SHOOT2 && eh[tg] > 0.f) atomicAdd(&dmg[tg], ADMG);   // equal addends
+        if (sq2(ax[tid], ay[tid], ex[tg], ey[tg]) <= SHOOT2 && eh[tg] > 0.f) atomicAdd(&nhit[tg], 1);
       }
     }
     __syncthreads();
     // ---- enemies: damage, then the nearest living ally (allies alive before the enemy fire)
     if (tid < N) {
       const float old = eh[tid];
-      const float nh = fmaxf(__fsub_rn(old, dmg[tid]), 0.f);
+      const float nh = fmaxf(__fsub_rn(old, __fmul_rn((float)nhit[tid], ADMG)), 0.f);
       eh[tid] = nh;
       dealt[tid] = __fsub_rn(old, nh);
       if (nh > 0.f) {
@@ -139,7 +140,7 @@ __global__ __launch_bounds__(SM_THREADS) void smac_env_kernel(SmacCfg c, SmacSta
           if (d < best) { best = d; near = i; }
         }
         if (best <= SHOOT2) {
-          atomicAdd(&admg[near], EDMG);
+          atomicAdd(&ahit[near], 1);
         } else if (best < INFINITY) {
           float vx, vy;
           float nrm = dist2(ex[tid], ey[tid], ax[near], ay[near], vx, vy);
@@ -151,7 +152,7 @@ __global__ __launch_bounds__(SM_THREADS) void smac_env_kernel(SmacCfg c, SmacSta
     }
     __syncthreads();
     if (tid < A) {
-      ah[tid] = fmaxf(__fsub_rn(ah[tid], admg[tid]), 0.f);
+      ah[tid] = fmaxf(__fsub_rn(ah[tid], __fmul_rn((float)ahit[tid], EDMG)), 0.f);
       lst[tid] = act[tid];
     }
     __syncthreads();

@@ -166,7 +166,8 @@ class SyntheticSMACEnv:
         in_rng = torch.gather(d2_ae, 2, tgt.unsqueeze(-1)).squeeze(-1) <= SHOOT * SHOOT
         e_alive = self.ehp > 0
         hit = att & in_rng & torch.gather(e_alive, 1, tgt)
-        dmg = torch.zeros(E, N, device=self.device).scatter_add_(1, tgt, hit.float() * ALLY_DMG)
+        # damage = hit count x per-hit damage (one rounding): independent of the reduction order of the scatter
+        dmg = torch.zeros(E, N, device=self.device).scatter_add_(1, tgt, hit.float()) * ALLY_DMG
         old_ehp = self.ehp
         self.ehp = (self.ehp - dmg).clamp(min=0.0)
         dealt = (old_ehp - self.ehp).sum(1)
@@ -181,7 +182,7 @@ class SyntheticSMACEnv:
         vec = tp - self.epos
         vec = vec / self._dist(vec[..., 0], vec[..., 1]).unsqueeze(-1).clamp(min=1e-6)
         self.epos = self.epos + vec * ENEMY_MOVE * walk.unsqueeze(-1)
-        admg = torch.zeros(E, A, device=self.device).scatter_add_(1, near, shoot.float() * ENEMY_DMG)
+        admg = torch.zeros(E, A, device=self.device).scatter_add_(1, near, shoot.float()) * ENEMY_DMG
         self.ahp = (self.ahp - admg).clamp(min=0.0)
         self.last = a
         self.t += 1
