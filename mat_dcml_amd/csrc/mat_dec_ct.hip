@@ -90,7 +90,7 @@ __device__ __forceinline__ void cross_proj(const Mat* m, const CT* xr, const bf1
 // x <- LN(rep + proj(attn(q = W_q rep, k = W_k x, v = W_v x)))   (ma_transformer.py:114)
 template <bool SAVE>
 __device__ __forceinline__ void cross_attn_fwd_ct(const Mat* m, const LNp& ln, CT* xr, const float* rep, bf16_t* sv_x1,
-                                                  bf16_t* sv_a, float* sv_lse, const Ctx& c) {
+                                                  bf16_t* sv_a, bf16_t* sv_alo, float* sv_lse, const Ctx& c) {
   const int lane = c.lane;
   __syncthreads();   // every wave done reading the self-attention's K / V
   cross_proj<true>(m, xr, nullptr, rep, SAVE ? sv_x1 : nullptr, c);
@@ -112,8 +112,12 @@ __device__ __forceinline__ void cross_attn_fwd_ct(const Mat* m, const LNp& ln, C
   for (int k = 0; k < MAXRT; ++k) {
     const int rt = c.wave + NW * k;
     if (rt < c.NT) {
-      const CTr a = ct_pack(O[k]);
-      if (SAVE) st_g(sv_a, c.tok0, rt, c.NR, a, lane);
+      CTr a, alo;
+      ct_split(O[k], a, alo);
+      if (SAVE) {
+        st_g(sv_a, c.tok0, rt, c.NR, a, lane);
+        st_g(sv_alo, c.tok0, rt, c.NR, alo, lane);
+      }
       CT t = ct_add(bp, rp[k]), xh;
       mm(t, Wp, a);
       ln_fwd_ct(t, xh, xr[k], gam, bet);
@@ -123,8 +127,8 @@ __device__ __forceinline__ void cross_attn_fwd_ct(const Mat* m, const LNp& ln, C
 
 // backward: dx (w.r.t. the sublayer output) -> d x1 (returned in dx); d rep accumulated into global drep
 __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, CT* dx, const float* rep, float* drep,
-                                                  const bf16_t* sv_x1, const bf16_t* sv_a, const float* sv_lse,
-                                                  bool first, const Ctx& c) {
+                                                  const bf16_t* sv_x1, const bf16_t* sv_a, const bf16_t* sv_alo,
+                                                  const float* sv_lse, bool first, const Ctx& c) {
   const int lane = c.lane;
   const LseR lse = lse_fetch(sv_lse, c);   // consumed after the recompute phase (latency hidden by passes 1-2)
   CT dres[MAXRT];
@@ -169,12 +173,14 @@ __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, C
       for (int k = 0; k < MAXRT; ++k) {
         const int rt = c.wave + NW * k;
         if (rt < c.NT) {
+          const CTr alo = ld_g(sv_alo, c.tok0, rt, c.NR, lane);
           CT da;
           ct_zero(da);
           mm(da, Wpb, ld_lds(c.DQ, rt, lane));
           const bool ok = tok_ok(rt, c);
-          st_lds(c.DA, rt, ct_pack(da), ok, lane);
-          attn_delta_ct(ld_lds(c.XB, rt, lane), da, rt, ok, c);
+          const CTr dap = ct_pack(da);
+          st_lds(c.DA, rt, dap, ok, lane);
+          attn_delta_ct(ld_lds(c.XB, rt, lane), alo, dap, rt, ok, c);
         }
       }
     }
@@ -610,8 +616,8 @@ __device__ __forceinline__ void dec_fwd_tile(const DecP& p, char* smem, int seq0
     const Blk& B = p.blk[b];
     Ctx cc = c;
     asm volatile("" : "+v"(cc.lane), "+v"(cc.tid));
-    self_attn_fwd_ct<SAVE>(B.m, B.ln[0], xr, true, p.sv[b].xin, p.sv[b].a1, p.sv[b].lse1, cc);
-    cross_attn_fwd_ct<SAVE>(B.m, B.ln[1], xr, p.rep, p.sv[b].x1, p.sv[b].a2, p.sv[b].lse2, cc);
+    self_attn_fwd_ct<SAVE>(B.m, B.ln[0], xr, true, p.sv[b].xin, p.sv[b].a1, p.sv[b].a1lo, p.sv[b].lse1, cc);
+    cross_attn_fwd_ct<SAVE>(B.m, B.ln[1], xr, p.rep, p.sv[b].x1, p.sv[b].a2, p.sv[b].a2lo, p.sv[b].lse2, cc);
     mlp_fwd_ct<SAVE>(B.m[8], B.m[9], B.ln[2], xr, p.sv[b].x2, p.sv[b].h, cc);
   }
   head_fwd_ct<MA, CONT>(p, xr, SAVE, c);
@@ -647,8 +653,9 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
     Ctx cc = c;
     asm volatile("" : "+v"(cc.lane), "+v"(cc.tid));
     mlp_bwd_ct(B.m[8], B.m[9], B.ln[2], dx, p.sv[bb].x2, p.sv[bb].h, cc);
-    cross_attn_bwd_ct(B.m, B.ln[1], dx, p.rep, p.drep, p.sv[bb].x1, p.sv[bb].a2, p.sv[bb].lse2, bb == NB - 1, cc);
-    self_attn_bwd_ct(B.m, B.ln[0], dx, p.sv[bb].xin, p.sv[bb].a1, p.sv[bb].lse1, true, cc);
+    cross_attn_bwd_ct(B.m, B.ln[1], dx, p.rep, p.drep, p.sv[bb].x1, p.sv[bb].a2, p.sv[bb].a2lo, p.sv[bb].lse2,
+                      bb == NB - 1, cc);
+    self_attn_bwd_ct(B.m, B.ln[0], dx, p.sv[bb].xin, p.sv[bb].a1, p.sv[bb].a1lo, p.sv[bb].lse1, true, cc);
   }
   // ---------------- embedding backward: dW_a[:, token] += d pre ; LN_dec params
   if (!CONT) {

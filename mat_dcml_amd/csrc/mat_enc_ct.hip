@@ -120,7 +120,7 @@ __device__ __forceinline__ void enc_fwd_tile(const EncP& p, const EncX& ex, char
     const Blk& B = p.blk[b];
     Ctx cc = c;   // opaque per-iteration lane id: keeps hipcc from hoisting (and spilling) every LDS address
     asm volatile("" : "+v"(cc.lane), "+v"(cc.tid));
-    self_attn_fwd_ct<SAVE>(B.m, B.ln[0], xr, false, p.sv[b].xin, p.sv[b].a1, p.sv[b].lse1, cc);
+    self_attn_fwd_ct<SAVE>(B.m, B.ln[0], xr, false, p.sv[b].xin, p.sv[b].a1, p.sv[b].a1lo, p.sv[b].lse1, cc);
     mlp_fwd_ct<SAVE>(B.m[8], B.m[9], B.ln[1], xr, p.sv[b].x1, p.sv[b].h, cc);
   }
   // value head: v = W_v2 · LN(GELU(W_v1 · rep + b)) + b   (ma_transformer.py:138-139,152)
@@ -281,7 +281,7 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
     Ctx cc = c;
     asm volatile("" : "+v"(cc.lane), "+v"(cc.tid));
     mlp_bwd_ct(B.m[8], B.m[9], B.ln[1], dx, p.sv[bb].x1, p.sv[bb].h, cc);
-    self_attn_bwd_ct(B.m, B.ln[0], dx, p.sv[bb].xin, p.sv[bb].a1, p.sv[bb].lse1, false, cc);
+    self_attn_bwd_ct(B.m, B.ln[0], dx, p.sv[bb].xin, p.sv[bb].a1, p.sv[bb].a1lo, p.sv[bb].lse1, false, cc);
   }
   // ---------------- embedding backward: x0 = LN0(GELU(pre)), pre = W_e · LN_obs(obs) + b_e
   {

@@ -33,7 +33,10 @@ constexpr int LDS_BUDGET = 160 * 1024 / WGPC;
 struct Mat { const bf16_t* fw; const bf16_t* bw; const float* b; float* dW; float* db; const bf16_t* fa; const bf16_t* ba; };
 struct LNp { const float* g; const float* b; float* dg; float* db; };
 struct Blk { Mat m[10]; LNp ln[3]; };
-struct Sv { bf16_t* xin; bf16_t* a1; float* lse1; bf16_t* x1; bf16_t* a2; float* lse2; bf16_t* x2; bf16_t* h; };
+// saved activations of one block; a1lo / a2lo = the bf16 residual O - bf16(O) of the attention outputs, so the
+// backward's delta = rowsum(dO O) sees O to ~16 significant bits (bf16 O alone put 10-40 % errors on dK / dQ)
+struct Sv { bf16_t* xin; bf16_t* a1; float* lse1; bf16_t* x1; bf16_t* a2; float* lse2; bf16_t* x2; bf16_t* h;
+            bf16_t* a1lo; bf16_t* a2lo; };
 
 struct EncP {
   int Bs, L, od, SQ, NRP, n_obj;
@@ -165,11 +168,13 @@ __device__ __forceinline__ void lse_store(const LseR& r, const Ctx& c) {
   }
 }
 
-// Backward tile start: zero only what no phase rewrites before reading — the padded rows [16 NT, NRP) of the six
-// token-major buffers and of delta.  Rows below 16 NT are always written (zeros for rows >= NR) by the phase that
-// produces them before any phase reads them; LSE is fully rewritten per attention.  (Round 2 zeroed all ~150 KB.)
+// Backward tile start: zero only what no phase rewrites before reading — the rows [NR, NRP) past the chunk's
+// tokens in the six token-major buffers and in delta (a shorter chunk after a longer one would otherwise see the
+// previous chunk's rows there: the tail of its last 16-row tile and the 32-row key chunks read past it).  Rows
+// below NR are always written before they are read; LSE is fully rewritten per attention.  (Round 2 zeroed all
+// ~150 KB per tile.)
 __device__ __forceinline__ void zero_pad_rows(const Ctx& c) {
-  const int r0 = c.NT * 16, nr = c.NRP - r0;
+  const int r0 = c.NR, nr = c.NRP - r0;
   if (nr <= 0) return;
   bf16_t* bufs[6] = {c.QB, c.KB, c.VB, c.DA, c.DQ, c.XB};
   const int per = nr * 8;   // 16-byte pieces per buffer

@@ -549,15 +549,17 @@ __device__ __forceinline__ void st_lds_head(bf16_t* buf, int rt, int h, f32x4 a,
 // delta_q = Σ_k P_qk dP_qk = Σ_d dO_qd O_qd per (query, head) (dP = dO Vᵀ, O = P V): from the saved forward output
 // O and dO in registers (CT layout, both heads) -> DEL [head][row] in LDS.  Replaces a full extra sweep over the keys
 // (scores, exp2 and dP MFMAs) in the query pass.
-__device__ __forceinline__ void attn_delta_ct(const CTr& o, const CT& dO, int rt, bool ok, const Ctx& c) {
-  const CT ov = ct_unpack(o);
+// O = hi + lo (saved bf16 pair); dO as stored in DA (bf16), the same values the dP MFMAs see.
+__device__ __forceinline__ void attn_delta_ct(const CTr& ohi, const CTr& olo, const CTr& dOr, int rt, bool ok,
+                                              const Ctx& c) {
+  const CT oh = ct_unpack(ohi), ol = ct_unpack(olo), dO = ct_unpack(dOr);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     float d = 0.f;
 #pragma unroll
     for (int mt = 2 * h; mt < 2 * h + 2; ++mt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) d += ov.v[mt][r] * dO.v[mt][r];
+      for (int r = 0; r < 4; ++r) d += (oh.v[mt][r] + ol.v[mt][r]) * dO.v[mt][r];
     d = cross_row_sum(d);
     if ((c.lane >> 4) == 0) c.DEL[h * c.NRP + rt * 16 + (c.lane & 15)] = ok ? d : 0.f;
   }
@@ -650,7 +652,7 @@ __device__ __forceinline__ void attn_bwd_kv_ct(const bf16_t* Q, bf16_t* K, bf16_
 // self attention: x <- LN(x + proj(attn(q(x), k(x), v(x))))   (ma_transformer.py:89-92,112)
 template <bool SAVE>
 __device__ __forceinline__ void self_attn_fwd_ct(const Mat* m, const LNp& ln, CT* xr, bool causal, bf16_t* sv_xin,
-                                                 bf16_t* sv_a, float* sv_lse, const Ctx& c) {
+                                                 bf16_t* sv_a, bf16_t* sv_alo, float* sv_lse, const Ctx& c) {
   const int lane = c.lane;
   {
     CTr xp[MAXRT];
@@ -677,8 +679,12 @@ __device__ __forceinline__ void self_attn_fwd_ct(const Mat* m, const LNp& ln, CT
   for (int k = 0; k < MAXRT; ++k) {
     const int rt = c.wave + NW * k;
     if (rt < c.NT) {
-      const CTr a = ct_pack(O[k]);
-      if (SAVE) st_g(sv_a, c.tok0, rt, c.NR, a, lane);
+      CTr a, alo;
+      ct_split(O[k], a, alo);
+      if (SAVE) {
+        st_g(sv_a, c.tok0, rt, c.NR, a, lane);
+        st_g(sv_alo, c.tok0, rt, c.NR, alo, lane);
+      }
       CT t = ct_add(bp, xr[k]), xh;
       mm(t, Wp, a);
       ln_fwd_ct(t, xh, xr[k], gam, bet);
@@ -798,7 +804,8 @@ __device__ __forceinline__ void mlp_bwd_ct(const Mat& m1, const Mat& m2, const L
 // input gradient of the q / k / v projections.  Self: q-input = kv-input = x (sv_xin).  The attention output
 // gradient dO must already be in DA.
 __device__ __forceinline__ void self_attn_bwd_ct(const Mat* m, const LNp& ln, CT* dx, const bf16_t* sv_xin,
-                                                 const bf16_t* sv_a, const float* sv_lse, bool causal, const Ctx& c) {
+                                                 const bf16_t* sv_a, const bf16_t* sv_alo, const float* sv_lse,
+                                                 bool causal, const Ctx& c) {
   const int lane = c.lane;
   const LseR lse = lse_fetch(sv_lse, c);   // consumed after the recompute phase (latency hidden by passes 1-2)
   CTr xin[MAXRT];
@@ -843,12 +850,14 @@ __device__ __forceinline__ void self_attn_bwd_ct(const Mat* m, const LNp& ln, CT
       for (int k = 0; k < MAXRT; ++k) {
         const int rt = c.wave + NW * k;
         if (rt < c.NT) {
+          const CTr alo = ld_g(sv_alo, c.tok0, rt, c.NR, lane);
           CT da;
           ct_zero(da);
           mm(da, Wpb, ld_lds(c.DQ, rt, lane));
           const bool ok = tok_ok(rt, c);
-          st_lds(c.DA, rt, ct_pack(da), ok, lane);
-          attn_delta_ct(ld_lds(c.XB, rt, lane), da, rt, ok, c);
+          const CTr dap = ct_pack(da);
+          st_lds(c.DA, rt, dap, ok, lane);
+          attn_delta_ct(ld_lds(c.XB, rt, lane), alo, dap, rt, ok, c);
         }
       }
     }

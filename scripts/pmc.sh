@@ -8,9 +8,12 @@ grep -oE "(SQ|TCC|TCP|GRBM)_[A-Z0-9_]+" $R/gpurun_out/pmc/list.txt | sort -u > $
 LIBS=${PMC_LIBS:-libmatdcml.so}
 for lib in $LIBS; do
 i=0
-for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT" "SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_BUSY_CYCLES" "TCC_EA0_ATOMIC_sum TCC_HIT_sum TCC_MISS_sum"; do
+PROG=${PMC_PROG:-tests/bench_train_kernels.py}
+SETS=${PMC_SETS:-"SQ_WAVE_CYCLES,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_ACTIVE_INST_ANY SQ_INSTS_VALU,SQ_INSTS_MFMA,SQ_INSTS_LDS,SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS,SQ_INSTS_SALU,SQ_INSTS_VMEM,SQ_BUSY_CYCLES TCC_EA0_ATOMIC_sum,TCC_HIT_sum,TCC_MISS_sum"}
+for set in $SETS; do
+  set=${set//,/ }
   i=$((i+1))
-  MAT_DCML_LIBNAME=$lib timeout -k 10 200 rocprofv3 --pmc $set --output-format csv -d $R/gpurun_out/pmc/$lib/p$i -o run -- python3 $R/tests/bench_train_kernels.py > $R/gpurun_out/pmc/$lib.p$i.log 2>&1 || { echo "pass $i failed rc=$?"; exit 1; }
+  MAT_DCML_LIBNAME=$lib timeout -k 10 200 rocprofv3 --pmc $set --output-format csv -d $R/gpurun_out/pmc/$lib/p$i -o run -- python3 $R/$PROG > $R/gpurun_out/pmc/$lib.p$i.log 2>&1 || { echo "pass $i failed rc=$?"; exit 1; }
 done
 done
 cd $R
