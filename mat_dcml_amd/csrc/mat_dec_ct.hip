@@ -582,7 +582,7 @@ __device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c)
   }
   __syncthreads();
   CP_MARK(1);
-  wgrad_g(c.DA, c.XB, c.NRP, c.g(p.d_wh2), 64, p.A, 64, c.g(p.d_bh2), c.wave, lane);
+  wgrad_g(c.DA, c.XB, c.KP, c.g(p.d_wh2), 64, p.A, 64, c.g(p.d_bh2), c.wave, lane);
   wgrad64(c.DQ, c.KB, p.h1, c);
   __syncthreads();
   CP_MARK(19);
@@ -699,8 +699,8 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
     flush_vec(dlb, c.g(p.d_lnd_b), lane);
     __syncthreads();
     if (p.d_wa) {
-      wgrad_g(c.DA, c.XB, c.NRP, c.g(p.d_wa), p.A + 1, 64, p.A + 1, nullptr, c.wave, lane);
-      wgrad_g(c.DQ, c.XB, c.NRP, c.g(p.d_wa), p.A + 1, 64, p.A + 1, nullptr, c.wave, lane);
+      wgrad_g(c.DA, c.XB, c.KP, c.g(p.d_wa), p.A + 1, 64, p.A + 1, nullptr, c.wave, lane);
+      wgrad_g(c.DQ, c.XB, c.KP, c.g(p.d_wa), p.A + 1, 64, p.A + 1, nullptr, c.wave, lane);
     }
   } else {
     float* EMB = (float*)c.QB;   // [(A+1)][64] f32 accumulators (QB + KB: 2 NRP x 128 B >= 65 x 256 B)

@@ -355,7 +355,7 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
         if (p.d_lno_b) atomicAdd(c.g(p.d_lno_b) + dim, ob);
       }
       __syncthreads();
-      wgrad_g(c.DA, c.XB, c.NRP, c.g(p.d_we), p.od, 64, p.od, nullptr, c.wave, lane);
+      wgrad_g(c.DA, c.XB, c.KP, c.g(p.d_we), p.od, 64, p.od, nullptr, c.wave, lane);
     }
   }
   CP_MARK(30);

@@ -95,7 +95,7 @@ struct DecP {
 };
 
 struct Ctx {
-  int tid, lane, wave, L, nseq, NR, NT, NRP, tok0;
+  int tid, lane, wave, L, nseq, NR, NT, NRP, KP, tok0;   // KP: rows [0, KP) = NR rounded up to 32 (<= NRP)
   ptrdiff_t gofs;   // gradient-copy offset (floats): this block's slice of the 8-way dW workspace, 0 = direct
   __device__ __forceinline__ float* g(float* p) const { return p ? p + gofs : p; }
   bf16_t *QB, *KB, *VB, *DA, *DQ, *XB;
@@ -168,13 +168,13 @@ __device__ __forceinline__ void lse_store(const LseR& r, const Ctx& c) {
   }
 }
 
-// Backward tile start: zero only what no phase rewrites before reading — the rows [NR, NRP) past the chunk's
+// Backward tile start: zero only what no phase rewrites before reading — the rows [NR, KP) past the chunk's
 // tokens in the six token-major buffers and in delta (a shorter chunk after a longer one would otherwise see the
 // previous chunk's rows there: the tail of its last 16-row tile and the 32-row key chunks read past it).  Rows
-// below NR are always written before they are read; LSE is fully rewritten per attention.  (Round 2 zeroed all
-// ~150 KB per tile.)
+// below NR are always written before they are read; LSE is fully rewritten per attention; nothing reads a row at
+// or past KP (32-row key chunks and the weight-gradient K loop stop there).  (Round 2 zeroed all ~150 KB per tile.)
 __device__ __forceinline__ void zero_pad_rows(const Ctx& c) {
-  const int r0 = c.NR, nr = c.NRP - r0;
+  const int r0 = c.NR, nr = c.KP - r0;
   if (nr <= 0) return;
   bf16_t* bufs[6] = {c.QB, c.KB, c.VB, c.DA, c.DQ, c.XB};
   const int per = nr * 8;   // 16-byte pieces per buffer
@@ -202,6 +202,7 @@ __device__ __forceinline__ Ctx make_ctx(const PT& p, char* smem, int seq0, int n
   c.NR = c.nseq * p.L;
   c.NT = (c.NR + 15) >> 4;
   c.NRP = p.NRP;
+  c.KP = min(p.NRP, (c.NR + 31) & ~31);
   c.tok0 = seq0 * p.L;
   // spread the fp32 weight-gradient atomics over g_copies copies (blockIdx % 8 ~ the XCD the block runs on):
   // 8x fewer adders per address than every workgroup hitting the same 16 KB matrix
@@ -222,17 +223,51 @@ __host__ __device__ inline size_t mat_train_lds_bytes(int NRP, int SQ, int L) {
 }
 
 
-// Persistent, balanced tiling: workgroup w owns the contiguous sequence range [Bs*w/G, Bs*(w+1)/G) and walks it in
-// near-equal chunks of <= SQ sequences.  With G = #CUs the makespan is ceil(Bs/G) sequences per CU instead of
-// ceil(Bs/SQ/G) full tiles (640 tiles of 5 on 256 CUs = 3 rounds of 5 -> 13 sequences per CU).
+// Persistent tiling: workgroup w owns the contiguous sequence range [Bs*w/G, Bs*(w+1)/G) and walks it in chunks of
+// <= SQ sequences.  With G = #CUs the makespan is ceil(Bs/G) sequences per CU instead of ceil(Bs/SQ/G) full tiles
+// (640 tiles of 5 on 256 CUs = 3 rounds of 5 -> 13 sequences per CU).
+//
+// Chunk plan: the token-parallel phases run in rounds of NW 16-row tiles (wave w owns tiles w, w + NW, ...), so a
+// chunk costs ceil(NT / NW) rounds plus a fixed per-chunk part (weight-fragment loads, barriers, the per-chunk
+// gradient flushes), MDL_CHUNK_A4 / 4 rounds.  Of: near-equal chunks (fewest chunks), full SQ chunks + a remainder,
+// and near-equal chunks with one more chunk, the cheapest is taken.  L = 33 in the 8-wave backward: 13 sequences
+// were (4, 4, 5) = 9 + 9 + 11 tiles = 6 rounds; (5, 5, 3) = 11 + 11 + 7 tiles = 5 rounds.
+#ifndef MDL_CHUNK_A4
+#define MDL_CHUNK_A4 4
+#endif
+__device__ __forceinline__ int chunk_rounds(int s, int L) {
+  const int nt = (s * L + 15) >> 4;
+  return (nt + NW - 1) / NW;
+}
+// > 0: that many near-equal chunks; < 0: -(number of chunks) of SQ sequences each but the last
+__device__ __forceinline__ int chunk_plan(int n, int SQ, int L) {
+  if (n <= 0) return 0;
+  const int n0 = (n + SQ - 1) / SQ;
+  auto bal = [&](int k) {
+    const int q = n / k, r = n - q * k;
+    return 4 * (r * chunk_rounds(q + 1, L) + (k - r) * chunk_rounds(q, L)) + MDL_CHUNK_A4 * k;
+  };
+  int best = n0, cost = bal(n0);
+  const int cg = 4 * ((n0 - 1) * chunk_rounds(SQ, L) + chunk_rounds(n - (n0 - 1) * SQ, L)) + MDL_CHUNK_A4 * n0;
+  if (cg < cost) { best = -n0; cost = cg; }
+  if (n0 + 1 <= n && bal(n0 + 1) < cost) best = n0 + 1;
+  return best;
+}
 #define FOR_TILES(p, CALL)                                                                         \
   {                                                                                                \
     const long long G_ = gridDim.x, w_ = blockIdx.x;                                               \
     const int lo_ = (int)((long long)(p).Bs * w_ / G_), hi_ = (int)((long long)(p).Bs * (w_ + 1) / G_); \
-    const int n_ = hi_ - lo_, nch_ = (n_ + (p).SQ - 1) / (p).SQ;                                   \
+    const int n_ = hi_ - lo_, plan_ = chunk_plan(n_, (p).SQ, (p).L);                               \
+    const int nch_ = plan_ < 0 ? -plan_ : plan_;                                                   \
     for (int ch_ = 0; ch_ < nch_; ++ch_) {                                                         \
-      const int s0 = lo_ + (int)((long long)n_ * ch_ / nch_);                                      \
-      const int ns = lo_ + (int)((long long)n_ * (ch_ + 1) / nch_) - s0;                           \
+      int s0, ns;                                                                                  \
+      if (plan_ < 0) {                                                                             \
+        s0 = lo_ + ch_ * (p).SQ;                                                                   \
+        ns = min((p).SQ, n_ - ch_ * (p).SQ);                                                       \
+      } else {                                                                                     \
+        s0 = lo_ + (int)((long long)n_ * ch_ / nch_);                                              \
+        ns = lo_ + (int)((long long)n_ * (ch_ + 1) / nch_) - s0;                                   \
+      }                                                                                            \
       if (ch_) __syncthreads();                                                                    \
       CALL;                                                                                        \
     }                                                                                              \

@@ -400,7 +400,7 @@ __device__ __forceinline__ void wgrad_g(const bf16_t* Y, const bf16_t* X, int KP
   }
 }
 __device__ __forceinline__ void wgrad64(const bf16_t* Y, const bf16_t* X, const Mat& m, const Ctx& c) {
-  wgrad_g(Y, X, c.NRP, c.g(m.dW), 64, 64, 64, c.g(m.db), c.wave, c.lane);
+  wgrad_g(Y, X, c.KP, c.g(m.dW), 64, 64, 64, c.g(m.db), c.wave, c.lane);
 }
 
 // q / k / v projections of the packed tiles xp (one weight matrix live at a time) -> QB / KB / VB; m0 = index of

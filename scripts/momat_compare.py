@@ -18,6 +18,10 @@ def published(name):
 
 
 def ours(path, key):
+    if path.endswith(".jsonl"):   # logs/scalars.jsonl: written as the run goes (a run cut at its time limit)
+        rows = [json.loads(line) for line in open(path) if line.strip()]
+        return [(int(r["step"]), float(r["value"])) for r in rows
+                if r["tag"].endswith(key) or r["tag"].split("/")[-1] == key]
     d = json.load(open(path))
     for k, v in d.items():
         if k.endswith(key) or k.split("/")[-1] == key:
@@ -32,6 +36,11 @@ def stats(series):
             "steps": series[-1][0], "logs": len(vals)}
 
 
+def window(series, lo, hi):
+    vals = [v for s, v in series if lo <= s <= hi]
+    return sum(vals) / len(vals) if vals else float("nan")
+
+
 def at(series, step):
     best = min(series, key=lambda sv: abs(sv[0] - step))
     return best[1]
@@ -39,13 +48,14 @@ def at(series, step):
 
 def main(paths):
     pub = {"ct": published("ct"), "payment": published("payment")}
-    print("| run | objective | env steps (logs) | first | final | best | last-1/16 mean | @80k | @400k | @800k |")
-    print("|---|---|---|---|---|---|---|---|---|---|")
+    print("| run | objective | env steps (logs) | first | final | best | last-1/16 mean | @80k | @400k | @800k | "
+          "mean 750k-800k | mean 400k-800k |")
+    print("|---|---|---|---|---|---|---|---|---|---|---|---|")
     for name, ser in pub.items():
         s = stats(ser)
         print(f"| published MOMAT | {name} | {s['steps']} ({s['logs']}) | {s['first']:.3f} | {s['final']:.3f} | "
               f"{s['best']:.3f} | {s['tail_mean']:.3f} | {at(ser, 80000):.3f} | {at(ser, 400000):.3f} | "
-              f"{at(ser, 800000):.3f} |")
+              f"{at(ser, 800000):.3f} | {window(ser, 750000, 800000):.3f} | {window(ser, 400000, 800000):.3f} |")
     for p in paths:
         run = os.path.basename(p).replace("summary_", "").replace(".json", "")
         for name, key in (("ct", "average_step_objective_0"), ("payment", "average_step_objective_1")):
@@ -56,7 +66,7 @@ def main(paths):
             s = stats(ser)
             print(f"| {run} | {name} | {s['steps']} ({s['logs']}) | {s['first']:.3f} | {s['final']:.3f} | "
                   f"{s['best']:.3f} | {s['tail_mean']:.3f} | {at(ser, 80000):.3f} | {at(ser, 400000):.3f} | "
-                  f"{at(ser, 800000):.3f} |")
+                  f"{at(ser, 800000):.3f} | {window(ser, 750000, 800000):.3f} | {window(ser, 400000, 800000):.3f} |")
 
 
 if __name__ == "__main__":
