@@ -233,7 +233,7 @@ __host__ __device__ inline size_t mat_train_lds_bytes(int NRP, int SQ, int L) {
 // and near-equal chunks with one more chunk, the cheapest is taken.  L = 33 in the 8-wave backward: 13 sequences
 // were (4, 4, 5) = 9 + 9 + 11 tiles = 6 rounds; (5, 5, 3) = 11 + 11 + 7 tiles = 5 rounds.
 #ifndef MDL_CHUNK_A4
-#define MDL_CHUNK_A4 4
+#define MDL_CHUNK_A4 8
 #endif
 __device__ __forceinline__ int chunk_rounds(int s, int L) {
   const int nt = (s * L + 15) >> 4;

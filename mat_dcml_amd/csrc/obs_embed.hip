@@ -162,7 +162,7 @@ __global__ __launch_bounds__(256) void obs_embed_bwd_m_kernel(OEArgs a) {
         h32[j] = (uint32_t)h0 | ((uint32_t)h1 << 16);
         l32[j] = (uint32_t)f2bf(xv[2 * j] - bf2f(h0)) | ((uint32_t)f2bf(xv[2 * j + 1] - bf2f(h1)) << 16);
       }
-      const int o = (row << 6) + ((lc ^ swz(row)) << 3);
+      const int o = (row << 6) + ((lc ^ ((row >> 1) & 7)) << 3);
       *(uint4*)(Pt + o) = up;
       *(uint4*)(Xh + o) = uh;
       *(uint4*)(Xl + o) = ul;

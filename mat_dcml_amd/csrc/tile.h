@@ -1,12 +1,8 @@
 // Token-tile MFMA helpers shared by the fused MAT kernels (gfx950): the token-major swizzled LDS layout and its
 // transposed (ds_read_b64_tr_b16) fragment reads.
 //
-// Token-major LDS buffers: [rows][64] bf16, 16-byte chunk c of row r stored at chunk c ^ swz(r), swz(r) = the linear
-// map r1 -> 2, r2 -> 4, r3 -> 5 of row bits 1..3 (found by exhaustive search over the linear XOR maps of row bits 0..4
-// against the bank rules of MICROARCH §LDS): conflict-free for the transposed ds_read_b64_tr_b16 fragment reads
-// (ld_frag_T), the ds_read_b128 row reads (lda_tm) and the permuted-row score reads of the attention; the ds_write_b64
-// CT stores (16 rows, one column piece: 128-B rows put all 16 on 8 bank pairs mod 32) stay at their 2-way minimum.
-// Round 2's (r >> 1) & 7 cost 2-way on all three read kinds (4 extra LDS cycles per 4).
+// Token-major LDS buffers: [rows][64] bf16, 16-byte chunk c of row r stored at chunk c ^ ((r>>1)&7) — the 16 rows
+// read by one ds_read_b128 lane group land on 16 distinct 4-bank groups.
 // RT = one 16x64 f32 register tile in the v_mfma_f32_16x16x32_bf16 C layout: v[ct][r] holds
 // (row 4*(lane>>4) + r, col 16*ct + (lane&15)).
 #pragma once
@@ -21,16 +17,12 @@ __device__ __forceinline__ void rt_zero(RT& t) {
   for (int c = 0; c < 4; ++c) t.v[c] = f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
-__device__ __forceinline__ int swz(int row) {
-  return (((row >> 1) & 3) << 1) ^ ((row & 8) ? 5 : 0);
-}
-
 __device__ __forceinline__ int tmo(int row, int col) {
-  return (row << 6) + ((((col >> 3) ^ swz(row))) << 3) + (col & 7);
+  return (row << 6) + ((((col >> 3) ^ ((row >> 1) & 7))) << 3) + (col & 7);
 }
 
 __device__ __forceinline__ bf16x8 lda_tm(const bf16_t* buf, int row, int lc) {
-  return *(const bf16x8*)(buf + (row << 6) + ((lc ^ swz(row)) << 3));
+  return *(const bf16x8*)(buf + (row << 6) + ((lc ^ ((row >> 1) & 7)) << 3));
 }
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -47,8 +39,8 @@ __device__ __forceinline__ bf16x8 ld_frag_T(const bf16_t* buf, int k0, int n0, i
   const int g = lane >> 4, c = lane & 15, q = c >> 2, p = c & 3;
   const int col = n0 + 4 * p;
   const int r0 = k0 + 8 * g + q, r1 = r0 + 4;
-  const bf16_t* a0 = buf + (r0 << 6) + ((((col >> 3) ^ swz(r0))) << 3) + (col & 7);
-  const bf16_t* a1 = buf + (r1 << 6) + ((((col >> 3) ^ swz(r1))) << 3) + (col & 7);
+  const bf16_t* a0 = buf + (r0 << 6) + ((((col >> 3) ^ ((r0 >> 1) & 7))) << 3) + (col & 7);
+  const bf16_t* a1 = buf + (r1 << 6) + ((((col >> 3) ^ ((r1 >> 1) & 7))) << 3) + (col & 7);
   const s16x4 lo = ld_tr(a0), hi = ld_tr(a1);
   bf16x8 f;
   f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
