@@ -47,6 +47,8 @@ def parse():
                         "(one-shot only if it matches RCCL and is faster at start-up)")
     p.add_argument("--config", default="dcml", choices=["dcml", "smac"],
                    help="dcml: the headline 32-worker DCML config; smac: MAT on the SMAC-shaped 27m_vs_30m stress env")
+    p.add_argument("--rollout_groups", type=int, default=1,
+                   help="env groups of the pipelined rollout (each on its own stream; identical rollout)")
     p.add_argument("--no_eval", action="store_true", help="skip the post-timing eval sweep (ct / payment / latency)")
     p.add_argument("--model_dir", default=None,
                    help="trained checkpoint for the eval block (default: the committed 32-worker run, if it matches)")
@@ -110,7 +112,7 @@ def main():
             "--episode_length", str(a.episode_length), "--lr", "5e-5", "--ppo_epoch", str(a.ppo_epoch),
             "--num_mini_batch", str(a.num_mini_batch), "--gamma", "0.99", "--use_valuenorm", "--use_popart",
             "--entropy_coef", "0.01", "--n_workers", str(a.n_workers), "--kernels", a.kernels, "--dtype", a.dtype,
-            "--seed", "1"]
+            "--seed", "1", "--rollout_groups", str(a.rollout_groups)]
     if a.phases:
         argv.append("--profile_phases")
     args = parse_args(argv, get_config(), warn=False)
@@ -172,6 +174,7 @@ def main():
                        "global_batch": a.envs * n, "seq_len": a.n_workers + 1,
                        "parallelism": f"dp{n}", "envs_per_gpu": a.envs, "episode_length": a.episode_length,
                        "ppo_epoch": a.ppo_epoch, "num_mini_batch": a.num_mini_batch,
+                       "rollout_groups": runner._groups(),
                        "device": torch.cuda.get_device_name(dev) if dev.type == "cuda" else "cpu"},
             "ranks": n, "backend": topo["backend"], "rank_devices": topo["devices"], "hosts": topo["hosts"],
             "kernels": paths, "grad_allreduce": getattr(runner.trainer, "grad_allreduce", topo["backend"]) if n > 1 else None,

@@ -170,6 +170,8 @@ _FRAMEWORK_FLAGS = [
     ("kernels", str, "auto", "auto|hip|torch — fused HIP kernels on GPU (auto) or the PyTorch reference path"),
     ("dtype", str, "bf16", "bf16|fp32 compute dtype (master weights and optimizer state are fp32)"),
     ("train_stride", int, 1, "decision stride for rollouts (1 = exact per-agent sampling, the reference)"),
+    ("rollout_groups", int, 1, "env groups of the rollout, each on its own HIP stream: one group's env step / insert / "
+     "encoder overlap the other groups' decode (SURVEY §2.4); the rollout is identical for any group count"),
     ("eval_stride", int, 2, "batch decision stride for evaluation (dcml_runner.py:320)"),
     ("recompute_gae_every_epoch", "false", T, "recompute next-value/GAE every PPO epoch (reference semantics)"),
     ("results_dir", str, None, "root of results/ (default: ./results)"),

@@ -32,7 +32,8 @@ PER_FILE_FLAGS = {
 
 
 def _flags(src):
-    return FLAGS + PER_FILE_FLAGS.get(os.path.basename(src), [])
+    extra = os.environ.get("MAT_DCML_BWD_FLAGS", "").split() if src.endswith("_bwd.hip") else []   # A/B variants
+    return FLAGS + PER_FILE_FLAGS.get(os.path.basename(src), []) + extra
 
 
 def _sources():

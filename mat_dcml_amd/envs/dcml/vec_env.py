@@ -136,7 +136,44 @@ class DeviceDCMLEnv:
             out = self._step_hip(actions)
         else:
             out = self._step_torch(actions)
+        self._sync_parent()
         return out
+
+    # ------------------------------------------------------------------ env-range views (pipelined rollouts)
+    # per-env state: dim 0 = env.  The step reads / writes only these (plus the shared, read-only tables).
+    _PER_ENV = ("gid", "counter", "task_ctr", "R", "C", "master_pr", "worker_pr", "avail", "n_disable", "arrive", "lw",
+                "rate", "up_rate", "obs", "share", "ava", "preset_idx", "preset_start")
+
+    def group_views(self, G: int):
+        """G envs-range views [g E/G, (g+1) E/G) sharing this env's state, each stepped on its own (the runner's
+        two-group pipelined rollout, SURVEY §2.4: one group's env step overlaps the other group's decode).  Every
+        draw is keyed by the global env id (``gid``), so stepping the views reproduces stepping the whole env.  The
+        HIP step updates the shared storage in place; the torch step rebinds its state tensors, so a view copies
+        them back into the parent's rows after each step (``_sync_parent``)."""
+        import copy
+        assert self.E % G == 0, (self.E, G)
+        n = self.E // G
+        views = []
+        for g in range(G):
+            v = copy.copy(self)
+            for k in ("_out", "last_debug", "last_near_int"):
+                v.__dict__.pop(k, None)
+            v._rows = {k: getattr(self, k)[g * n:(g + 1) * n] for k in self._PER_ENV}
+            for k, t in v._rows.items():
+                setattr(v, k, t)
+            v.E = n
+            views.append(v)
+        return views
+
+    def _sync_parent(self):
+        rows = self.__dict__.get("_rows")
+        if rows is None:
+            return
+        for k, t in rows.items():
+            cur = getattr(self, k)
+            if cur is not t:   # rebound by the torch path: write the new values into the parent's rows
+                t.copy_(cur)
+                setattr(self, k, t)
 
     # ------------------------------------------------------------------ reset
     def _reset(self, mask: torch.Tensor):

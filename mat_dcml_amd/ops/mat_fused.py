@@ -174,6 +174,9 @@ def set_sampling_key(model, seed: int, env0: int = 0):
 def next_draw_key(model):
     """(k0, k1, counter) for the next stochastic decode call; advances the counter.  Without ``set_sampling_key``
     the key comes from torch's CPU generator on first use (torch.manual_seed reproducible)."""
+    held = getattr(model, "_mdl_draw_held", None)
+    if held is not None:   # inside sampling_group(): every env group of one rollout step shares the step's counter
+        return held
     key = getattr(model, "_mdl_draw_key", None)
     if key is None:
         key = [int(x) for x in torch.randint(0, 2 ** 31 - 1, (2,))] + [0]
@@ -181,6 +184,31 @@ def next_draw_key(model):
     k0, k1, c = key
     key[2] = (c + 1) & 0xFFFFFFFF
     return k0, k1, c
+
+
+class sampling_group:
+    """Decode calls of ONE rollout step made per env group (runner ``rollout_groups``): the groups share the
+    step's draw counter (taken once, ``hold``) and each names its first global env id, so the groups' draws are
+    the ones a single call over all envs makes."""
+
+    def __init__(self, model):
+        self.model = model
+        self.env0 = int(getattr(model, "_mdl_env0", 0))
+        self.has_env0 = hasattr(model, "_mdl_env0")
+
+    def hold(self):
+        self.model._mdl_draw_held = None
+        self.model._mdl_draw_held = next_draw_key(self.model)
+
+    def group(self, first_env: int):
+        self.model._mdl_env0 = self.env0 + int(first_env)
+
+    def close(self):
+        self.model._mdl_draw_held = None
+        if self.has_env0:
+            self.model._mdl_env0 = self.env0
+        else:
+            self.model.__dict__.pop("_mdl_env0", None)
 
 
 def decode(model, rep, ava=None, deterministic=False, stride=1, rand=None):

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import os
 import time
+from contextlib import nullcontext as _null
 
 import numpy as np
 import torch
@@ -127,6 +128,9 @@ class DCMLRunner:
     @torch.no_grad()
     def rollout(self):
         self.trainer.prep_rollout()
+        G = self._groups()
+        if G > 1:
+            return self._rollout_groups(G)
         for step in range(self.episode_length):
             with self.timers("decode"):
                 values, actions, logp = self.collect(step)
@@ -137,9 +141,93 @@ class DCMLRunner:
                     self._track(reward, done, delay, pay)
                     self.insert(obs, share, reward, done, ava, values, actions, logp, delay, pay)
 
-    def _insert_fused(self, obs, share, reward, done, ava, values, actions, logp, delay, pay):
+    def _groups(self):
+        """Env groups of the pipelined rollout (``--rollout_groups``): > 1 only where it can overlap anything (HIP
+        env kernels, a CUDA device) and the rollout stays identical (globally keyed sampling noise)."""
+        G = int(getattr(self.all_args, "rollout_groups", 1) or 1)
+        if G <= 1 or self.n_rollout_threads % G or not hasattr(self.envs, "group_views") \
+                or not hasattr(self.policy.transformer, "_mdl_env0"):
+            return 1
+        return G
+
+    def _rollout_groups(self, G):
+        """The rollout as G env groups, each on its own stream (SURVEY §2.4 overlap plan): group g's decode and
+        group g'’s env step / insert / encoder are independent, so the device runs them side by side (the decode
+        of one env per workgroup leaves most of each CU idle on its own).  Each step takes the sampling counter
+        once and every group names its first global env id (``mat_fused.sampling_group``); the env groups are
+        views of the one env (``group_views``), so buffers, env state and statistics equal the 1-group rollout's."""
+        from ..ops import mat_fused
+        b, E = self.buffer, self.n_rollout_threads
+        n = E // G
+        if getattr(self, "_gviews", None) is None or len(self._gviews) != G:
+            self._gviews = self.envs.group_views(G)
+            cuda = self.device.type == "cuda"
+            self._gstreams = [torch.cuda.Stream(self.device) if cuda else None for _ in range(G)]
+            self._gstats = [torch.zeros(4, device=self.device, dtype=torch.float64) for _ in range(G)]
+        streams = self._gstreams
+        cur = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
+        for s in streams:
+            if s is not None:
+                s.wait_stream(cur)
+        sg = mat_fused.sampling_group(self.policy.transformer)
+        try:
+            for step in range(self.episode_length):
+                sg.hold()
+                for g in range(G):
+                    lo, hi = g * n, (g + 1) * n
+                    with torch.cuda.stream(streams[g]) if streams[g] is not None else _null():
+                        sg.group(lo)
+                        values, actions, logp = self.policy.get_actions(
+                            None, b.obs[step][lo:hi], b.available_actions[step][lo:hi], deterministic=False,
+                            stride=self.train_stride)
+                        obs, share, reward, done, delay, pay, ava = self._gviews[g].step(actions)
+                        self._insert_rows(lo, hi, self._gstats[g], obs, share, reward, done, ava, values, actions,
+                                          logp, delay, pay)
+                b.step = (b.step + 1) % b.T
+        finally:
+            sg.close()
+            for s in streams:
+                if s is not None:
+                    cur.wait_stream(s)
+        for st in self._gstats:   # the groups' finished-episode statistics (fixed order)
+            self._done_stats += st
+            st.zero_()
+
+    def _insert_rows(self, lo, hi, stats, obs, share, reward, done, ava, values, actions, logp, delay, pay):
+        """insert of env rows [lo, hi) of the current slot: the fused launch, or the torch ops on row views."""
+        b, t = self.buffer, self.buffer.step
+        if self._insert_fused(obs, share, reward, done, ava, values, actions, logp, delay, pay, rows=(lo, hi),
+                              stats=stats, advance=False):
+            return
+        A = b.A
+        self._ep_reward[lo:hi] += reward
+        self._ep_delay[lo:hi] += delay
+        self._ep_pay[lo:hi] += pay
+        d = done.to(torch.float64)
+        stats += torch.stack([d.sum(), (self._ep_reward[lo:hi].double() * d).sum(),
+                              (self._ep_delay[lo:hi].double() * d).sum(), (self._ep_pay[lo:hi].double() * d).sum()])
+        keep = (~done).float()
+        self._ep_reward[lo:hi] *= keep
+        self._ep_delay[lo:hi] *= keep
+        self._ep_pay[lo:hi] *= keep
+        m = hi - lo
+        b.share_obs[t + 1][lo:hi] = share if share.dim() == 2 else share[:, 0]
+        b.obs[t + 1][lo:hi] = obs
+        b.available_actions[t + 1][lo:hi] = ava
+        b.actions[t][lo:hi] = actions.reshape(b.actions[t][lo:hi].shape)
+        b.action_log_probs[t][lo:hi] = logp.reshape(b.action_log_probs[t][lo:hi].shape)
+        b.value_preds[t][lo:hi] = values.reshape(b.value_preds[t][lo:hi].shape)
+        if b.n_objective == 2:
+            b.rewards[t][lo:hi] = torch.stack([-delay, -pay], -1).view(m, 1, 2).expand(m, A, 2)
+        else:
+            b.rewards[t][lo:hi] = reward.view(m, 1, 1).expand(m, A, 1)
+        b.masks[t + 1][lo:hi] = (~done).float().view(m, 1, 1).expand(m, A, 1)
+
+    def _insert_fused(self, obs, share, reward, done, ava, values, actions, logp, delay, pay, rows=None, stats=None,
+                      advance=True):
         """_track + insert as one HIP launch (ops/kernels.rollout_insert) when every operand is a contiguous f32
-        device tensor of the buffer's slot size; False -> the torch path."""
+        device tensor of the buffer's slot size; False -> the torch path.  ``rows`` = (lo, hi): env rows of one
+        rollout group (their slot rows and episode sums, statistics into ``stats``)."""
         b = self.buffer
         if getattr(self, "_ins_ok", None) is None:
             from ..ops import kernels
@@ -149,9 +237,11 @@ class DCMLRunner:
             return False
         from ..ops import kernels
         t = b.step
+        lo, hi = rows if rows is not None else (0, b.E)
         sh = share if share.dim() == 2 else share[:, 0]
-        pairs = [(sh, b.share_obs[t + 1]), (obs, b.obs[t + 1]), (ava, b.available_actions[t + 1]),
-                 (actions, b.actions[t]), (logp, b.action_log_probs[t]), (values, b.value_preds[t])]
+        pairs = [(sh, b.share_obs[t + 1][lo:hi]), (obs, b.obs[t + 1][lo:hi]),
+                 (ava, b.available_actions[t + 1][lo:hi]), (actions, b.actions[t][lo:hi]),
+                 (logp, b.action_log_probs[t][lo:hi]), (values, b.value_preds[t][lo:hi])]
         for src, dst in pairs:
             if (src.dtype != torch.float32 or src.numel() != dst.numel() or not src.is_contiguous()
                     or not dst.is_contiguous()):
@@ -159,9 +249,11 @@ class DCMLRunner:
         if done.dtype != torch.bool or not b.rewards[t].is_contiguous():
             return False
         kernels.rollout_insert(pairs, reward.contiguous(), delay.contiguous(), pay.contiguous(), done.contiguous(),
-                               b.rewards[t], b.masks[t + 1], self._ep_reward, self._ep_delay, self._ep_pay,
-                               self._done_stats)
-        b.step = (t + 1) % b.T
+                               b.rewards[t][lo:hi], b.masks[t + 1][lo:hi], self._ep_reward[lo:hi],
+                               self._ep_delay[lo:hi], self._ep_pay[lo:hi],
+                               self._done_stats if stats is None else stats)
+        if advance:
+            b.step = (t + 1) % b.T
         return True
 
     def _track(self, reward, done, delay, pay):
