@@ -252,6 +252,20 @@ __device__ __forceinline__ void attention_mfma(const bf16_t* KV, int rowK, int r
   *(uint2*)(xa + 16) = make_uint2(pk2f(o1[0] * il, o1[1] * il), pk2f(o1[2] * il, o1[3] * il));
 }
 
+// inclusive prefix sum over the 64 lanes: DPP row_shr 1, 2, 4, 8 within each 16-lane row (zero fill), then the
+// totals of the lower rows (3 readlanes) — VALU only, no ds_bpermute round trips
+__device__ __forceinline__ float wave_incl_scan(float x, int lane) {
+  x += dppf<0x111>(x);
+  x += dppf<0x112>(x);
+  x += dppf<0x114>(x);
+  x += dppf<0x118>(x);
+  const float t0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 15));
+  const float t1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 31));
+  const float t2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 47));
+  const int r = lane >> 4;
+  return x + ((r >= 1 ? t0 : 0.f) + (r >= 2 ? t1 : 0.f) + (r >= 3 ? t2 : 0.f));
+}
+
 // categorical sample over <= 4 register logits (every lane of the row computes it alike): availability mask,
 // inverse-CDF draw (argmax when deterministic); returns the action, its masked logit and the log-sum-exp
 constexpr int SMALL_AD = 4;
@@ -503,7 +517,13 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
   float* EMB = RN + pad4((size_t)EPW * L * AD);              // [n_tok][64] action-embedding rows (float4 reads)
   float* WH2 = EMB + (size_t)p.n_tok * 64;                   // [AD][64], then bh2 [AD]
   float* QKV0S = WH2 + pad4((size_t)AD * 65);                // [n_tok][3][64] block-0 token table (p.qkv0)
+  float* HW4 = QKV0S + (size_t)p.n_tok * 192;                // wide head: [16][AD] float4 of the folded W_h2
+  float* HGC = HW4 + (size_t)AD * 64;                        //   then G[AD], C[AD]
   const bool stage = p.stage != 0;
+  // wide fused head (one-row discrete passes, 4 < AD <= 64: SMAC's 36 actions): lane a of every wave computes logit a
+  // from the folded LayerNorm (p.hfold) and the wave samples with ballots / a prefix scan — replaces the generic head
+  // phase's per-action loop of 16-lane reductions and its three serial passes over the logits
+  const bool whead = stage && p.hfold != nullptr && !p.cont && AD > SMALL_AD;
   const bool fast0 = p.qkv0 != nullptr && !p.cont && p.stride == 1;   // one row per pass, token inputs
 
   // ---------------------------------------------------------------- one-time loads
@@ -549,6 +569,13 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
     for (int i = tid; i < p.n_tok * 64; i += 256) EMB[i] = p.emb[i];
     for (int i = tid; i < AD * 65; i += 256) WH2[i] = i < AD * 64 ? p.wh2[i] : p.bh2[i - AD * 64];
     if (p.qkv0) for (int i = tid; i < p.n_tok * 192; i += 256) QKV0S[i] = p.qkv0[i];
+    if (whead) {   // transposed: float4 (kq, a) = W'[a][4kq .. 4kq+3], so lane a's reads are consecutive (no conflicts)
+      for (int i = tid; i < AD * 64; i += 256) {
+        const int a = i >> 6, k = i & 63;
+        HW4[((k >> 2) * AD + a) * 4 + (k & 3)] = p.hfold[i];
+      }
+      for (int i = tid; i < 2 * AD; i += 256) HGC[i] = p.hfold[AD * 64 + i];
+    }
   }
   const float* emb = stage ? EMB : p.emb;
   const float* wh2 = stage ? WH2 : p.wh2;
@@ -788,6 +815,56 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
         }
         __syncthreads();
         MDL_PROF_MARK(10);
+      } else if (fast0 && whead && plo < p.n_disc) {
+        float* HX = Q;   // the row's 64 head1 outputs (the head1 staging buffer)
+        {   // J1, every wave: head1 of its 16 columns for the row, GELU -> HX
+          bf16x8 a[2];
+          float xf[16];
+          afrag_ln(S, LNP + (3 * (NB - 1) + 2) * 128, LNP + (3 * (NB - 1) + 2) * 128 + 64, lane, a, xf);
+          const f32x4 acc = mfma2(a, wb[NG - 1], f32x4{0, 0, 0, 0});
+          if (g4 == 0) HX[16 * wave + c16] = gelu_erf(acc[0] + bcol[NG - 1]);
+        }
+        __syncthreads();
+        MDL_PROF_MARK(9);
+        {   // J2, every wave alike (bit-identical): lane a = action a
+          const bool aok = lane < AD;
+          const int ac = aok ? lane : 0;
+          const float4* hx4 = (const float4*)HX;
+          const float4* w4 = (const float4*)HW4;
+          float s1 = 0.f, s2 = 0.f, pa = 0.f;
+#pragma unroll
+          for (int kq = 0; kq < 16; ++kq) {
+            const float4 x = hx4[kq], w = w4[kq * AD + ac];
+            s1 += (x.x + x.y) + (x.z + x.w);
+            s2 += (x.x * x.x + x.y * x.y) + (x.z * x.z + x.w * x.w);
+            pa += (w.x * x.x + w.y * x.y) + (w.z * x.z + w.w * x.w);
+          }
+          const float mean = s1 * (1.f / 64.f);
+          const float rstd = rsqrtf(fmaxf(s2 * (1.f / 64.f) - mean * mean, 0.f) + 1e-5f);
+          const int i = plo;
+          const size_t oi = (size_t)env0 * L + i, li = (size_t)i;
+          const float lg = rstd * (pa - mean * HGC[ac]) + HGC[AD + ac];
+          const float l = aok ? ((p.ava && AVA[li * AD + ac] == 0.f) ? -1e10f : lg) : -INFINITY;
+          const float mx = wave_max(l);
+          int act = __ffsll((unsigned long long)__ballot(l == mx)) - 1;   // first maximum (argmax)
+          const float e = aok ? __expf(l - mx) : 0.f;
+          const float lse = mx + __logf(wave_sum(e));
+          if (!p.deterministic) {   // inverse CDF: the number of actions whose running probability is below u
+            const float cdf = wave_incl_scan(aok ? __expf(l - lse) : 0.f, lane);
+            const float uu = RU[li];
+            act = min((int)__popcll((unsigned long long)__ballot(aok && cdf < uu)), AD - 1);
+          }
+          act = __builtin_amdgcn_readfirstlane(act);
+          const float la = __shfl(l, act, 64);
+          if (wave == 0 && lane == 0) {
+            p.out_a[oi] = (float)act;
+            p.out_lp[oi] = la - lse;
+            PEND[i] = act;
+          }
+          if (g4 == 0 && c16 < 4 && i + 1 < L) write_next_row0(qkv0, emb, 1 + act, i + 1, L, 4 * wave + c16, QT, KV, XR);
+        }
+        __syncthreads();
+        MDL_PROF_MARK(10);
       } else {
       // ---------------- [I] head1: GELU(W_h1 · LN3(S) + b) -> Q (f32 staging)
       {
@@ -840,7 +917,8 @@ MDL_API int mdl_decode_prof_read(unsigned long long* out) {
 #endif
 
 size_t mat_decode_stage_bytes(int epw, int L, int AD, int n_tok) {
-  return ((size_t)epw * L * (64 + 2 * AD + 1) + (size_t)n_tok * (64 + 192) + (size_t)AD * 65) * 4 + 96;   // + padding
+  const size_t wide = AD > SMALL_AD ? (size_t)AD * 66 : 0;   // wide fused head: folded W_h2 (transposed), G, C
+  return ((size_t)epw * L * (64 + 2 * AD + 1) + (size_t)n_tok * (64 + 192) + (size_t)AD * 65 + wide) * 4 + 96;   // + padding
 }
 
 size_t mat_decode_lds_bytes(int NB, int epw, int rmax, int L) {

@@ -136,9 +136,9 @@ def decoder_pack(model):
                 wh2=dec.head[3].weight.detach().float().contiguous(), bh2=dec.head[3].bias.detach().float().contiguous(),
                 stdv=std.contiguous(), n_tok=toks.shape[0], tok_start=tok_start, tok_zero=tok_zero,
                 cont=int(cont or avail), avail=int(avail))
-    if not (cont or avail) and A <= 4:
-        # head LayerNorm folded into the logit GEMV of the fused one-row head: W_h2 diag(gamma), Σ_c W_h2 gamma,
-        # W_h2 beta + b_h2 (csrc/mat_decode.hip DecParams.hfold)
+    if not (cont or avail) and A <= 64:
+        # head LayerNorm folded into the logit GEMV of the fused one-row heads (<= 4 actions: register logits;
+        # <= 64: one action per lane): W_h2 diag(gamma), Σ_c W_h2 gamma, W_h2 beta + b_h2 (DecParams.hfold)
         w2, b2 = dec.head[3].weight.detach().float(), dec.head[3].bias.detach().float()
         gam, bet = dec.head[2].weight.detach().float(), dec.head[2].bias.detach().float()
         w2g = w2 * gam.view(1, -1)
