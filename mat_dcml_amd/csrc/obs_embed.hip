@@ -15,7 +15,7 @@
 
 namespace {
 
-constexpr int OE_TOK = 64;   // tokens per forward workgroup (4 waves x 16)
+constexpr int OE_TOK = 16;   // tokens per forward workgroup (its 4 waves split the k-steps)
 
 struct OEArgs {
   int N, od, KS;               // tokens, obs dim, k-steps of 32 (ceil(od / 32))
@@ -66,16 +66,21 @@ __global__ __launch_bounds__(256) void obs_embed_pack_kernel(OEArgs a) {
   }
 }
 
-// forward: wave w of the block owns tokens t0 + 16w .. +15 (token on lane & 15, features 16mt + 4g + r in registers)
+// forward: one 16-token tile per workgroup, the k-steps dealt round robin to the 4 waves (token on lane & 15,
+// features 16mt + 4g + r in registers), partial sums reduced through LDS in fixed wave order.  Round 2 gave each
+// wave its own 16 tokens and all 41 k-steps of SMAC's 1288-wide rows: the rollout's 864 tokens were 14 workgroups
+// of a 41-step dependent load chain (40 us per call).
 __global__ __launch_bounds__(256) void obs_embed_fwd_kernel(OEArgs a) {
+  __shared__ f32x4 part[3][4][64];
+  __shared__ float pst[3][2][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
-  const int tok = blockIdx.x * OE_TOK + wave * 16 + c;
+  const int tok = blockIdx.x * OE_TOK + c;
   const bool ok = tok < a.N;
   const float* xr = a.x + (size_t)(ok ? tok : 0) * a.od;
   f32x4 acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   float sx = 0.f, sxx = 0.f;
   const bool vec4 = (a.od & 3) == 0;
-  for (int s = 0; s < a.KS; ++s) {
+  for (int s = wave; s < a.KS; s += 4) {
     const int k0 = 32 * s + 8 * g;
     float v[8];
     if (vec4 && k0 + 8 <= a.od) {
@@ -103,6 +108,21 @@ __global__ __launch_bounds__(256) void obs_embed_fwd_kernel(OEArgs a) {
       acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, lo, acc[mt], 0, 0, 0);
     }
   }
+  if (wave > 0) {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) part[wave - 1][mt][lane] = acc[mt];
+    pst[wave - 1][0][lane] = sx;
+    pst[wave - 1][1][lane] = sxx;
+  }
+  __syncthreads();
+  if (wave > 0) return;
+#pragma unroll
+  for (int w = 0; w < 3; ++w) {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) acc[mt] += part[w][mt][lane];
+    sx += pst[w][0][lane];
+    sxx += pst[w][1][lane];
+  }
   sx = cross_row_sum(sx);
   sxx = cross_row_sum(sxx);
   const float mu = sx / (float)a.od;
@@ -128,46 +148,64 @@ __global__ __launch_bounds__(256) void obs_embed_fwd_kernel(OEArgs a) {
 }
 
 // backward step 1: M += Pᵀ x over a token range, for one 64-column block of x.  Token-major swizzled bf16 LDS tiles
-// of 32 tokens (P, x hi, x lo); wave w owns output rows f in [16w, 16w+16); 4 column tiles of 16.
-constexpr int OEB_SPLIT = 16;   // token ranges per column block
+// of 32 tokens (P, x hi, x lo); wave w owns output rows f in [16w, 16w+16); 4 column tiles of 16.  The next tile's
+// global loads (float4 when od % 4 == 0) are issued before this tile's MFMAs; 64 token ranges per column block
+// (SMAC: 21 x 64 = 1,344 workgroups).  Round 2 (16 ranges, scalar loads, no prefetch) ran at ~0.4 TB/s: 628 us.
+constexpr int OEB_SPLIT = 64;   // token ranges per column block
+struct OEBTile { float p[8], x[8]; };
+__device__ __forceinline__ void oeb_load(const OEArgs& a, int t, int t_hi, int col0, OEBTile& T) {
+  const int lc = threadIdx.x & 7;
+  const bool ok = t < t_hi;
+  const int k0 = col0 + 8 * lc;
+  const float rr = ok ? a.stat[2 * (size_t)t + 1] : 0.f;
+  if (ok) {
+    const float4* dp = (const float4*)(a.dpre + (size_t)t * 64 + 8 * lc);
+    const float4 d0 = dp[0], d1 = dp[1];
+    T.p[0] = d0.x * rr; T.p[1] = d0.y * rr; T.p[2] = d0.z * rr; T.p[3] = d0.w * rr;
+    T.p[4] = d1.x * rr; T.p[5] = d1.y * rr; T.p[6] = d1.z * rr; T.p[7] = d1.w * rr;
+    const float* xr = a.x + (size_t)t * a.od;
+    if ((a.od & 3) == 0 && k0 + 8 <= a.od) {
+      const float4 x0 = *(const float4*)(xr + k0), x1 = *(const float4*)(xr + k0 + 4);
+      T.x[0] = x0.x; T.x[1] = x0.y; T.x[2] = x0.z; T.x[3] = x0.w; T.x[4] = x1.x; T.x[5] = x1.y; T.x[6] = x1.z; T.x[7] = x1.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) T.x[j] = k0 + j < a.od ? xr[k0 + j] : 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { T.p[j] = 0.f; T.x[j] = 0.f; }
+  }
+}
 __global__ __launch_bounds__(256) void obs_embed_bwd_m_kernel(OEArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t Pt[32 * 64], Xh[32 * 64], Xl[32 * 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c16 = lane & 15, g = lane >> 4;
   const int col0 = blockIdx.x * 64;
   const int t_lo = (int)((long long)a.N * blockIdx.y / OEB_SPLIT), t_hi = (int)((long long)a.N * (blockIdx.y + 1) / OEB_SPLIT);
+  const int row = threadIdx.x >> 3, lc = threadIdx.x & 7;
+  const int o = (row << 6) + ((lc ^ ((row >> 1) & 7)) << 3);
   RT acc;
   rt_zero(acc);
+  OEBTile T;
+  if (t_lo < t_hi) oeb_load(a, t_lo + row, t_hi, col0, T);
   for (int t0 = t_lo; t0 < t_hi; t0 += 32) {
-    // stage: 32 tokens x 64 values of P = dpre * r and of x (hi / lo); thread -> (row, 8-column chunk)
-    {
-      const int row = threadIdx.x >> 3, lc = threadIdx.x & 7;
-      const int t = t0 + row;
-      const bool ok = t < t_hi;
-      float pv[8], xv[8];
-      const float rr = ok ? a.stat[2 * (size_t)t + 1] : 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        pv[j] = ok ? a.dpre[(size_t)t * 64 + 8 * lc + j] * rr : 0.f;
-        const int k = col0 + 8 * lc + j;
-        xv[j] = (ok && k < a.od) ? a.x[(size_t)t * a.od + k] : 0.f;
-      }
+    {   // stage this tile: 32 tokens x 64 values of P = dpre * r and of x (hi / lo); thread -> (row, 8-column chunk)
       uint4 up, uh, ul;
       uint32_t* p32 = (uint32_t*)&up;
       uint32_t* h32 = (uint32_t*)&uh;
       uint32_t* l32 = (uint32_t*)&ul;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        p32[j] = (uint32_t)f2bf(pv[2 * j]) | ((uint32_t)f2bf(pv[2 * j + 1]) << 16);
-        const uint16_t h0 = f2bf(xv[2 * j]), h1 = f2bf(xv[2 * j + 1]);
+        p32[j] = (uint32_t)f2bf(T.p[2 * j]) | ((uint32_t)f2bf(T.p[2 * j + 1]) << 16);
+        const uint16_t h0 = f2bf(T.x[2 * j]), h1 = f2bf(T.x[2 * j + 1]);
         h32[j] = (uint32_t)h0 | ((uint32_t)h1 << 16);
-        l32[j] = (uint32_t)f2bf(xv[2 * j] - bf2f(h0)) | ((uint32_t)f2bf(xv[2 * j + 1] - bf2f(h1)) << 16);
+        l32[j] = (uint32_t)f2bf(T.x[2 * j] - bf2f(h0)) | ((uint32_t)f2bf(T.x[2 * j + 1] - bf2f(h1)) << 16);
       }
-      const int o = (row << 6) + ((lc ^ ((row >> 1) & 7)) << 3);
       *(uint4*)(Pt + o) = up;
       *(uint4*)(Xh + o) = uh;
       *(uint4*)(Xl + o) = ul;
     }
     __syncthreads();
+    if (t0 + 32 < t_hi) oeb_load(a, t0 + 32 + row, t_hi, col0, T);   // next tile in flight under the MFMAs
     const bf16x8 pa = ld_frag_T(Pt, 0, 16 * wave, lane);
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) {

@@ -74,7 +74,12 @@ __device__ __forceinline__ float u01f(uint32_t u) { return (float)u01_open(u); }
 __device__ __forceinline__ float dir_x(int k) { return k == 2 ? 1.f : (k == 3 ? -1.f : 0.f); }   // N, S, E, W
 __device__ __forceinline__ float dir_y(int k) { return k == 0 ? 1.f : (k == 1 ? -1.f : 0.f); }
 
-__global__ __launch_bounds__(SM_THREADS) void smac_env_kernel(SmacCfg c, SmacState s, SmacOut o) {
+// grid (E, P): the P workgroups of env e each run the (cheap, deterministic) step on their own LDS copy of the env
+// and build 1/P of its observation / state / availability rows (SMAC 27m_vs_30m: 27 x (1288 + 1458 + 36) values per
+// env — one workgroup per env left 224 of 256 CUs idle at 32 envs: 81 us per step).  The state is read from `s` and
+// written, by workgroup 0 of each env only, to the other copy `so` (ping-pong, swapped by the host), so no
+// workgroup can see a half-updated env.
+__global__ __launch_bounds__(SM_THREADS) void smac_env_kernel(SmacCfg c, SmacState s, SmacState so, SmacOut o) {
   __shared__ float ax[SM_MAXU], ay[SM_MAXU], ah[SM_MAXU], ex[SM_MAXU], ey[SM_MAXU], eh[SM_MAXU];
   __shared__ int nhit[SM_MAXU], ahit[SM_MAXU];   // hit counts: damage = count x per-hit damage, one rounding
   __shared__ float dealt[SM_MAXU];
@@ -82,6 +87,9 @@ __global__ __launch_bounds__(SM_THREADS) void smac_env_kernel(SmacCfg c, SmacSta
   __shared__ uint32_t keys[SM_MAXU];
   __shared__ int s_reset;
   const int e = blockIdx.x, tid = threadIdx.x, A = c.A, N = c.N;
+  const int part = blockIdx.y, P = gridDim.y;
+  const bool lead = part == 0;   // writes the state and the per-env outputs
+  __shared__ long long s_t, s_ctr;
   const uint32_t g = (uint32_t)s.gid[e];
   if (tid < A) {
     ax[tid] = s.apos[((size_t)e * A + tid) * 2];
@@ -96,7 +104,11 @@ __global__ __launch_bounds__(SM_THREADS) void smac_env_kernel(SmacCfg c, SmacSta
     eh[tid] = s.ehp[(size_t)e * N + tid];
   }
   if (tid < SM_MAXU) { nhit[tid] = 0; ahit[tid] = 0; dealt[tid] = 0.f; }
-  if (tid == 0) s_reset = c.mode == 1;
+  if (tid == 0) {
+    s_reset = c.mode == 1;
+    s_t = s.t[e];
+    s_ctr = s.ep_ctr[e];
+  }
   __syncthreads();
   if (c.mode == 0) {
     // ---- actions of the policy rows -> agents; dead agents no-op
@@ -166,32 +178,37 @@ __global__ __launch_bounds__(SM_THREADS) void smac_env_kernel(SmacCfg c, SmacSta
         sum_dealt = __fadd_rn(sum_dealt, dealt[j]);
       }
       for (int i = 0; i < A; ++i) a_alive += ah[i] > 0.f;
-      const long long t = s.t[e] + 1;
+      const long long t = s_t + 1;
       const bool won = e_alive == 0;
       const bool lost = a_alive == 0 && !won;
       const bool tout = t >= c.limit && !won && !lost;
       const bool done = won || lost || tout;
       const float rw = __fadd_rn(__fadd_rn(sum_dealt, __fmul_rn(10.f, (float)kills)), won ? 200.f : 0.f);
-      o.reward[e] = __fmul_rn(rw, c.inv_reward_scale);
-      o.won[e] = won;
-      o.lost[e] = lost;
-      o.timeout[e] = tout;
-      o.dead_allies[e] = (float)(A - a_alive);
-      o.dead_enemies[e] = (float)(N - e_alive);
       const float bg = s.battles_game[e] + (done ? 1.f : 0.f), bw = s.battles_won[e] + (won ? 1.f : 0.f);
-      s.battles_game[e] = bg;
-      s.battles_won[e] = bw;
-      o.battles_game_out[e] = bg;
-      o.battles_won_out[e] = bw;
-      s.t[e] = t;
+      if (lead) {
+        o.reward[e] = __fmul_rn(rw, c.inv_reward_scale);
+        o.won[e] = won;
+        o.lost[e] = lost;
+        o.timeout[e] = tout;
+        o.dead_allies[e] = (float)(A - a_alive);
+        o.dead_enemies[e] = (float)(N - e_alive);
+        so.battles_game[e] = bg;
+        so.battles_won[e] = bw;
+        o.battles_game_out[e] = bg;
+        o.battles_won_out[e] = bw;
+      }
+      s_t = t;
       s_reset = done;
     }
     __syncthreads();
-    if (tid < A) o.dones[(size_t)e * A + tid] = s_reset || !(ah[c.rao ? prm[tid] : tid] > 0.f);
+    if (lead && tid < A) o.dones[(size_t)e * A + tid] = s_reset || !(ah[c.rao ? prm[tid] : tid] > 0.f);
+  } else if (lead && tid == 0) {   // reset of every env: the counters carry over
+    so.battles_game[e] = s.battles_game[e];
+    so.battles_won[e] = s.battles_won[e];
   }
   // ---- battle reset (new unit positions, full hp, fresh agent order)
   if (s_reset) {
-    const uint32_t ctr = (uint32_t)s.ep_ctr[e];
+    const uint32_t ctr = (uint32_t)s_ctr;
     if (tid < A) {
       const u4 r = philox4x32_10(ctr, g, (uint32_t)tid, P_SMAC, c.k0, c.k1);
       ax[tid] = __fadd_rn(8.f, __fmul_rn(3.f, u01f(r.x)));
@@ -213,29 +230,35 @@ __global__ __launch_bounds__(SM_THREADS) void smac_env_kernel(SmacCfg c, SmacSta
       prm[rank] = tid;
     }
     if (tid == 0) {
-      s.t[e] = 0;
-      s.ep_ctr[e] = (int64_t)ctr + 1;
+      s_t = 0;
+      s_ctr = (long long)ctr + 1;
     }
   }
   __syncthreads();
-  // ---- write back the state
-  if (tid < A) {
-    s.apos[((size_t)e * A + tid) * 2] = ax[tid];
-    s.apos[((size_t)e * A + tid) * 2 + 1] = ay[tid];
-    s.ahp[(size_t)e * A + tid] = ah[tid];
-    s.last[(size_t)e * A + tid] = lst[tid];
-    s.perm[(size_t)e * A + tid] = prm[tid];
-  }
-  if (tid < N) {
-    s.epos[((size_t)e * N + tid) * 2] = ex[tid];
-    s.epos[((size_t)e * N + tid) * 2 + 1] = ey[tid];
-    s.ehp[(size_t)e * N + tid] = eh[tid];
+  // ---- write back the state (the other copy; workgroup 0 of the env)
+  if (lead) {
+    if (tid < A) {
+      so.apos[((size_t)e * A + tid) * 2] = ax[tid];
+      so.apos[((size_t)e * A + tid) * 2 + 1] = ay[tid];
+      so.ahp[(size_t)e * A + tid] = ah[tid];
+      so.last[(size_t)e * A + tid] = lst[tid];
+      so.perm[(size_t)e * A + tid] = prm[tid];
+    }
+    if (tid < N) {
+      so.epos[((size_t)e * N + tid) * 2] = ex[tid];
+      so.epos[((size_t)e * N + tid) * 2 + 1] = ey[tid];
+      so.ehp[(size_t)e * N + tid] = eh[tid];
+    }
+    if (tid == 0) {
+      so.t[e] = s_t;
+      so.ep_ctr[e] = s_ctr;
+    }
   }
   // ---- observations (StarCraft2_Env.get_obs_agent layout with the map's unit-type bits)
   const int u = c.u, nA = c.nA;
   const int EF = 5 + u, AF = 5 + u + nA, OF = 5 + u + nA;
   const int o_e = 4, o_a = o_e + N * EF, o_o = o_a + (A - 1) * AF, o_i = o_o + OF;
-  for (int x = tid; x < A * c.obs_dim; x += SM_THREADS) {
+  for (int x = part * SM_THREADS + tid; x < A * c.obs_dim; x += P * SM_THREADS) {
     const int j = x / c.obs_dim, f = x - j * c.obs_dim;
     const int i = c.rao ? prm[j] : j;
     const float al = ah[i] > 0.f ? 1.f : 0.f;
@@ -287,7 +310,7 @@ __global__ __launch_bounds__(SM_THREADS) void smac_env_kernel(SmacCfg c, SmacSta
   // ---- per-agent state (get_state_agent layout: absolute positions per entity, centre offsets for the agent)
   const int SE = 8 + u, SA = 8 + u + nA, SO = 7 + u + nA;
   const int s_e = 4, s_a = s_e + N * SE, s_o = s_a + (A - 1) * SA, s_i = s_o + SO;
-  for (int x = tid; x < A * c.state_dim; x += SM_THREADS) {
+  for (int x = part * SM_THREADS + tid; x < A * c.state_dim; x += P * SM_THREADS) {
     const int j = x / c.state_dim, f = x - j * c.state_dim;
     const int i = c.rao ? prm[j] : j;
     const float al = ah[i] > 0.f ? 1.f : 0.f;
@@ -339,7 +362,7 @@ __global__ __launch_bounds__(SM_THREADS) void smac_env_kernel(SmacCfg c, SmacSta
     o.state[(size_t)e * A * c.state_dim + x] = v;
   }
   // ---- availability (get_avail_agent_actions): dead -> no-op only
-  for (int x = tid; x < A * nA; x += SM_THREADS) {
+  for (int x = part * SM_THREADS + tid; x < A * nA; x += P * SM_THREADS) {
     const int j = x / nA, q = x - j * nA;
     const int i = c.rao ? prm[j] : j;
     const float al = ah[i] > 0.f ? 1.f : 0.f;
@@ -361,12 +384,19 @@ __global__ __launch_bounds__(SM_THREADS) void smac_env_kernel(SmacCfg c, SmacSta
 
 }  // namespace
 
-MDL_API int mdl_smac_env(const SmacCfg* c, const SmacState* s, const SmacOut* o, hipStream_t st) {
+MDL_API int mdl_smac_env(const SmacCfg* c, const SmacState* s, const SmacState* so, const SmacOut* o, hipStream_t st) {
   if (c->A < 1 || c->A > SM_MAXU || c->N < 1 || c->N > SM_MAXU || c->nA != 6 + c->N || c->E < 1) return -1;
   if (c->obs_dim != 4 + c->N * (5 + c->u) + (c->A - 1) * (5 + c->u + c->nA) + (5 + c->u + c->nA) + c->A) return -2;
   if (c->state_dim != 4 + c->N * (8 + c->u) + (c->A - 1) * (8 + c->u + c->nA) + (7 + c->u + c->nA) + c->A) return -2;
   if (c->mode == 0 && !o->actions) return -1;
-  hipLaunchKernelGGL(smac_env_kernel, dim3(c->E), dim3(SM_THREADS), 0, st, *c, *s, *o);
+  // workgroups per env: enough for ~2 per CU of a 256-CU device, each with at least one thread per 4 of its values
+  const int work = c->A * (c->obs_dim + c->state_dim + c->nA);
+  int P = (512 + c->E - 1) / c->E;
+  P = P < 1 ? 1 : P;
+  const int pmax = (work + 4 * SM_THREADS - 1) / (4 * SM_THREADS);
+  P = P > pmax ? pmax : P;
+  P = P < 1 ? 1 : (P > 16 ? 16 : P);
+  hipLaunchKernelGGL(smac_env_kernel, dim3(c->E, P), dim3(SM_THREADS), 0, st, *c, *s, *so, *o);
   MDL_CHECK_LAUNCH();
   return 0;
 }

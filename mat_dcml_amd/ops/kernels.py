@@ -240,6 +240,34 @@ def rollout_insert(copies, reward, delay, pay, done, rew_slot, mask_slot, ep_r, 
     check(lib().mdl_rollout_insert(ctypes.byref(a), _stream()), "rollout_insert")
 
 
+class SmacInsArgs(ctypes.Structure):
+    _fields_ = [("seg", InsSeg * 6), ("E", ctypes.c_int), ("A", ctypes.c_int)] + \
+               [(n, ctypes.c_void_p) for n in ("reward", "dones", "won", "dead", "d_rew", "d_mask", "d_active", "ep_r",
+                                               "stats")]
+
+
+sig("mdl_smac_insert", ctypes.POINTER(SmacInsArgs), vp)
+
+
+def smac_insert(copies, reward, dones, won, dead, rew_slot, mask_slot, active_slot, ep_r, stats):
+    """One launch: the SMAC runner's _track_smac + _insert_smac (csrc/rl_ops.hip smac_insert_kernel)."""
+    a = SmacInsArgs()
+    for k, (src, dst) in enumerate(copies):
+        assert src.dtype == dst.dtype == torch.float32 and src.numel() == dst.numel()
+        assert src.is_contiguous() and dst.is_contiguous()
+        a.seg[k] = InsSeg(src.data_ptr(), dst.data_ptr(), src.numel())
+    E, A = dones.shape
+    a.E, a.A = E, A
+    for n, t in (("reward", reward), ("dones", dones), ("won", won), ("dead", dead), ("d_rew", rew_slot),
+                 ("d_mask", mask_slot), ("d_active", active_slot), ("ep_r", ep_r), ("stats", stats)):
+        assert t.is_contiguous(), n
+        setattr(a, n, t.data_ptr())
+    assert dones.dtype == torch.bool and won.dtype == torch.bool and stats.dtype == torch.float64
+    assert reward.numel() == E and rew_slot.numel() == E * A and mask_slot.numel() == E * A
+    assert active_slot.numel() == E * A and dead.dtype == torch.float32 and ep_r.numel() == E
+    check(lib().mdl_smac_insert(ctypes.byref(a), _stream()), "smac_insert")
+
+
 # ----------------------------------------------------------------------------------------- DCML env
 class EnvCfg(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in ("E", "W", "A", "P", "obs_dim", "share_dim", "fixed", "preset",
@@ -352,7 +380,7 @@ class SmacOut(ctypes.Structure):
                                                "battles_game_out")]
 
 
-sig("mdl_smac_env", ctypes.POINTER(SmacCfg), ctypes.POINTER(SmacState), ctypes.POINTER(SmacOut), vp)
+sig("mdl_smac_env", ctypes.POINTER(SmacCfg), ctypes.POINTER(SmacState), ctypes.POINTER(SmacState), ctypes.POINTER(SmacOut), vp)
 
 
 def smac_env(env, actions):
@@ -371,8 +399,13 @@ def smac_env(env, actions):
     c = SmacCfg(E=E, A=A, N=N, nA=env.n_actions, u=sp.unit_type_bits, limit=sp.limit, obs_dim=sp.obs_dim,
                 state_dim=sp.state_dim, rao=int(env.random_agent_order), mode=0 if actions is not None else 1,
                 k0=env.k0, k1=env.k1, inv_reward_scale=1.0 / env.reward_scale)
-    s = SmacState(*[getattr(env, n).data_ptr() for n in ("gid", "ep_ctr", "apos", "ahp", "epos", "ehp", "t", "last",
-                                                        "battles_won", "battles_game", "perm")])
+    names = ("gid", "ep_ctr", "apos", "ahp", "epos", "ehp", "t", "last", "battles_won", "battles_game", "perm")
+    # ping-pong state: the kernel reads the env's tensors and writes the spare copy, which then becomes the env's
+    spare = getattr(env, "_smac_spare", None)
+    if spare is None or any(spare[n].shape != getattr(env, n).shape for n in names[1:]):
+        spare = env._smac_spare = {n: torch.empty_like(getattr(env, n)) for n in names[1:]}
+    s = SmacState(*[getattr(env, n).data_ptr() for n in names])
+    so = SmacState(env.gid.data_ptr(), *[spare[n].data_ptr() for n in names[1:]])
     f32 = dict(device=dev, dtype=torch.float32)
     obs = torch.empty(E, A, sp.obs_dim, **f32)
     state = torch.empty(E, A, sp.state_dim, **f32)
@@ -388,7 +421,12 @@ def smac_env(env, actions):
     o = SmacOut(act.data_ptr() if act is not None else None, obs.data_ptr(), state.data_ptr(), ava.data_ptr(),
                 reward.data_ptr(), dones.data_ptr(), flags[0].data_ptr(), flags[1].data_ptr(), flags[2].data_ptr(),
                 scal[0].data_ptr(), scal[1].data_ptr(), scal[2].data_ptr(), scal[3].data_ptr())
-    check(lib().mdl_smac_env(ctypes.byref(c), ctypes.byref(s), ctypes.byref(o), _stream()), "smac_env")
+    check(lib().mdl_smac_env(ctypes.byref(c), ctypes.byref(s), ctypes.byref(so), ctypes.byref(o), _stream()),
+          "smac_env")
+    for n in names[1:]:
+        cur = getattr(env, n)
+        setattr(env, n, spare[n])
+        spare[n] = cur
     info = {"won": flags[0], "lost": flags[1], "bad_transition": flags[2], "battles_won": scal[2],
             "battles_game": scal[3], "dead_allies": scal[0], "dead_enemies": scal[1]}
     return obs, state, ava, reward, dones, info

@@ -70,6 +70,8 @@ class SMACRunner(DCMLRunner):
         self.policy = TransformerPolicy(a, [obs_dim], [share_dim], act_space, self.num_agents, device=self.device)
         self.comm.broadcast_module_(self.policy.transformer)
         self.comm.seed_sampling_rng(a.seed)
+        from ..ops import mat_fused   # exploration noise keyed by the global env id, as the DCML runner
+        mat_fused.set_sampling_key(self.policy.transformer, a.seed, env0=rank * E)
         self.comm.attach_flat_grads(self.policy.transformer.parameters())
         self.trainer = MATTrainer(a, self.policy, self.num_agents, device=self.device, comm=self.comm)
         pol = self.policy
@@ -108,9 +110,36 @@ class SMACRunner(DCMLRunner):
             with self.timers("env"):
                 obs, state, reward, dones, info, ava = self.envs.step(actions)
             with self.timers("insert"):
-                self._track_smac(reward, dones, info)
-                self._insert_smac(obs, reward, dones, ava, values, actions, logp)
+                if not self._insert_fused(obs, reward, dones, info, ava, values, actions, logp):
+                    self._track_smac(reward, dones, info)
+                    self._insert_smac(obs, reward, dones, ava, values, actions, logp)
         self._info = info
+
+    def _insert_fused(self, obs, reward, dones, info, ava, values, actions, logp):
+        """_track_smac + _insert_smac as one HIP launch (ops/kernels.smac_insert) on the device path; False -> torch."""
+        b = self.buffer
+        if getattr(self, "_ins_ok", None) is None:
+            from ..ops import kernels
+            self._ins_ok = self.device.type == "cuda" and kernels.available()
+        if not self._ins_ok:
+            return False
+        from ..ops import kernels
+        t, E, A = b.step, b.E, b.A
+        pairs = [(obs, b.obs[t + 1]), (ava, b.available_actions[t + 1]), (actions, b.actions[t]),
+                 (logp, b.action_log_probs[t]), (values, b.value_preds[t])]
+        r = reward.reshape(E, -1)[:, 0]
+        won, dead = info["won"], info["dead_allies"]
+        for src, dst in pairs:
+            if (src.dtype != torch.float32 or src.numel() != dst.numel() or not src.is_contiguous()
+                    or not dst.is_contiguous()):
+                return False
+        if (dones.dtype != torch.bool or won.dtype != torch.bool or dead.dtype != torch.float32
+                or b.rewards.shape[-1] != 1 or not r.is_contiguous()):
+            return False
+        kernels.smac_insert(pairs, r, dones.contiguous(), won.contiguous(), dead.contiguous(), b.rewards[t],
+                            b.masks[t + 1], b.active_masks[t + 1], self._ep_reward, self._done_stats)
+        b.step = (t + 1) % b.T
+        return True
 
     def _track_smac(self, reward, dones, info):
         E = reward.shape[0]

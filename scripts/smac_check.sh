@@ -4,7 +4,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_train.py tests/test_gpu_ppo.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/smac_tests.log 2>&1; rc=$?
+timeout -k 10 300 python -u -m pytest tests/test_gpu_train.py tests/test_gpu_ppo.py tests/test_gpu_rl_ops.py tests/test_gpu_decode.py tests/test_gpu_smac_env.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/smac_tests.log 2>&1; rc=$?
 grep -E "FAILED|Error|assert" gpurun_out/smac_tests.log | head -20; tail -2 gpurun_out/smac_tests.log
 [ $rc -ne 0 ] && exit 1
 timeout -k 10 300 python -u bench.py --config smac --steps 3 --warmup 1 > gpurun_out/bench_smac.log 2>&1 || { tail -20 gpurun_out/bench_smac.log; exit 2; }

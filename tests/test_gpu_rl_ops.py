@@ -107,8 +107,10 @@ def test_masked_sums_and_gather_match_torch(gpu):
     act = torch.randn(T * E, A, 1, device=gpu, generator=g)
     adv_f = adv.reshape(T * E, A, 1)
     idx = torch.randperm(T * E, device=gpu, generator=g)[:800]
-    out = kernels.gather_rows({"obs": obs, "actions": act, "adv": adv_f}, idx, sums, ("adv",))
+    wide = torch.randn(T * E, A, 12, device=gpu, generator=g)   # row width % 4 == 0: the float4 path
+    out = kernels.gather_rows({"obs": obs, "actions": act, "adv": adv_f, "wide": wide}, idx, sums, ("adv",))
     assert torch.equal(out["obs"], obs[idx]) and torch.equal(out["actions"], act[idx])
+    assert torch.equal(out["wide"], wide[idx])
     norm = rl_ops.normalize_from_sums(adv, ref).reshape(T * E, A, 1)[idx]
     torch.testing.assert_close(out["adv"], norm, rtol=1e-6, atol=1e-6)
 

@@ -72,3 +72,36 @@ def test_smac_env_kernel_is_one_launch_and_fast(gpu):
     us = s.elapsed_time(e) / 20 * 1e3
     print(f"smac env step, 32 envs x 27 agents (obs 1288, state 1458): {us:.1f} us")
     assert us < 200
+
+
+def _smac_runner(gpu, envs=8, T=6):
+    from mat_dcml_amd.config import _SMAC_FLAGS, get_config, parse_args
+    from mat_dcml_amd.runner.smac_runner import SMACRunner
+    argv = ["--env_name", "StarCraft2", "--algorithm_name", "mat", "--map_name", "27m_vs_30m", "--n_rollout_threads",
+            str(envs), "--episode_length", str(T), "--use_value_active_masks", "--seed", "2"]
+    args = parse_args(argv, get_config(), extra=_SMAC_FLAGS, warn=False)
+    r = SMACRunner({"all_args": args, "device": gpu, "run_dir": None})
+    from mat_dcml_amd.ops import mat_fused
+    mat_fused.set_sampling_key(r.policy.transformer, 2, env0=0)   # the same exploration draws in both runners
+    r.warmup()
+    return r
+
+
+def test_smac_fused_insert_matches_torch_insert(gpu):
+    """runner/smac_runner._insert_fused (one launch, csrc/rl_ops.hip smac_insert_kernel) vs the torch _track_smac +
+    _insert_smac on the same rollout: identical buffers (rewards, masks, active masks, slots) and episode statistics."""
+    fused, ref = _smac_runner(gpu), _smac_runner(gpu)
+    ref._ins_ok = False
+    for _ in range(3):   # battles finish within the episode (limit) so the done / active branches are exercised
+        fused.rollout()
+        ref.rollout()
+        fused.buffer.after_update()
+        ref.buffer.after_update()
+    torch.cuda.synchronize()
+    assert fused._ins_ok
+    for k in ("obs", "available_actions", "actions", "action_log_probs", "value_preds", "rewards", "masks",
+              "active_masks"):
+        a, b = getattr(fused.buffer, k), getattr(ref.buffer, k)
+        assert torch.equal(a, b), (k, (a - b).abs().max())
+    assert torch.equal(fused._ep_reward, ref._ep_reward)
+    torch.testing.assert_close(fused._done_stats, ref._done_stats, rtol=1e-12, atol=1e-9)
