@@ -264,6 +264,16 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(GatherArgs a) {
     sd = (float)sqrt(var) + a.eps;
   }
   const int w = e.width;
+  if (w < 1024) {   // narrow rows (DCML: 33 x 7): one flat element loop over the whole minibatch (coalesced across rows)
+    const int total = a.rows * w;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+      const int r = i / w, c = i - r * w;
+      float v = e.src[(size_t)a.idx[r] * w + c];
+      if (e.norm) v = (v - mean) / sd;
+      e.dst[i] = v;
+    }
+    return;
+  }
   const bool vec = (w & 3) == 0 && ((reinterpret_cast<uintptr_t>(e.src) | reinterpret_cast<uintptr_t>(e.dst)) & 15) == 0;
   // work item = (row, 4096-float chunk of the row): 16 floats per lane, the 4 float4 loads issued before the stores
   const int nch = (w + GATHER_CHUNK - 1) / GATHER_CHUNK;
@@ -305,10 +315,12 @@ MDL_API int mdl_gather_rows(const GatherArgs* a, hipStream_t s) {
   for (int k = 0; k < a->n; ++k)
     if (a->e[k].width < 1 || (long long)a->rows * a->e[k].width >= (1ll << 31)) return -2;
   if (a->rows == 0) return 0;
-  long long items = 0;
-  for (int k = 0; k < a->n; ++k)
-    items = std::max(items, (long long)a->rows * ((a->e[k].width + GATHER_CHUNK - 1) / GATHER_CHUNK));
-  const int gx = (int)(items < 8192 ? items : 8192);
+  long long items = 0;   // wide rows: (row, chunk) items; narrow rows: 256-element blocks of the flat loop
+  for (int k = 0; k < a->n; ++k) {
+    const long long w = a->e[k].width;
+    items = std::max(items, w < 1024 ? ((long long)a->rows * w + 255) / 256 : (long long)a->rows * ((w + GATHER_CHUNK - 1) / GATHER_CHUNK));
+  }
+  const int gx = (int)(items < 1 ? 1 : (items < 8192 ? items : 8192));
   hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)gx, a->n), dim3(256), 0, s, *a);
   MDL_CHECK_LAUNCH();
   return 0;

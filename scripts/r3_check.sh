@@ -1,27 +1,16 @@
 #!/bin/bash
-# Round-3 check: every GPU test, the default bench, the SMAC bench, kernel stats of both.
+# Round-3 check: every GPU test, smoke(), default bench (with eval block), kernel stats, A/B of library variants.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 150 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_all.txt 2>&1; rc=$?
-tail -4 gpurun_out/gpu_all.txt
-[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit 1
-timeout -k 10 300 python -u bench.py > gpurun_out/bench.log 2>&1 || { tail -20 gpurun_out/bench.log; exit 2; }
-grep "^{" gpurun_out/bench.log | cut -c1-300
-timeout -k 10 300 python -u bench.py --config smac --steps 5 --warmup 2 > gpurun_out/bench_smac.log 2>&1 || { tail -20 gpurun_out/bench_smac.log; exit 3; }
-grep "^{" gpurun_out/bench_smac.log | cut -c1-300
-for cfg in dcml smac; do
-  rm -rf gpurun_out/prof_$cfg
-  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_$cfg -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --config $cfg --steps 3 --warmup 1 > $GRAFT_REPO_ROOT/gpurun_out/prof_$cfg.log 2>&1) || { tail -20 gpurun_out/prof_$cfg.log; exit 4; }
-  f=$(find gpurun_out/prof_$cfg -name "*kernel_stats.csv" | head -1)
-  cp "$f" gpurun_out/kernel_stats_$cfg.csv
-  find gpurun_out/prof_$cfg -name "*kernel_trace.csv" -delete
-  python3 - $cfg <<'PY'
-import csv, sys
-rows = list(csv.DictReader(open(f"gpurun_out/kernel_stats_{sys.argv[1]}.csv")))
-print("==", sys.argv[1])
-for r in rows[:10]:
-    print(f"{float(r['AverageNs'])/1e3:9.1f} us avg {int(r['Calls']):6d} calls  {r['Name'][:90]}")
-PY
-done
+rm -f gpurun_out/ct_ab.txt
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -v -s --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1 || { grep -E "FAILED|Error" gpurun_out/pytest_gpu.log | head; tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+tail -1 gpurun_out/pytest_gpu.log
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 2; }
+tail -1 gpurun_out/smoke.log | cut -c1-200
+timeout -k 10 300 python -u bench.py > gpurun_out/bench.log 2>&1 || { tail -20 gpurun_out/bench.log; exit 3; }
+tail -1 gpurun_out/bench.log | cut -c1-240
+bash scripts/kstats.sh || exit 4
+[ -n "$(ls mat_dcml_amd/_lib/libmatdcml_ab_*.so 2>/dev/null)" ] && { bash scripts/ct_ab.sh || exit 5; }
+exit 0
