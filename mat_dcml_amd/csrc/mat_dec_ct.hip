@@ -56,7 +56,7 @@ __device__ __forceinline__ CT dec_embed_pre_ct(const DecP& p, int rt, int& tokid
 // array's address into a pointer select, which kept all of xr in scratch memory in the forward kernel)
 template <bool REG>
 __device__ __forceinline__ void cross_proj(const Mat* m, const CT* xr, const bf16_t* sv_x1_in, const float* rep,
-                                           bf16_t* sv_x1_out, const Ctx& c) {
+                                           bf16_t* sv_x1_out, const Ctx& c, bool store_xb = true) {
   const int lane = c.lane;
   CTr xp[MAXRT], rp[MAXRT];
 #pragma unroll
@@ -67,7 +67,7 @@ __device__ __forceinline__ void cross_proj(const Mat* m, const CT* xr, const bf1
       if constexpr (REG) xp[k] = ct_pack(xr[k]);
       else xp[k] = ld_g(sv_x1_in, c.tok0, rt, c.NR, lane);
       if (sv_x1_out) st_g(sv_x1_out, c.tok0, rt, c.NR, xp[k], lane);
-      if constexpr (!REG) st_lds(c.XB, rt, xp[k], tok_ok(rt, c), lane);
+      if constexpr (!REG) { if (store_xb) st_lds(c.XB, rt, xp[k], tok_ok(rt, c), lane); }
     }
   }
 #pragma unroll
@@ -187,10 +187,10 @@ __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, C
   }
   __syncthreads();
   CP_MARK(4);
+  // q / k / v recompute (writes QB / KB / VB only; x1 goes to XB later) before the Wp weight gradient (reads DQ / XB):
+  // its atomics drain under the attention, one barrier fewer
+  cross_proj<false>(m, nullptr, sv_x1, rep, nullptr, c, false);
   wgrad64(c.DQ, c.XB, m[7], c);
-  __syncthreads();
-  CP_MARK(5);
-  cross_proj<false>(m, nullptr, sv_x1, rep, nullptr, c);
   lse_store(lse, c);
   __syncthreads();
   CP_MARK(6);
@@ -201,30 +201,30 @@ __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, C
   __syncthreads();
   CP_MARK(8);
   {
-    CTr rq[MAXRT];
+    CTr rq[MAXRT], xq[MAXRT];
 #pragma unroll
-    for (int k = 0; k < MAXRT; ++k) {   // q input (rep) into QB for dW_q
+    for (int k = 0; k < MAXRT; ++k) {   // q input (rep) into QB for dW_q, k / v input (x1) into XB for dW_k / dW_v
       const int rt = c.wave + NW * k;
-      if (rt < c.NT) rq[k] = ct_pack(ld_gf(rep, c.tok0, rt, c.NR, lane));
+      if (rt < c.NT) {
+        rq[k] = ct_pack(ld_gf(rep, c.tok0, rt, c.NR, lane));
+        xq[k] = ld_g(sv_x1, c.tok0, rt, c.NR, lane);
+      }
     }
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
       const int rt = c.wave + NW * k;
-      if (rt < c.NT) st_lds(c.QB, rt, rq[k], tok_ok(rt, c), lane);
+      if (rt < c.NT) {
+        st_lds(c.QB, rt, rq[k], tok_ok(rt, c), lane);
+        st_lds(c.XB, rt, xq[k], tok_ok(rt, c), lane);
+      }
     }
   }
-  __syncthreads();
-  CP_MARK(9);
-  wgrad64(c.DQ, c.QB, m[4], c);
-  wgrad64(c.KB, c.XB, m[5], c);
-  wgrad64(c.VB, c.XB, m[6], c);
-  CP_MARK(18);
 #pragma unroll
   for (int k = 0; k < MAXRT; ++k) {
     const int rt = c.wave + NW * k;
     if (rt < c.NT) ct_zero(dx[k]);
   }
-  proj3_bwd(m, 4, c.DQ, c.KB, c.VB, dres, dx, c);
+  proj3_bwd(m, 4, c.DQ, c.KB, c.VB, dres, dx, c);   // reads DQ / KB / VB: before the barrier and the weight gradients
   {
     CT cur[MAXRT];
 #pragma unroll
@@ -241,6 +241,11 @@ __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, C
       if (rt < c.NT) st_gf(drep, c.tok0, rt, c.NR, ct_add(cur[k], dres[k]), lane);
     }
   }
+  __syncthreads();
+  CP_MARK(9);
+  wgrad64(c.DQ, c.QB, m[4], c);
+  wgrad64(c.KB, c.XB, m[5], c);
+  wgrad64(c.VB, c.XB, m[6], c);
   __syncthreads();
   CP_MARK(10);
 }

@@ -864,29 +864,31 @@ __device__ __forceinline__ void self_attn_bwd_ct(const Mat* m, const LNp& ln, CT
   }
   __syncthreads();
   CP_MARK(11);
-  wgrad64(c.DQ, c.XB, m[3], c);
-  __syncthreads();
-  CP_MARK(12);
+  // q / k / v recompute first (global weight loads, LDS writes to QB / KB / VB only), then the Wp weight gradient
+  // (reads DQ / XB): its fp32 atomics drain under the attention instead of stalling the next global loads behind
+  // them (vmcnt counts them in order), and one barrier fewer.  XB takes x (the X of dWq/k/v) once every wave is past
+  // dWp (after the query-pass barrier).
   proj3(m, 0, xin, c);
+  wgrad64(c.DQ, c.XB, m[3], c);
+  lse_store(lse, c);
+  __syncthreads();
+  CP_MARK(13);
+  attn_bwd_q_ct(c.QB, c.KB, c.VB, c.DA, c.DQ, causal, c);
 #pragma unroll
   for (int k = 0; k < MAXRT; ++k) {
     const int rt = c.wave + NW * k;
     if (rt < c.NT) st_lds(c.XB, rt, xin[k], tok_ok(rt, c), lane);   // X of dWq / dWk / dWv
   }
-  lse_store(lse, c);
-  __syncthreads();
-  CP_MARK(13);
-  attn_bwd_q_ct(c.QB, c.KB, c.VB, c.DA, c.DQ, causal, c);
   __syncthreads();
   CP_MARK(14);
   attn_bwd_kv_ct(c.QB, c.KB, c.VB, c.DA, causal, c);
   __syncthreads();
   CP_MARK(15);
+  proj3_bwd(m, 0, c.DQ, c.KB, c.VB, dx, dx, c);   // before the weight gradients: its weight loads do not queue
+  CP_MARK(16);                                     // behind their atomics
   wgrad64(c.DQ, c.XB, m[0], c);
   wgrad64(c.KB, c.XB, m[1], c);
   wgrad64(c.VB, c.XB, m[2], c);
-  CP_MARK(16);
-  proj3_bwd(m, 0, c.DQ, c.KB, c.VB, dx, dx, c);
   __syncthreads();
   CP_MARK(17);
 }

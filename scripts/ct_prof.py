@@ -13,10 +13,10 @@ from test_gpu_train import make  # noqa: E402
 from mat_dcml_amd.ops import kernels, mat_train  # noqa: E402
 
 NAMES = {0: "tile start (zero LDS)", 1: "head bwd (tiles)", 19: "head bwd wgrads", 2: "mlp bwd tiles",
-         3: "mlp bwd wgrads", 4: "cross bwd proj+LN", 5: "cross bwd wgrad proj", 6: "cross bwd recompute qkv",
-         7: "cross attn bwd q", 8: "cross attn bwd kv", 9: "cross stage rep", 18: "cross wgrad qkv",
-         10: "cross dX + drep", 11: "self bwd proj+LN", 12: "self bwd wgrad proj", 13: "self bwd recompute qkv",
-         14: "self attn bwd q", 15: "self attn bwd kv", 16: "self wgrad qkv", 17: "self dX", 30: "embedding bwd",
+         3: "mlp bwd wgrads", 4: "cross bwd proj+LN", 6: "cross recompute qkv + wgrad proj",
+         7: "cross attn bwd q", 8: "cross attn bwd kv", 9: "cross stage rep/x1 + dX + drep", 10: "cross wgrad qkv",
+         11: "self bwd proj+LN", 13: "self recompute qkv + wgrad proj", 14: "self attn bwd q (+ stage x)",
+         15: "self attn bwd kv", 16: "self dX", 17: "self wgrad qkv", 30: "embedding bwd",
          20: "self qkv fwd", 21: "self attn fwd", 22: "self proj+LN fwd", 23: "mlp fwd (wave 0)", 24: "cross qkv fwd",
          25: "cross attn fwd", 26: "cross proj+LN fwd", 27: "head fwd", 28: "embedding fwd"}
 
