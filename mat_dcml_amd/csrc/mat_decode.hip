@@ -477,7 +477,10 @@ __device__ unsigned long long g_decode_prof[16];
 #define MDL_PROF_SUB(k) do { } while (0)
 #endif
 
-template <int NB>
+// STG: the inputs are staged in LDS (p.stage) — a compile-time switch, so every table / row pointer of the agent
+// loop is statically an LDS or a global pointer (a runtime select made them generic: flat loads waiting on both
+// counters, vmcnt(0) lgkmcnt(0), in the head / next-row / residual reads of every agent step)
+template <int NB, bool STG>
 __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
 #ifdef MDL_DECODE_PROF
   const bool prof_on = blockIdx.x == 0 && threadIdx.x == 0;
@@ -519,7 +522,7 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
   float* QKV0S = WH2 + pad4((size_t)AD * 65);                // [n_tok][3][64] block-0 token table (p.qkv0)
   float* HW4 = QKV0S + (size_t)p.n_tok * 192;                // wide head: [16][AD] float4 of the folded W_h2
   float* HGC = HW4 + (size_t)AD * 64;                        //   then G[AD], C[AD]
-  const bool stage = p.stage != 0;
+  constexpr bool stage = STG;
   // wide fused head (one-row discrete passes, 4 < AD <= 64: SMAC's 36 actions): lane a of every wave computes logit a
   // from the folded LayerNorm (p.hfold) and the wave samples with ballots / a prefix scan — replaces the generic head
   // phase's per-action loop of 16-lane reductions and its three serial passes over the logits
@@ -960,18 +963,19 @@ MDL_API int mdl_mat_decode(const DecParams* p, int NB, hipStream_t st) {
   q.q2pre = q2_ok && lds + q2b <= 160 * 1024 && p->rep != nullptr;
   if (q.q2pre) lds += q2b;
   p = &q;
-  switch (NB) {
-    case 1:
-      hipFuncSetAttribute((const void*)mat_decode_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL(mat_decode_kernel<1>, dim3(grid), dim3(256), lds, st, *p); break;
-    case 2:
-      hipFuncSetAttribute((const void*)mat_decode_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL(mat_decode_kernel<2>, dim3(grid), dim3(256), lds, st, *p); break;
-    case 3:
-      hipFuncSetAttribute((const void*)mat_decode_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL(mat_decode_kernel<3>, dim3(grid), dim3(256), lds, st, *p); break;
+#define MDL_DECODE_LAUNCH(NB_, STG_)                                                                            \
+  hipFuncSetAttribute((const void*)mat_decode_kernel<NB_, STG_>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+  hipLaunchKernelGGL((mat_decode_kernel<NB_, STG_>), dim3(grid), dim3(256), lds, st, *p)
+  switch (NB * 2 + (p->stage ? 1 : 0)) {
+    case 2: MDL_DECODE_LAUNCH(1, false); break;
+    case 3: MDL_DECODE_LAUNCH(1, true); break;
+    case 4: MDL_DECODE_LAUNCH(2, false); break;
+    case 5: MDL_DECODE_LAUNCH(2, true); break;
+    case 6: MDL_DECODE_LAUNCH(3, false); break;
+    case 7: MDL_DECODE_LAUNCH(3, true); break;
     default: return -3;
   }
+#undef MDL_DECODE_LAUNCH
   MDL_CHECK_LAUNCH();
   return 0;
 }
