@@ -477,6 +477,14 @@ __device__ unsigned long long g_decode_prof[16];
 #define MDL_PROF_SUB(k) do { } while (0)
 #endif
 
+// an LDS pointer held in a VGPR (opaque to uniformity analysis), address space kept for ds_* instructions
+template <typename T>
+__device__ __forceinline__ T* lds_v(T* p) {
+  auto q = (__attribute__((address_space(3))) T*)p;
+  asm volatile("" : "+v"(q));
+  return (T*)q;
+}
+
 // STG: the inputs are staged in LDS (p.stage) — a compile-time switch, so every table / row pointer of the agent
 // loop is statically an LDS or a global pointer (a runtime select made them generic: flat loads waiting on both
 // counters, vmcnt(0) lgkmcnt(0), in the head / next-row / residual reads of every agent step)
@@ -522,6 +530,14 @@ __global__ __launch_bounds__(256, 1) void mat_decode_kernel(DecParams p) {
   float* QKV0S = WH2 + pad4((size_t)AD * 65);                // [n_tok][3][64] block-0 token table (p.qkv0)
   float* HW4 = QKV0S + (size_t)p.n_tok * 192;                // wide head: [16][AD] float4 of the folded W_h2
   float* HGC = HW4 + (size_t)AD * 64;                        //   then G[AD], C[AD]
+#ifndef MDL_DECODE_SGPR_CARVE
+  // the carve's region bases as VGPRs (LDS addresses are VGPR operands anyway): as ~20 uniform SGPR values live
+  // across the agent loop they were the bulk of the kernel's SGPR spills (v_writelane / v_readlane + hazard nops)
+  KV = lds_v(KV); S = lds_v(S); Q = lds_v(Q); XR = lds_v(XR); XA = lds_v(XA); QT = lds_v(QT); Q2T = lds_v(Q2T);
+  LNP = lds_v(LNP); TOK = lds_v(TOK); PEND = lds_v(PEND); EROW = lds_v(EROW); REP = lds_v(REP); AVA = lds_v(AVA);
+  RU = lds_v(RU); RN = lds_v(RN); EMB = lds_v(EMB); WH2 = lds_v(WH2); QKV0S = lds_v(QKV0S); HW4 = lds_v(HW4);
+  HGC = lds_v(HGC);
+#endif
   constexpr bool stage = STG;
   // wide fused head (one-row discrete passes, 4 < AD <= 64: SMAC's 36 actions): lane a of every wave computes logit a
   // from the folded LayerNorm (p.hfold) and the wave samples with ballots / a prefix scan — replaces the generic head
