@@ -127,8 +127,9 @@ def test_decode_discrete_smac_shape(gpu, det):
         print(f"mat_decode B=32 L=27 A=36: {s.elapsed_time(e) / 20 * 1e3:.1f} us per env step")
 
 
-def test_decode_latency(gpu):
-    L, B = 33, 256
+@pytest.mark.parametrize("L", [33, 101])
+def test_decode_latency(gpu, L):
+    B = 256
     m = make(L, gpu)
     obs, ava, rep, rand = inputs(m, B, L, gpu)
     for _ in range(3):
@@ -140,7 +141,7 @@ def test_decode_latency(gpu):
         mat_fused.decode(m, rep, ava, False, 1, rand)
     e.record()
     torch.cuda.synchronize()
-    print(f"mat_decode B=256 L=33: {s.elapsed_time(e) / 20 * 1e3:.1f} us per env step")
+    print(f"mat_decode B=256 L={L}: {s.elapsed_time(e) / 20 * 1e3:.1f} us per env step")
 
 
 @pytest.mark.parametrize("L,A,B", [(6, 1, 64), (2, 6, 40), (17, 3, 16), (33, 2, 8)])
