@@ -70,8 +70,19 @@ class RolloutBuffer:
         """GAE per objective column.  ``use_advantage_norm`` = the DMO buffer (``dmo_shared_buffer.py:233-280``):
         delta = normalize(r) + γ·v' − v on normalised predictions, returns = denormalize(gae + v) once the
         normaliser has statistics (the raw objectives before that)."""
-        self.value_preds[-1].copy_(next_value.view_as(self.value_preds[-1]))
         vn = value_normalizer if self.use_valuenorm else None
+        if not self.use_advantage_norm:
+            from ..ops import kernels
+            n_obj = self.rewards.shape[-1]
+            nv = next_value.reshape(-1)
+            if (kernels.use_hip(self.rewards) and self.value_preds.shape[-1] == n_obj and self.masks.shape[-1] == 1
+                    and nv.numel() == self.value_preds[-1].numel() and nv.dtype == torch.float32
+                    and (vn is None or vn.running_mean.numel() in (1, n_obj))):
+                # one launch: V(T) slot copy + ValueNorm statistics + the reverse scan (ops/kernels.gae_reverse_scan_vn)
+                kernels.gae_reverse_scan_vn(self.rewards, self.value_preds, self.masks, nv.contiguous(), vn, self.gamma,
+                                            self.gae_lambda, self.advantages, self.returns)
+                return
+        self.value_preds[-1].copy_(next_value.view_as(self.value_preds[-1]))
         if self.use_advantage_norm and vn is not None:
             updated = bool(vn.debiasing_term.reshape(-1)[0] > 0)
             r = vn.normalize(self.rewards)

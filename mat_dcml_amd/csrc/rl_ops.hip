@@ -40,6 +40,52 @@ MDL_API int mdl_gae_reverse_scan(const float* rew, const float* vpred, const flo
   return 0;
 }
 
+// The same scan with the ValueNorm statistics derived in-kernel from the running moments (valuenorm.py
+// running_mean_var: d = max(debias, eps), mean = m / d, var = max(m2 / d - mean^2, 1e-2); nvn = 1 or n_obj entries)
+// and the bootstrap value V(T) taken from next_value (also written into the buffer's last slot): one launch per
+// epoch instead of the scan + ~10 torch launches of the statistics and the slot copy.
+__global__ __launch_bounds__(256) void gae_reverse_scan_vn_kernel(
+    const float* __restrict__ rew, float* __restrict__ vpred, const float* __restrict__ masks,
+    const float* __restrict__ next_value, const float* __restrict__ rm, const float* __restrict__ rmsq,
+    const float* __restrict__ deb, float eps, int nvn, float* __restrict__ adv, float* __restrict__ ret,
+    int T, int n, int n_obj, float gamma, float lam) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int o = i % n_obj, im = i / n_obj, nm = n / n_obj;
+  float mean = 0.f, sd = 1.f;
+  if (rm) {
+    const int k = nvn == 1 ? 0 : o;
+    const float d = fmaxf(deb[0], eps);
+    mean = rm[k] / d;
+    sd = sqrtf(fmaxf(rmsq[k] / d - mean * mean, 1e-2f));
+  }
+  const float nv = next_value[i];
+  vpred[(size_t)T * n + i] = nv;
+  float g = 0.f;
+  float v_next = nv * sd + mean;
+  for (int t = T - 1; t >= 0; --t) {
+    const float v = vpred[(size_t)t * n + i] * sd + mean;
+    const float m = masks[(size_t)(t + 1) * nm + im];
+    const float delta = rew[(size_t)t * n + i] + gamma * v_next * m - v;
+    g = delta + gamma * lam * m * g;
+    adv[(size_t)t * n + i] = g;
+    ret[(size_t)t * n + i] = g + v;
+    v_next = v;
+  }
+}
+
+MDL_API int mdl_gae_reverse_scan_vn(const float* rew, float* vpred, const float* masks, const float* next_value,
+                                    const float* rm, const float* rmsq, const float* deb, float eps, int nvn,
+                                    float* adv, float* ret, int T, int n, int n_obj, float gamma, float lam,
+                                    hipStream_t s) {
+  if (n_obj <= 0 || n % n_obj || (rm && nvn != 1 && nvn != n_obj)) return -1;
+  const int bs = 256;
+  hipLaunchKernelGGL(gae_reverse_scan_vn_kernel, dim3((n + bs - 1) / bs), dim3(bs), 0, s, rew, vpred, masks, next_value,
+                     rm, rmsq, deb, eps, nvn, adv, ret, T, n, n_obj, gamma, lam);
+  MDL_CHECK_LAUNCH();
+  return 0;
+}
+
 // Philox test/fill kernel: out[i] = philox(c0 = i, c1, c2, c3; k0, k1) as 4 uint32 (stored in int64 for torch).
 __global__ void philox_fill_kernel(int64_t* out, int n, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
                                    uint32_t k1) {

@@ -109,6 +109,30 @@ def gae_reverse_scan(rewards, value_preds, masks, meanstd, gamma, lam, adv_out, 
                                      T, n, n_obj, gamma, lam, _stream()), "gae_reverse_scan")
 
 
+sig("mdl_gae_reverse_scan_vn", vp, vp, vp, vp, vp, vp, vp, f32, i32, vp, vp, i32, i32, i32, f32, f32, vp)
+
+
+def gae_reverse_scan_vn(rewards, value_preds, masks, next_value, vn, gamma, lam, adv_out, ret_out):
+    """gae_reverse_scan with the ValueNorm statistics computed in-kernel from ``vn``'s running moments (or none) and
+    V(T) = next_value, which is also written into value_preds[-1]."""
+    T = rewards.shape[0]
+    n = rewards[0].numel()
+    n_obj = rewards.shape[-1]
+    assert value_preds.shape[0] == T + 1 and masks.numel() * n_obj == (T + 1) * n and next_value.numel() == n
+    for t in (rewards, value_preds, masks, adv_out, ret_out, next_value):
+        assert t.is_contiguous() and t.dtype == torch.float32
+    rm = rmsq = deb = None
+    nvn, eps = 1, 1e-5
+    if vn is not None:
+        rm, rmsq, deb = vn.running_mean, vn.running_mean_sq, vn.debiasing_term
+        for t in (rm, rmsq, deb):
+            assert t.is_contiguous() and t.dtype == torch.float32
+        nvn, eps = rm.numel(), float(vn.epsilon)
+    check(lib().mdl_gae_reverse_scan_vn(P(rewards), P(value_preds), P(masks), P(next_value), P(rm), P(rmsq), P(deb),
+                                        eps, nvn, P(adv_out), P(ret_out), T, n, n_obj, gamma, lam, _stream()),
+          "gae_reverse_scan_vn")
+
+
 u32 = ctypes.c_uint32
 sig("mdl_philox_fill", vp, i32, u32, u32, u32, u32, u32, vp)
 

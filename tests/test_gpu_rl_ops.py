@@ -41,6 +41,31 @@ def test_gae_multi_objective_matches_torch(gpu):
     assert torch.allclose(ret1[:T], ret2[:T], atol=1e-3, rtol=1e-4)
 
 
+@pytest.mark.parametrize("K,nvn", [(1, 1), (2, 2), (2, 1), (1, 0)])
+def test_gae_vn_kernel_matches_torch(gpu, K, nvn):
+    """kernels.gae_reverse_scan_vn (buffer.compute_returns): ValueNorm statistics derived in-kernel from the running
+    moments and V(T) from next_value, vs the torch statistics + scan; nvn 0 = no value normaliser."""
+    T, E, A = 50, 32, 33
+    g = torch.Generator(device=gpu).manual_seed(3 + K + nvn)
+    rew = torch.randn(T, E, A, K, device=gpu, generator=g) * 10
+    vp = torch.randn(T + 1, E, A, K, device=gpu, generator=g)
+    nv = torch.randn(E, A, K, device=gpu, generator=g)
+    masks = (torch.rand(T + 1, E, A, 1, device=gpu, generator=g) > 0.2).float()
+    vn = None
+    if nvn:
+        vn = ValueNorm(nvn, device=gpu)
+        vn.update(torch.randn(1000, nvn, device=gpu, generator=g) * 20 + 3)
+    vp_ref = vp.clone()
+    vp_ref[-1].copy_(nv)
+    adv1, ret1 = torch.zeros(T, E, A, K, device=gpu), torch.zeros(T + 1, E, A, K, device=gpu)
+    adv2, ret2 = adv1.clone(), ret1.clone()
+    rl_ops.gae_torch(rew, vp_ref, masks, 0.99, 0.95, vn, adv1, ret1)
+    kernels.gae_reverse_scan_vn(rew, vp, masks, nv.reshape(-1).contiguous(), vn, 0.99, 0.95, adv2, ret2)
+    assert torch.equal(vp[-1], nv)
+    assert torch.allclose(adv1, adv2, atol=1e-3, rtol=1e-4)
+    assert torch.allclose(ret1[:T], ret2[:T], atol=1e-3, rtol=1e-4)
+
+
 def test_train_iteration_on_gpu(gpu):
     from mat_dcml_amd.config import get_config, parse_args
     from mat_dcml_amd.runner.dcml_runner import DCMLRunner
