@@ -287,14 +287,21 @@ MDL_API int mdl_adam(const AdamArgs* a, hipStream_t st) {
 // ------------------------------------------------------------------------------------------- dW workspace
 // g[i] += sum_k ws[k * stride + i]; ws zeroed for the next minibatch (the training kernels spread their weight-
 // gradient atomics over `copies` copies, see mat_train_common.h Ctx::gofs).
+// all the copies' loads of an element first (independent, in flight together), then the zero stores: with the
+// store after each load the loads serialised behind possibly-aliasing stores (32 dependent memory round trips)
 __global__ __launch_bounds__(256) void grad_reduce_kernel(float* g, float* ws, int n, long long stride, int copies) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     float s = 0.f;
-    for (int k = 0; k < copies; ++k) {
-      float* w = ws + (size_t)k * stride + i;
-      s += *w;
-      *w = 0.f;
+    int k = 0;
+    for (; k + 8 <= copies; k += 8) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = ws[(size_t)(k + j) * stride + i];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[j];
     }
+    for (; k < copies; ++k) s += ws[(size_t)k * stride + i];
+    for (k = 0; k < copies; ++k) ws[(size_t)k * stride + i] = 0.f;
     g[i] += s;
   }
 }
