@@ -41,7 +41,9 @@ def parse():
     p.add_argument("--num_mini_batch", type=int, default=4)
     p.add_argument("--kernels", default="auto")
     p.add_argument("--dtype", default="bf16")
-    p.add_argument("--phases", action="store_true")
+    p.add_argument("--phases", action="store_true", help="also print the phase summary to stderr")
+    p.add_argument("--no_phase_timers", action="store_true",
+                   help="no hipEvent phase breakdown in the JSON (phase_ms_per_step); for the timer-overhead A/B")
     p.add_argument("--allreduce", default="rccl", choices=["rccl", "oneshot", "auto"],
                    help="data-parallel gradient all-reduce: RCCL (default), the one-shot peer-memory kernel, or auto "
                         "(one-shot only if it matches RCCL and is faster at start-up)")
@@ -127,8 +129,10 @@ def main():
 
     for _ in range(a.warmup):
         runner.train_iteration()
-    if a.phases:
-        runner.timers.summary()
+    # phase breakdown of the timed steps: hipEvent pairs recorded in the stream (no sync inside the loop), resolved
+    # once after the timed region (utils/timers.PhaseTimers)
+    runner.timers.enabled = not a.no_phase_timers
+    runner.timers.summary(reset=True)
     sync()
     comm.barrier()
     sync()
@@ -153,14 +157,22 @@ def main():
                                  for k in ("grad_allreduce", "stats_allreduce")},
             "collectives_per_step": {k: max(r[1].get(k + "_calls", 0) for r in per_rank) // max(a.steps, 1)
                                      for k in ("grad_allreduce", "stats_allreduce")}}
+    phases = None
+    if runner.timers.enabled:
+        tot = runner.timers.totals_ms()
+        n_mb = a.steps * a.ppo_epoch * a.num_mini_batch
+        phases = {"phase_ms_per_step": {k: round(v / a.steps, 3) for k, v in tot.items()},
+                  "train_kernels_ms_per_minibatch": {k[6:]: round(tot[k] / n_mb, 4) for k in ("train_fwd", "train_bwd")
+                                                     if k in tot}}
+        runner.timers.summary(reset=True)
     env_steps = a.steps * a.episode_length * a.envs * n
     value = env_steps / dt
     eval_info = None
     if not a.no_eval and comm.is_main and dev.type == "cuda":
         eval_info = eval_block(a, args, runner, dev)
     if comm.is_main:
-        if a.phases:
-            print(runner.timers.summary(), file=sys.stderr)
+        if a.phases and phases:
+            print(phases, file=sys.stderr)
         print(json.dumps({
             "metric": METRIC if a.n_workers == 32 else f"env-steps/sec (whole node) MAT-AS {a.n_workers}-worker DCML",
             "value": round(value, 2), "unit": "env-steps/s", "n_gpus": topo["distinct_devices"], "steps": a.steps,
@@ -177,14 +189,23 @@ def main():
                        "rollout_groups": runner._groups(),
                        "device": torch.cuda.get_device_name(dev) if dev.type == "cuda" else "cpu"},
             "ranks": n, "backend": topo["backend"], "rank_devices": topo["devices"], "hosts": topo["hosts"],
-            "kernels": paths, "grad_allreduce": getattr(runner.trainer, "grad_allreduce", topo["backend"]) if n > 1 else None,
+            "kernels": paths, "native_build": _native_build(), "grad_allreduce": getattr(runner.trainer, "grad_allreduce", topo["backend"]) if n > 1 else None,
             "grad_allreduce_probe": comm.oneshot_probe,
             # scaling diagnostics: each rank's own ms per step (max = ms_per_step up to the closing barrier) and the
             # critical-path collective time per step (hipEvents on the compute stream, max over ranks)
             **diag,
+            # per-phase GPU time per step (decode / env / insert / update; train_fwd / train_bwd = the four fused
+            # training kernels inside the update) and the training kernels per minibatch
+            **(phases or {}),
             "eval": eval_info,
         }), flush=True)
     comm.destroy()
+
+
+def _native_build():
+    """Source hash of the loaded HIP library (ops/kernels.lib() checked it against the tree), or None."""
+    from mat_dcml_amd.ops import kernels
+    return kernels.BUILD_ID
 
 
 DEFAULT_CKPT = {32: "profiles/r1_train32/transformer_799.pt"}

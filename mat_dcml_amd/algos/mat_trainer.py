@@ -45,6 +45,8 @@ class MATTrainer:
         self.policy = policy
         self.num_agents = num_agents
         self.comm = comm
+        from ..utils.timers import PhaseTimers
+        self.timers = PhaseTimers(device, enabled=False)   # the runner shares its own (bench.py phase breakdown)
         self.clip_param = args.clip_param
         self.ppo_epoch = args.ppo_epoch
         self.num_mini_batch = args.num_mini_batch
@@ -135,7 +137,8 @@ class MATTrainer:
     def ppo_update(self, mb):
         """One minibatch step.  ``mb`` is a dict of device tensors shaped (B, A, ·)."""
         pol = self.policy
-        values, logp, entropy = pol.evaluate_actions(None, mb["obs"], mb["actions"], mb["ava"], mb["active"])
+        with self.timers("train_fwd"):
+            values, logp, entropy = pol.evaluate_actions(None, mb["obs"], mb["actions"], mb["ava"], mb["active"])
         imp = torch.exp(logp - mb["old_logp"])
         surr1 = imp * mb["adv"]
         surr2 = torch.clamp(imp, 1.0 - self.clip_param, 1.0 + self.clip_param) * mb["adv"]
@@ -152,7 +155,8 @@ class MATTrainer:
             flat.buf.zero_()
         else:
             pol.optimizer.zero_grad(set_to_none=False)
-        loss.backward()
+        with self.timers("train_bwd"):
+            loss.backward()
         if self.poison:
             for p in self.params:
                 p.grad.fill_(float("nan"))
@@ -179,14 +183,17 @@ class MATTrainer:
         pol = self.policy
         m = pol.transformer
         enc, dec, _ = mat_train._state(m, mb["obs"].device)
-        v, rep = enc.forward(mb["obs"], save=True)
-        logp, ent = dec.forward(rep, mb["actions"], mb["ava"], save=True)
+        tm = self.timers
+        with tm("train_fwd"):
+            v, rep = enc.forward(mb["obs"], save=True)
+            logp, ent = dec.forward(rep, mb["actions"], mb["ava"], save=True)
         buf = self.comm._flat.buf
         buf.zero_()
         dv, dlp, dent = self.loss_fused.run(v, logp, ent, mb, self.comm, pre_stats=pre_stats)
         m._mdl_gws_active = hasattr(m, "_mdl_gws")   # weight-gradient atomics into the 8-copy workspace
-        drep = dec.backward(dlp, dent)
-        enc.backward(drep, dv)
+        with tm("train_bwd"):
+            drep = dec.backward(dlp, dent)
+            enc.backward(drep, dv)
         m._mdl_gws_active = False
         mat_train.reduce_grad_workspace(m)
         dec.ctx = None

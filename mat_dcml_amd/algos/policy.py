@@ -115,7 +115,8 @@ class TransformerPolicy:
             # globally keyed noise (mat_fused.set_sampling_key): the same draws as the decode kernel's
             B, L = obs.shape[0], obs.shape[1]
             k0, k1, c = mat_fused.next_draw_key(m)
-            rand = act_mod.philox_rand(B, L, m.action_dim, k0, k1, c, m._mdl_env0, obs.device)
+            rand = act_mod.philox_rand(B, L, m.action_dim, k0, k1, c, m._mdl_env0, obs.device,
+                                       normal=m.action_type != "Discrete")
         if not self._is_mat():   # variants (models/variants.py): model-level API
             with self._autocast():
                 a, lp, v = m.get_actions(cent_obs, obs, available_actions, deterministic, stride, rand)

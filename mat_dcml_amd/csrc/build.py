@@ -50,6 +50,45 @@ def _hash(path):
     return h.hexdigest()[:16]
 
 
+def source_hash(src_dir=HERE):
+    """Hash of every HIP source / header of ``src_dir`` (names + contents): the identity of the kernel sources a
+    library was built from.  Embedded in the library as ``mdl_build_source_hash`` and checked by ``ops/kernels.lib()``
+    before anything launches, so a stale ``.so`` shipped next to newer sources can never run silently."""
+    h = hashlib.sha256()
+    for f in sorted(os.listdir(src_dir)):
+        if f.endswith((".h", ".hip")):
+            h.update(f.encode() + b"\0")
+            with open(os.path.join(src_dir, f), "rb") as fh:
+                h.update(fh.read())
+            h.update(b"\0")
+    return h.hexdigest()[:16]
+
+
+def flags_hash(srcs=None):
+    """Hash of the compile flags of every translation unit (environment-dependent A/B flags included)."""
+    h = hashlib.sha256()
+    for src in srcs or _sources():
+        h.update((os.path.basename(src) + ":" + " ".join(_flags(src)) + "\n").encode())
+    return h.hexdigest()[:16]
+
+
+def _buildinfo(srcs):
+    """A one-symbol-pair translation unit carrying the build identity (source hash, flags hash)."""
+    sh, fh = source_hash(), flags_hash(srcs)
+    os.makedirs(os.path.join(OUT_DIR, "obj"), exist_ok=True)
+    obj = os.path.join(OUT_DIR, "obj", f"buildinfo_{sh}_{fh}.o")
+    if not os.path.exists(obj):
+        cpp = obj[:-2] + ".cpp"
+        with open(cpp, "w") as f:
+            f.write(f'extern "C" __attribute__((visibility("default"))) const char mdl_build_source_hash[] = "{sh}";\n'
+                    f'extern "C" __attribute__((visibility("default"))) const char mdl_build_flags_hash[] = "{fh}";\n')
+        r = subprocess.run([HIPCC, "-O2", "-fPIC", "-c", cpp, "-o", obj + ".tmp"], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {cpp}:\n{r.stderr}")
+        os.replace(obj + ".tmp", obj)
+    return obj
+
+
 def _compile(src):
     os.makedirs(os.path.join(OUT_DIR, "obj"), exist_ok=True)
     obj = os.path.join(OUT_DIR, "obj", os.path.basename(src) + "." + _hash(src) + ".o")
@@ -67,6 +106,7 @@ def build(verbose=True, jobs=None):
     jobs = jobs or min(8, len(srcs)) or 1
     with cf.ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(_compile, srcs))
+    objs.append(_buildinfo(srcs))
     cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", OUT + ".tmp"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:

@@ -18,8 +18,9 @@
 // Two buffer halves alternate by epoch parity: a rank can only overwrite half (e & 1) at epoch e + 2 after every
 // peer signalled epoch e + 1 for the slice, i.e. after every peer's epoch-e kernel (same stream) has finished
 // reading it.  Waits are bounded: a missing peer sets the local error word and the kernel exits (never a hang);
-// the host checks the word (`mdl_ar_error`) and the
-// workgroup writes NaN over its output slice (the optimizer's non-finite guard then skips that step).  All cross-GPU traffic uses vector-memory loads / stores / atomics.
+// the workgroup writes NaN over its output slice (the optimizer's non-finite guard then skips that step) and sets
+// bit 31 of every PEER's error word too, so every rank's host check (`mdl_ar_error` / the asynchronous poll) raises,
+// not only the one that timed out.  All cross-GPU traffic uses vector-memory loads / stores / atomics.
 #include "common.h"
 #include <cstring>
 
@@ -81,6 +82,11 @@ __global__ __launch_bounds__(AR_THREADS) void oneshot_allreduce_kernel(ArArgs a)
     }
   }
   __syncthreads();
+  if (timed_out && tid < a.world && tid != a.rank) {
+    // tell EVERY peer (bit 31 of its error word): a peer whose own waits succeeded has applied this step, but its
+    // next poll raises too, so all ranks stop together instead of training on diverged replicas
+    atomicOr(reinterpret_cast<unsigned*>(a.region[tid] + a.err_off), 0x80000000u | (1u << a.rank));   // rank < 16
+  }
   if (timed_out) {   // NaN output: FlatAdam's non-finite guard skips the step instead of applying a partial sum
     for (long long i = (a.vec ? 4 * lo : lo) + tid; i < (a.vec ? 4 * hi : hi); i += AR_THREADS) a.dst[i] = __int_as_float(0x7fc00000);
     return;

@@ -64,16 +64,19 @@ def normal_entropy(std):
     return 0.5 + LOG_SQRT_2PI + torch.log(std)
 
 
-def philox_rand(B, L, act_dim, k0, k1, ctr, env0, device):
+def philox_rand(B, L, act_dim, k0, k1, ctr, env0, device, normal=True):
     """The decode kernel's in-kernel sampling noise on the host (csrc/mat_decode.hip draw_u / draw_n): Philox4x32-10
     of (env0 + b, row, ctr, P_POLICY + k) with key (k0, k1); u = x word, Normals by Box-Muller (dims 0, 1 from the
     y, z words of block 0; dims 2k, 2k + 1 from the x, y words of block k).  Keyed by the global env id, so the eager
-    rollout is independent of how envs are split over ranks too."""
+    rollout is independent of how envs are split over ranks too.  ``normal=False`` (Discrete action spaces, which
+    never read them): only ``u`` — no Box-Muller blocks."""
     from ..utils import philox as px
     env = torch.arange(B, device=device, dtype=torch.int64).view(B, 1) + int(env0)
     row = torch.arange(L, device=device, dtype=torch.int64).view(1, L)
     r0 = px.philox4x32(env, row, int(ctr), px.P_POLICY, k0, k1)
     u = px.u01_open(r0[0]).float()
+    if not normal:
+        return {"u": u}
     n = torch.empty(B, L, act_dim, device=device)
     for k in range((act_dim + 1) // 2):
         r = r0 if k == 0 else px.philox4x32(env, row, int(ctr), px.P_POLICY + k, k0, k1)

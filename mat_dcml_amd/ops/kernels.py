@@ -24,13 +24,73 @@ def mode():
     return os.environ.get("MAT_DCML_KERNELS", "auto").lower()
 
 
+def _csrc():
+    return os.path.join(os.path.dirname(_HERE), "csrc")
+
+
+def _build_mod():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_mat_dcml_build", os.path.join(_csrc(), "build.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def build_identity(L):
+    """(source hash, flags hash) embedded in a loaded library (None for a library built before the guard)."""
+    try:
+        return tuple((ctypes.c_char * 17).in_dll(L, n).value.decode()   # const char[17] arrays, not pointers
+                     for n in ("mdl_build_source_hash", "mdl_build_flags_hash"))
+    except ValueError:
+        return None
+
+
+def check_build(L, src_dir=None, default_lib=None):
+    """None when library ``L`` was built from the sources in ``src_dir`` (and, for the default library, with the
+    default flags); otherwise the reason it is stale."""
+    b = _build_mod()
+    got = build_identity(L)
+    if got is None:
+        return "the library carries no build identity (built before the staleness guard)"
+    want = b.source_hash(src_dir or _csrc())
+    if got[0] != want:
+        return f"built from sources {got[0]}, the tree has {want}"
+    if default_lib if default_lib is not None else LIB_PATH.endswith("libmatdcml.so"):
+        wf = b.flags_hash()
+        if got[1] != wf:
+            return f"built with flags {got[1]}, the build would use {wf}"
+    return None
+
+
+BUILD_ID = None   # the loaded library's source hash (logged by bench.py / smoke)
+
+
 def lib():
-    global _lib, _load_error
+    """Load the HIP library, refusing a stale one: its embedded source / flags hash must match the tree.  A stale
+    library is rebuilt when hipcc exists (the default library only) and is an error otherwise."""
+    global _lib, _load_error, BUILD_ID
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             _load_error = f"{LIB_PATH} not built (run python -c 'import __graft_entry__ as g; g.build()')"
             raise RuntimeError(_load_error)
-        _lib = ctypes.CDLL(LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        why = check_build(L)
+        if why is not None:
+            b = _build_mod()
+            if not (os.path.exists(b.HIPCC) and LIB_PATH == b.OUT):
+                _load_error = f"stale native library {LIB_PATH}: {why}; rebuild it (python mat_dcml_amd/csrc/build.py)"
+                raise RuntimeError(_load_error)
+            import _ctypes
+            _ctypes.dlclose(L._handle)
+            print(f"[kernels] {LIB_PATH} is stale ({why}): rebuilding", flush=True)
+            b.build()
+            L = ctypes.CDLL(LIB_PATH)
+            why = check_build(L)
+            if why is not None:
+                _load_error = f"native library still stale after a rebuild: {why}"
+                raise RuntimeError(_load_error)
+        BUILD_ID = build_identity(L)[0]
+        _lib = L
         _declare(_lib)
     return _lib
 

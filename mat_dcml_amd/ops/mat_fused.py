@@ -160,6 +160,22 @@ def decoder_pack(model):
     return pack
 
 
+def refresh_packs(model):
+    """Rebuild every weight pack that is keyed by ``model._mdl_version`` (encoder / decoder fragment packs, the decode
+    operands, the wide-observation embedding pack) on the CURRENT stream.  A caller that then forks work onto other
+    streams (the runner's pipelined rollout) makes them wait on this stream: otherwise the first group would rebuild
+    the packs lazily on its own stream after an optimizer step and the other groups, seeing the version already
+    current, would read half-written packs."""
+    from . import mat_train
+    if not next(model.parameters()).is_cuda or kernels.mode() == "torch":
+        return
+    if supports(model):
+        decoder_pack(model)
+    if mat_train.encoder_supported(model):
+        enc, _, _ = mat_train._state(model, next(model.parameters()).device)
+        enc.refresh_packs()
+
+
 def set_sampling_key(model, seed: int, env0: int = 0):
     """Key the rollout's exploration noise by (seed, GLOBAL env id, decode-call counter): row b of a decode batch draws
     from env ``env0 + b``.  Every rank uses the same key and counter, and the runner passes its env-id offset, so a

@@ -104,12 +104,15 @@ class ObsEmbed:
                       ud=self.ud.data_ptr(), d_we=_gptr(self.lin.weight), d_be=_gptr(self.lin.bias),
                       d_g=_gptr(self.ln.weight), d_b=_gptr(self.ln.bias))
 
-    def forward(self, obs2d):
+    def refresh(self):
         ver = getattr(self.model, "_mdl_version", 0)
         if ver != self.version:
             a = self._args()
             check(lib().mdl_obs_embed_pack(ctypes.byref(a), kernels._stream()), "obs_embed_pack")
             self.version = ver
+
+    def forward(self, obs2d):
+        self.refresh()
         N = obs2d.shape[0]
         pre = torch.empty(N, 64, device=obs2d.device)
         stat = torch.empty(N, 2, device=obs2d.device)
@@ -312,6 +315,15 @@ class EncoderFused:
         p.lnh = _ln(enc.head[2])
         p.wh2, p.bh2, p.d_wh2 = enc.head[3].weight.data_ptr(), enc.head[3].bias.data_ptr(), _gptr(enc.head[3].weight)
         self.p, self.sig = p, s
+
+    def refresh_packs(self):
+        """Build every version-keyed weight pack the forward reads (shared ModelPack, the wide-observation embedding
+        pack) on the CURRENT stream — see mat_fused.refresh_packs."""
+        model_pack(self.model)
+        if self.model.encoder.obs_dim > MAX_FUSED_OBS:
+            if getattr(self, "emb", None) is None:
+                self.emb = ObsEmbed(self.model)
+            self.emb.refresh()
 
     def forward(self, obs, save=True):
         """obs (B, L, od) -> (v (B, L, n_obj), rep (B, L, 64) f32)."""

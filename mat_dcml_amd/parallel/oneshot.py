@@ -123,7 +123,8 @@ class OneShotAllReduce:
         """Asynchronous error check, once per training iteration: raise if the error word copied by the PREVIOUS
         poll (on the current stream, into pinned memory) is set, then queue the next copy.  A timed-out wait also
         wrote NaN over its output slice, so the optimizer has already skipped that step; this turns it into a
-        loud failure one iteration later without a device synchronisation."""
+        loud failure one iteration later without a device synchronisation.  The timed-out rank also set bit 31 of
+        every peer's word (csrc/xgmi_allreduce.hip), so the peers whose own waits succeeded raise here as well."""
         if getattr(self, "_err_host", None) is None:
             self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
             self._err_ev = None

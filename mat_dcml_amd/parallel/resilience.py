@@ -52,9 +52,13 @@ class FaultInjector:
     def poison_grads(self, iteration: int) -> bool:
         return iteration in self.nan_at
 
-    def maybe_kill(self, iteration: int):
+    def maybe_kill(self, iteration: int, before=None):
+        """Injected hard kill at ``iteration``; ``before()`` (e.g. the runner's pending-log flush) runs first."""
         if self.kill_at is not None and iteration == self.kill_at:
+            if before is not None:
+                before()
             print(f"[fault_inject] rank {self.rank}: killed at iteration {iteration}", file=sys.stderr, flush=True)
+            sys.stdout.flush()   # os._exit skips the interpreter's buffer flush
             os._exit(KILL_EXIT_CODE)
 
 

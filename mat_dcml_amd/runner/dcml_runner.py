@@ -99,6 +99,7 @@ class DCMLRunner:
         self.save_dir = os.path.join(str(self.run_dir), "models") if self.run_dir else None
         self.writter = ScalarWriter(self.log_dir or "/tmp/mat_dcml_logs", enabled=bool(self.run_dir) and self.comm.is_main)
         self.timers = PhaseTimers(self.device, enabled=getattr(a, "profile_phases", False))
+        self.trainer.timers = self.timers
         self.start_episode = 0
         if a.model_dir:
             self.policy.restore(a.model_dir)
@@ -166,6 +167,9 @@ class DCMLRunner:
             self._gstats = [torch.zeros(4, device=self.device, dtype=torch.float64) for _ in range(G)]
         streams = self._gstreams
         cur = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
+        # every version-keyed weight pack is rebuilt HERE, on the current stream, before the groups' streams fork
+        # off it: lazily on group 0's stream, group 1 would read it half-written after an optimizer step
+        mat_fused.refresh_packs(self.policy.transformer)
         for s in streams:
             if s is not None:
                 s.wait_stream(cur)
@@ -306,15 +310,21 @@ class DCMLRunner:
         for episode in range(self.start_episode, episodes):
             if self.use_linear_lr_decay:
                 self.policy.lr_decay(episode, episodes)
-            self.faults.maybe_kill(episode)
+            self.faults.maybe_kill(episode, before=self._log_flush)   # the last queued log is not lost
             self.trainer.poison = self.faults.poison_grads(episode)
-            infos = self.train_iteration()
+            try:
+                infos = self.train_iteration()
+            except BaseException:
+                self._log_flush()   # a faulting iteration still prints the previous interval's statistics
+                raise
             total = (episode + 1) * self.episode_length * self.n_rollout_threads * self.comm.world_size
             if episode % self.save_interval == 0 or episode == episodes - 1:
+                self._log_flush()
                 self.save(episode)
             if episode % self.log_interval == 0:
                 self.log(episode, episodes, total, start, infos)
             if self.use_eval and episode % self.eval_interval == 0:
+                self._log_flush()   # this episode's log prints before the eval output (the reference's order)
                 self.eval(total)
             last_infos = infos
         self._log_flush()

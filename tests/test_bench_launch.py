@@ -43,6 +43,14 @@ def test_bench_self_launches_two_ranks():
     assert cm["grad_allreduce"] + cm["stats_allreduce"] < out["ms_per_step"]
     # SMALL = 1 epoch x 1 minibatch: one gradient average and one epoch-statistics all-reduce per step
     assert out["collectives_per_step"] == {"grad_allreduce": 1, "stats_allreduce": 1}
+    # phase breakdown: per-step time of the rollout phases and the update, and the training
+    # forward / backward per minibatch
+    ph = out["phase_ms_per_step"]
+    assert {"decode", "env", "insert", "update", "train_fwd", "train_bwd"} <= set(ph) and all(v > 0 for v in ph.values())
+    assert ph["train_fwd"] + ph["train_bwd"] <= ph["update"]
+    assert sum(ph[k] for k in ("decode", "env", "insert", "update")) <= out["ms_per_step"] * 1.001
+    tk = out["train_kernels_ms_per_minibatch"]
+    assert set(tk) == {"fwd", "bwd"} and abs(tk["fwd"] - ph["train_fwd"]) < 1e-2   # 1 epoch x 1 minibatch
 
 
 def test_bench_rejects_world_size_mismatch():

@@ -132,6 +132,13 @@ def _timeout_case(comm):
             raised = True
         res = (bool(torch.isnan(y).all()), raised, polled)
     comm.barrier()
+    if comm.rank == 1:   # the timed-out rank flagged its peers too (bit 31): every rank's check raises
+        try:
+            ar.check()
+            res = (None, False, ar.error_word())
+        except RuntimeError:
+            res = (None, True, ar.error_word())
+    comm.barrier()
     ar.close()
     return res
 
@@ -140,3 +147,4 @@ def _timeout_case(comm):
 def test_oneshot_missing_peer_poisons_output_and_raises(gpu):
     out = spawn(_timeout_case, world=2, gpu=True)
     assert out[0] == (True, True, True), out[0]
+    assert out[1][1] and out[1][2] & 0x80000000 and out[1][2] & 1, out[1]   # flagged by rank 0

@@ -65,6 +65,17 @@ def test_killed_run_restarts_from_checkpoint(tmp_path):
     assert (models / "transformer_2.pt").exists()
 
 
+def test_kill_flushes_the_queued_log(tmp_path):
+    """log() only queues its statistics (asynchronous all-reduce); an injected kill at episode 2 must still print the
+    episode-1 log line that was queued before it."""
+    small = [a if a != "100" else "1" for a in SMALL]   # --log_interval 1
+    cmd = [sys.executable, os.path.join(REPO, "DCML_MAT_Train.py")] + small + \
+        ["--num_env_steps", "24", "--results_dir", str(tmp_path), "--fault_inject", "kill@0:2"]
+    r = subprocess.run(cmd, cwd=str(tmp_path), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 17, r.stderr[-2000:]
+    assert "updates 1/3 episodes" in r.stdout, r.stdout[-2000:]
+
+
 def test_heartbeat_detects_silent_rank(monkeypatch):
     import time
     import types

@@ -31,14 +31,30 @@ def _state(r):
     return out, r._done_stats.clone()
 
 
-def _compare(G, n_workers, envs, T, device, iters=1):
+def _update_weights(r, it):
+    """An optimizer-step stand-in that changes every weight identically in both runners (a real train() reduces
+    gradients with fp32 atomics, so the two runners' weights would differ by rounding) and bumps the pack version:
+    the next rollout must see every weight pack rebuilt (the groups' streams raced the lazy rebuild)."""
+    from mat_dcml_amd.ops import mat_fused
+    m = r.policy.transformer
+    g = torch.Generator().manual_seed(100 + it)
+    with torch.no_grad():
+        for p_ in m.parameters():
+            p_.add_(0.05 * torch.randn(p_.shape, generator=g).to(p_.device))
+    mat_fused.bump_version(m)
+
+
+def _compare(G, n_workers, envs, T, device, iters=1, update=False):
     ref, grp = _runner(1, n_workers, envs, T, device), _runner(G, n_workers, envs, T, device)
     assert grp._groups() == G
-    for _ in range(iters):
+    for it in range(iters):
         ref.rollout()
         grp.rollout()
         ref.buffer.after_update()
         grp.buffer.after_update()
+        if update:
+            _update_weights(ref, it)
+            _update_weights(grp, it)
     if device.type == "cuda":
         torch.cuda.synchronize()
     (a, sa), (b, sb) = _state(ref), _state(grp)
@@ -70,13 +86,13 @@ def test_group_views_step_like_the_whole_env():
 
 
 def test_grouped_rollout_equals_single_group_cpu():
-    _compare(2, 4, 4, 5, torch.device("cpu"), iters=2)
+    _compare(2, 4, 4, 5, torch.device("cpu"), iters=2, update=True)
 
 
 @pytest.mark.gpu
 def test_grouped_rollout_equals_single_group_gpu(gpu):
     """HIP env views + fused insert per group on two streams, fused encoder / decode kernels."""
-    ref, grp = _compare(2, 32, 64, 6, torch.device("cuda"), iters=2)
+    ref, grp = _compare(2, 32, 64, 6, torch.device("cuda"), iters=3, update=True)
     from mat_dcml_amd.ops import kernels
     assert grp.envs._kern is not None and kernels.available()
     for r in (ref, grp):   # timing report (not asserted: the overlap gain is measured by bench.py)
