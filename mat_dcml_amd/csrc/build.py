@@ -8,6 +8,7 @@ from __future__ import annotations
 import concurrent.futures as cf
 import hashlib
 import os
+import re
 import subprocess
 import sys
 
@@ -40,10 +41,25 @@ def _sources():
     return sorted(os.path.join(HERE, f) for f in os.listdir(HERE) if f.endswith(".hip"))
 
 
+def _deps(path, seen=None):
+    """The translation unit and every local file it #includes (transitively), sorted."""
+    seen = set() if seen is None else seen
+    if path in seen or not os.path.exists(path):
+        return seen
+    seen.add(path)
+    with open(path) as f:
+        for line in f:
+            m = re.match(r'\s*#\s*include\s+"([^"]+)"', line)
+            if m:
+                _deps(os.path.join(os.path.dirname(path), m.group(1)), seen)
+    return seen
+
+
 def _hash(path):
+    """Object-cache key: the contents of the unit and its local includes, plus its flags (an edit to one kernel no
+    longer rebuilds every other unit)."""
     h = hashlib.sha256()
-    deps = sorted(os.path.join(HERE, f) for f in os.listdir(HERE) if f.endswith((".h", ".hip")))
-    for p in [path] + deps:
+    for p in [path] + sorted(_deps(path) - {path}):
         with open(p, "rb") as f:
             h.update(f.read())
     h.update(" ".join(_flags(path)).encode())
