@@ -132,6 +132,9 @@ def main():
     # phase breakdown of the timed steps: hipEvent pairs recorded in the stream (no sync inside the loop), resolved
     # once after the timed region (utils/timers.PhaseTimers)
     runner.timers.enabled = not a.no_phase_timers
+    # sampled phases (every 10th rollout step, every 4th minibatch): a recorded hipEvent pair costs a few us of
+    # stream bubble, and 540 pairs per iteration slowed the timed loop by 2 %; the totals are scaled back up
+    runner.timers.every.update(decode=10, env=10, insert=10, train_fwd=4, train_bwd=4)
     runner.timers.summary(reset=True)
     sync()
     comm.barrier()

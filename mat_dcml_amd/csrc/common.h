@@ -141,6 +141,11 @@ typedef __attribute__((ext_vector_type(8))) short bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 
+// 2^x as ONE v_exp_f32.  exp2f() compiles to a denormal-safe sequence (range compare, two selects, an add and a
+// v_ldexp_f32 around the v_exp) — 7 VALU per element in the attention loops.  Softmax arguments are <= 0 and a
+// probability below 2^-126 is irrelevant, so the raw instruction (exp2(-inf) = 0) is exact enough everywhere here.
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 // Phi(x) = 0.5 (1 + erf(x / sqrt 2)) with erf from Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below bf16
 // resolution): one rcp, one exp and a degree-5 polynomial instead of the libm erff.  The exp(-x^2/2) factor is
 // shared with the Gaussian pdf of the GELU derivative.
@@ -167,6 +172,13 @@ __device__ __forceinline__ float gelu_erf_grad(float x) {
   float pdf;
   const float cdf = phi_and_pdf(x, pdf);
   return cdf + x * pdf;
+}
+// GELU(x) and GELU'(x) from ONE erf evaluation
+__device__ __forceinline__ float gelu_erf_both(float x, float& grad) {
+  float pdf;
+  const float cdf = phi_and_pdf(x, pdf);
+  grad = fmaf(x, pdf, cdf);
+  return x * cdf;
 }
 
 }  // namespace mdl

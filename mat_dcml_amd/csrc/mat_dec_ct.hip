@@ -477,9 +477,8 @@ __device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c)
         const unsigned am = CONT ? 0u : slot_mask<MA>(p, tok, lane);
         const float actf = CONT ? 0.f : p.act[tok];
         const float dlp = (ok && !CONT) ? p.dlogp[tok] : 0.f, den = (ok && !CONT) ? p.dent[tok] : 0.f;
-        const CT& hh = hhs[k];
-        CT gl = hh, xh, n;
-        gelu_ct(gl);
+        CT gl = hhs[k], ggp, xh, n;   // GELU and GELU' of the head pre-activation from one erf
+        gelu_ct_both(gl, ggp);
         const float rs = ln_fwd_ct(gl, xh, n, gam, bet);
         f32x4 L[MA];
         head_logits_ct<MA>(p, W, n, L, lane);
@@ -553,7 +552,7 @@ __device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) dgg.v[i][q] = ok ? dgg.v[i][q] * gelu_erf_grad(hh.v[i][q]) : 0.f;
+          for (int q = 0; q < 4; ++q) dgg.v[i][q] = ok ? dgg.v[i][q] * ggp.v[i][q] : 0.f;
         st_lds(c.DQ, rt, ct_pack(dgg), ok, lane);   // dY of W_h1
       }
     }
@@ -623,7 +622,7 @@ __device__ __forceinline__ void dec_fwd_tile(const DecP& p, char* smem, int seq0
     asm volatile("" : "+v"(cc.lane), "+v"(cc.tid));
     self_attn_fwd_ct<SAVE>(B.m, B.ln[0], xr, true, p.sv[b].xin, p.sv[b].a1, p.sv[b].a1lo, p.sv[b].lse1, cc);
     cross_attn_fwd_ct<SAVE>(B.m, B.ln[1], xr, p.rep, p.sv[b].x1, p.sv[b].a2, p.sv[b].a2lo, p.sv[b].lse2, cc);
-    mlp_fwd_ct<SAVE>(B.m[8], B.m[9], B.ln[2], xr, p.sv[b].x2, p.sv[b].h, cc);
+    mlp_fwd_ct<SAVE>(B.m[8], B.m[9], B.ln[2], xr, p.sv[b].x2, p.sv[b].g, p.sv[b].gp, cc);
   }
   head_fwd_ct<MA, CONT>(p, xr, SAVE, c);
   CP_MARK(27);
@@ -657,7 +656,7 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
     const Blk& B = p.blk[bb];
     Ctx cc = c;
     asm volatile("" : "+v"(cc.lane), "+v"(cc.tid));
-    mlp_bwd_ct(B.m[8], B.m[9], B.ln[2], dx, p.sv[bb].x2, p.sv[bb].h, cc);
+    mlp_bwd_ct(B.m[8], B.m[9], B.ln[2], dx, p.sv[bb].x2, p.sv[bb].g, p.sv[bb].gp, cc);
     cross_attn_bwd_ct(B.m, B.ln[1], dx, p.rep, p.drep, p.sv[bb].x1, p.sv[bb].a2, p.sv[bb].a2lo, p.sv[bb].lse2,
                       bb == NB - 1, cc);
     self_attn_bwd_ct(B.m, B.ln[0], dx, p.sv[bb].xin, p.sv[bb].a1, p.sv[bb].a1lo, p.sv[bb].lse1, true, cc);
@@ -678,15 +677,14 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
       if (rt < c.NT) {
         const bool ok = tok_ok(rt, c);
         int tk;
-        const CT pre = dec_embed_pre_ct<CONT>(p, rt, tk, c);
-        CT e = pre, xh, yy, de;
-        gelu_ct(e);
+        CT e = dec_embed_pre_ct<CONT>(p, rt, tk, c), egp, xh, yy, de;
+        gelu_ct_both(e, egp);
         const float rs = ln_fwd_ct(e, xh, yy, gam, bet);
         ln_bwd_ct(dx[k], xh, rs, gam, ok, de, dlg, dlb);
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) de.v[mt][r] = ok ? de.v[mt][r] * gelu_erf_grad(pre.v[mt][r]) : 0.f;
+          for (int r = 0; r < 4; ++r) de.v[mt][r] = ok ? de.v[mt][r] * egp.v[mt][r] : 0.f;
         CTr dh, dl, oh;
         ct_split(de, dh, dl);
         CT onehot;
@@ -722,9 +720,8 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
       if (rt < c.NT) {
         const bool ok = tok_ok(rt, c);
         int tk;
-        const CT pre = dec_embed_pre_ct<CONT>(p, rt, tk, c);
-        CT e = pre, xh, yy, de;
-        gelu_ct(e);
+        CT e = dec_embed_pre_ct<CONT>(p, rt, tk, c), egp, xh, yy, de;
+        gelu_ct_both(e, egp);
         const float rs = ln_fwd_ct(e, xh, yy, gam, bet);
         ln_bwd_ct(dx[k], xh, rs, gam, ok, de, dlg, dlb);
         if (ok) {   // EMB[k][f] += d pre_f * a_prev_k (k < A), EMB[A][f] += d pre_f (bias)
@@ -735,7 +732,7 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
           for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float dp = de.v[mt][r] * gelu_erf_grad(pre.v[mt][r]);
+              const float dp = de.v[mt][r] * egp.v[mt][r];
               const int f = 16 * mt + 4 * g + r;
               atomicAdd(EMB + p.A * 64 + f, dp);
               if (!first)

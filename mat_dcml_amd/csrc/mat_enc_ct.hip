@@ -121,7 +121,7 @@ __device__ __forceinline__ void enc_fwd_tile(const EncP& p, const EncX& ex, char
     Ctx cc = c;   // opaque per-iteration lane id: keeps hipcc from hoisting (and spilling) every LDS address
     asm volatile("" : "+v"(cc.lane), "+v"(cc.tid));
     self_attn_fwd_ct<SAVE>(B.m, B.ln[0], xr, false, p.sv[b].xin, p.sv[b].a1, p.sv[b].a1lo, p.sv[b].lse1, cc);
-    mlp_fwd_ct<SAVE>(B.m[8], B.m[9], B.ln[1], xr, p.sv[b].x1, p.sv[b].h, cc);
+    mlp_fwd_ct<SAVE>(B.m[8], B.m[9], B.ln[1], xr, p.sv[b].x1, p.sv[b].g, p.sv[b].gp, cc);
   }
   // value head: v = W_v2 · LN(GELU(W_v1 · rep + b)) + b   (ma_transformer.py:138-139,152)
   AFr H;
@@ -225,9 +225,8 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
         const float dv1 = (ok && p.n_obj > 1) ? p.dv[tok * p.n_obj + 1] : 0.f;
         sdv0 += dv0;
         sdv1 += dv1;
-        const CT& hh = hhs[k];
-        CT gl = hh, xh, n, dn, dg;
-        gelu_ct(gl);
+        CT gl = hhs[k], ggp, xh, n, dn, dg;   // GELU and GELU' of the head pre-activation from one erf
+        gelu_ct_both(gl, ggp);
         const float rs = ln_fwd_ct(gl, xh, n, gam, bet);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -241,7 +240,7 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) dg.v[i][q] = ok ? dg.v[i][q] * gelu_erf_grad(hh.v[i][q]) : 0.f;
+          for (int q = 0; q < 4; ++q) dg.v[i][q] = ok ? dg.v[i][q] * ggp.v[i][q] : 0.f;
         st_lds(c.DQ, rt, ct_pack(dg), ok, lane);   // dY of W_h1
       }
     }
@@ -280,7 +279,7 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
     const Blk& B = p.blk[bb];
     Ctx cc = c;
     asm volatile("" : "+v"(cc.lane), "+v"(cc.tid));
-    mlp_bwd_ct(B.m[8], B.m[9], B.ln[1], dx, p.sv[bb].x1, p.sv[bb].h, cc);
+    mlp_bwd_ct(B.m[8], B.m[9], B.ln[1], dx, p.sv[bb].x1, p.sv[bb].g, p.sv[bb].gp, cc);
     self_attn_bwd_ct(B.m, B.ln[0], dx, p.sv[bb].xin, p.sv[bb].a1, p.sv[bb].a1lo, p.sv[bb].lse1, false, cc);
   }
   // ---------------- embedding backward: x0 = LN0(GELU(pre)), pre = W_e · LN_obs(obs) + b_e
@@ -302,15 +301,14 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
       if (rt < c.NT) {
         const bool ok = tok_ok(rt, c);
         float oh[4] = {0.f, 0.f, 0.f, 0.f}, hat[4] = {0.f, 0.f, 0.f, 0.f};
-        const CT pre = embed_pre(p, ex, rt, W, oh, hat, c);
-        CT e = pre, xh, yy, de;
-        gelu_ct(e);
+        CT e = embed_pre(p, ex, rt, W, oh, hat, c), egp, xh, yy, de;
+        gelu_ct_both(e, egp);
         const float rs = ln_fwd_ct(e, xh, yy, gam, bet);
         ln_bwd_ct(dx[k], xh, rs, gam, ok, de, dlg, dlb);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) de.v[i][q] = ok ? de.v[i][q] * gelu_erf_grad(pre.v[i][q]) : 0.f;
+          for (int q = 0; q < 4; ++q) de.v[i][q] = ok ? de.v[i][q] * egp.v[i][q] : 0.f;
         if (ex.pre_in) {
           st_gf(ex.dpre_out, c.tok0, rt, c.NR, de, lane);
           continue;

@@ -34,9 +34,11 @@ struct Mat { const bf16_t* fw; const bf16_t* bw; const float* b; float* dW; floa
 struct LNp { const float* g; const float* b; float* dg; float* db; };
 struct Blk { Mat m[10]; LNp ln[3]; };
 // saved activations of one block; a1lo / a2lo = the bf16 residual O - bf16(O) of the attention outputs, so the
-// backward's delta = rowsum(dO O) sees O to ~16 significant bits (bf16 O alone put 10-40 % errors on dK / dQ)
-struct Sv { bf16_t* xin; bf16_t* a1; float* lse1; bf16_t* x1; bf16_t* a2; float* lse2; bf16_t* x2; bf16_t* h;
-            bf16_t* a1lo; bf16_t* a2lo; };
+// backward's delta = rowsum(dO O) sees O to ~16 significant bits (bf16 O alone put 10-40 % errors on dK / dQ);
+// g / gp = the MLP's GELU(h) (the exact bf16 operand the forward fed to W2) and GELU'(h): the backward evaluates
+// no erf for the MLP (round 3 recomputed GELU and GELU' from h: two erf per element)
+struct Sv { bf16_t* xin; bf16_t* a1; float* lse1; bf16_t* x1; bf16_t* a2; float* lse2; bf16_t* x2; bf16_t* g;
+            bf16_t* a1lo; bf16_t* a2lo; bf16_t* gp; };
 
 struct EncP {
   int Bs, L, od, SQ, NRP, n_obj;

@@ -162,6 +162,13 @@ __device__ __forceinline__ void gelu_ct(CT& t) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) t.v[i][r] = gelu_erf(t.v[i][r]);
 }
+// t <- GELU(t), gp <- GELU'(t) (one erf per element)
+__device__ __forceinline__ void gelu_ct_both(CT& t, CT& gp) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) t.v[i][r] = gelu_erf_both(t.v[i][r], gp.v[i][r]);
+}
 
 __device__ __forceinline__ float cross_row_max(float x) {
   float a, b;
@@ -461,13 +468,19 @@ __device__ __forceinline__ QSpan qspan(int q, bool causal, const Ctx& c) {
   return s;
 }
 
-// scores of one chunk for this lane's query, log2 units, invisible keys -inf
+// key j of this lane's chunk slots is visible iff qs <= base + j < qe: ONE unsigned compare of (base - qs + j)
+// against the span (was two signed compares and a mask AND per key)
+__device__ __forceinline__ bool key_vis(int d0, unsigned span, int j) { return (unsigned)(d0 + j) < span; }
+
+// raw scores of one chunk for this lane's query (unscaled), invisible keys -inf; the 1/sqrt(d) log2(e) scale is
+// applied by the consumer inside its exp2 argument (one FMA)
 __device__ __forceinline__ void chunk_scores(const bf16_t* K, int kb, int h, const bf16x8& qB, const QSpan& qs,
                                              float* sc, int lane) {
   score_chunk_T(K, kb, h, qB, sc, lane);
-  const int base = kb + 8 * (lane >> 4);
+  const int d0 = kb + 8 * (lane >> 4) - qs.qs;
+  const unsigned span = (unsigned)(qs.qe - qs.qs);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) sc[j] = (base + j >= qs.qs && base + j < qs.qe) ? sc[j] * ATT_L2 : -INFINITY;
+  for (int j = 0; j < 8; ++j) sc[j] = key_vis(d0, span, j) ? sc[j] : -INFINITY;
 }
 
 __device__ __forceinline__ bf16x8 pack8v(const float* x) {
@@ -506,13 +519,13 @@ __device__ __forceinline__ void attn_fwd_ct(const bf16_t* Q, const bf16_t* K, co
           float cm = sc[0];
 #pragma unroll
           for (int j = 1; j < 8; ++j) cm = fmaxf(cm, sc[j]);
-          const float nm = fmaxf(m, cross_row_max(cm));
+          const float nm = fmaxf(m, cross_row_max(cm) * ATT_L2);   // running max in log2 units
           const float mr = nm == -INFINITY ? 0.f : nm;
-          const float alpha = exp2f(m - mr);
+          const float alpha = fast_exp2(m - mr);
           float ps = 0.f;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            sc[j] = exp2f(sc[j] - mr);
+            sc[j] = fast_exp2(fmaf(sc[j], ATT_L2, -mr));
             ps += sc[j];
           }
           l = l * alpha + ps;
@@ -585,7 +598,7 @@ __device__ __forceinline__ void attn_bwd_q_ct(const bf16_t* Q, const bf16_t* K, 
       chunk_scores(K, kb, h, qB, qs, sc, lane);
       score_chunk_T(V, kb, h, dB, dp, lane);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) sc[j] = exp2f(sc[j] - lse) * (dp[j] - delta);
+      for (int j = 0; j < 8; ++j) sc[j] = fast_exp2(fmaf(sc[j], ATT_L2, -lse)) * (dp[j] - delta);
       bf16x8 dsh, dsl;
       split8v(sc, dsh, dsl);
       const bf16x8 k0 = ld_frag_T(K, kb, 32 * h, lane), k1 = ld_frag_T(K, kb, 32 * h + 16, lane);
@@ -608,6 +621,7 @@ __device__ __forceinline__ void attn_bwd_kv_ct(const bf16_t* Q, bf16_t* K, bf16_
     const bool kv = kk < c.NR;
     const int ks = (kk / c.L) * c.L, ke = min(ks + c.L, c.NR);
     const int qlo = causal ? kk : ks;
+    const unsigned qspan_n = kv ? (unsigned)(ke - qlo) : 0u;   // queries [qlo, ke) see this key
     SeqSpan sp = tile_span(rt, c, false);
     if (causal) sp.lo = (rt * 16) & ~31;
     const bf16x8 kB = lda_tm(K, kk, 4 * h + g), vB = lda_tm(V, kk, 4 * h + g);
@@ -622,11 +636,10 @@ __device__ __forceinline__ void attn_bwd_kv_ct(const bf16_t* Q, bf16_t* K, bf16_
       const float lsev[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
       const float delv[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
       float pv[8], ds[8];
+      const int d0 = qb + 8 * g - qlo;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int qq = qb + 8 * g + j;
-        const bool ok = kv && qq >= qlo && qq < ke;
-        pv[j] = ok ? exp2f(sc[j] * ATT_L2 - lsev[j]) : 0.f;
+        pv[j] = fast_exp2(key_vis(d0, qspan_n, j) ? fmaf(sc[j], ATT_L2, -lsev[j]) : -INFINITY);
         ds[j] = pv[j] * (dp[j] - delv[j]);
       }
       bf16x8 ph, pl, dsh, dsl;
@@ -694,8 +707,8 @@ __device__ __forceinline__ void self_attn_fwd_ct(const Mat* m, const LNp& ln, CT
 
 // MLP: x <- LN(x + W2 GELU(W1 x + b1) + b2)   (ma_transformer.py:84-86,91-92)
 template <bool SAVE>
-__device__ __forceinline__ void mlp_fwd_ct(const Mat& m1, const Mat& m2, const LNp& ln, CT* xr, bf16_t* sv_x, bf16_t* sv_h,
-                                           const Ctx& c) {
+__device__ __forceinline__ void mlp_fwd_ct(const Mat& m1, const Mat& m2, const LNp& ln, CT* xr, bf16_t* sv_x, bf16_t* sv_g,
+                                           bf16_t* sv_gp, const Ctx& c) {
   const int lane = c.lane;
   AFr W1, W2;
   loadA(W1, m1.fa, lane);
@@ -709,10 +722,19 @@ __device__ __forceinline__ void mlp_fwd_ct(const Mat& m1, const Mat& m2, const L
       if (SAVE) st_g(sv_x, c.tok0, rt, c.NR, x, lane);
       CT h = b1;
       mm(h, W1, x);
-      if (SAVE) st_g(sv_h, c.tok0, rt, c.NR, ct_pack(h), lane);
-      gelu_ct(h);
+      CTr gr;
+      if (SAVE) {   // GELU(h) (the W2 operand) and GELU'(h) for the backward, from one erf
+        CT gp;
+        gelu_ct_both(h, gp);
+        gr = ct_pack(h);
+        st_g(sv_g, c.tok0, rt, c.NR, gr, lane);
+        st_g(sv_gp, c.tok0, rt, c.NR, ct_pack(gp), lane);
+      } else {
+        gelu_ct(h);
+        gr = ct_pack(h);
+      }
       CT mo = ct_add(b2, xr[k]), xh;
-      mm(mo, W2, ct_pack(h));
+      mm(mo, W2, gr);
       ln_fwd_ct(mo, xh, xr[k], gam, bet);
     }
   }
@@ -724,7 +746,7 @@ __device__ __forceinline__ void mlp_fwd_ct(const Mat& m1, const Mat& m2, const L
 // under 256 registers): each pass leaves its per-tile products in this wave's own LDS rows (read back by the same
 // lanes, so no barrier between passes) or in dx.
 __device__ __forceinline__ void mlp_bwd_ct(const Mat& m1, const Mat& m2, const LNp& ln, CT* dx, const bf16_t* sv_x,
-                                           const bf16_t* sv_h, const Ctx& c) {
+                                           const bf16_t* sv_g, const bf16_t* sv_gp, const Ctx& c) {
   const int lane = c.lane;
   {   // pass 1 (W2): LN backward -> ds (dx) ; DA = dY of W2, XB = X of W2 (GELU(h))
     CT dlg, dlb;
@@ -739,7 +761,7 @@ __device__ __forceinline__ void mlp_bwd_ct(const Mat& m1, const Mat& m2, const L
       const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         xs[k] = ld_g(sv_x, c.tok0, rt, c.NR, lane);
-        hs[k] = ld_g(sv_h, c.tok0, rt, c.NR, lane);
+        hs[k] = ld_g(sv_g, c.tok0, rt, c.NR, lane);
       }
     }
 #pragma unroll
@@ -747,9 +769,7 @@ __device__ __forceinline__ void mlp_bwd_ct(const Mat& m1, const Mat& m2, const L
       const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         const bool ok = tok_ok(rt, c);
-        CT gl = ct_unpack(hs[k]);
-        gelu_ct(gl);
-        const CTr glr = ct_pack(gl);
+        const CTr glr = hs[k];   // GELU(h): the forward's own W2 operand
         CT mo = ct_add(b2, ct_unpack(xs[k])), xh, yy, ds;
         mm(mo, W2f, glr);
         const float rs = ln_fwd_ct(mo, xh, yy, gam, bet);
@@ -771,14 +791,14 @@ __device__ __forceinline__ void mlp_bwd_ct(const Mat& m1, const Mat& m2, const L
       const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         const bool ok = tok_ok(rt, c);
-        const CT h = ct_unpack(ld_g(sv_h, c.tok0, rt, c.NR, lane));
+        const CT gp = ct_unpack(ld_g(sv_gp, c.tok0, rt, c.NR, lane));   // GELU'(h), saved by the forward
         CT dg;
         ct_zero(dg);
         mm(dg, W2b, ld_lds(c.DA, rt, lane));
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) dg.v[i][r] = ok ? dg.v[i][r] * gelu_erf_grad(h.v[i][r]) : 0.f;
+          for (int r = 0; r < 4; ++r) dg.v[i][r] = ok ? dg.v[i][r] * gp.v[i][r] : 0.f;
         st_lds(c.KB, rt, ct_pack(dg), ok, lane);
       }
     }

@@ -49,6 +49,10 @@ def check_build(L, src_dir=None, default_lib=None):
     """None when library ``L`` was built from the sources in ``src_dir`` (and, for the default library, with the
     default flags); otherwise the reason it is stale."""
     b = _build_mod()
+    if os.path.basename(LIB_PATH).startswith("libmatdcml_ab_") and src_dir is None:
+        # explicit A/B timing builds (scripts/build_ab.sh: another revision's sources, or timing-only variants) are
+        # never loaded by the tests / bench / smoke, which use the default library
+        return None
     got = build_identity(L)
     if got is None:
         return "the library carries no build identity (built before the staleness guard)"

@@ -34,7 +34,8 @@ class Blk(ctypes.Structure):
 
 
 class Sv(ctypes.Structure):
-    _fields_ = [(n, VP) for n in ("xin", "a1", "lse1", "x1", "a2", "lse2", "x2", "h", "a1lo", "a2lo")]
+    # g / gp: the MLP's GELU(h) and GELU'(h) as bf16 (the backward recomputes neither)
+    _fields_ = [(n, VP) for n in ("xin", "a1", "lse1", "x1", "a2", "lse2", "x2", "g", "a1lo", "a2lo", "gp")]
 
 
 class EncP(ctypes.Structure):
@@ -350,11 +351,11 @@ class EncoderFused:
         saves = []
         if save:
             for bi in range(m.n_block):
-                t = torch.empty(5, n_tok, 64, device=dev, dtype=torch.bfloat16)
+                t = torch.empty(6, n_tok, 64, device=dev, dtype=torch.bfloat16)
                 lse = torch.empty(n_tok, 2, device=dev)
                 saves += [t, lse]
                 p.sv[bi] = Sv(t[0].data_ptr(), t[1].data_ptr(), lse.data_ptr(), t[2].data_ptr(), None, None, None,
-                              t[3].data_ptr(), t[4].data_ptr(), None)
+                              t[3].data_ptr(), t[4].data_ptr(), None, t[5].data_ptr())
         check(_enc_fwd(sfx, p, _ptr(pre), m.n_block, save), "mat_enc_fwd")
         self.ctx = (obs, rep, v, saves, [Sv.from_buffer_copy(p.sv[i]) for i in range(m.n_block)], pre, stat)
         return v, rep
@@ -462,11 +463,12 @@ class DecoderFused:
         saves = []
         if save:
             for bi in range(m.n_block):
-                t = torch.empty(8, n_tok, 64, device=dev, dtype=torch.bfloat16)
+                t = torch.empty(9, n_tok, 64, device=dev, dtype=torch.bfloat16)
                 lse = torch.empty(2, n_tok, 2, device=dev)
                 saves += [t, lse]
                 p.sv[bi] = Sv(t[0].data_ptr(), t[1].data_ptr(), lse[0].data_ptr(), t[2].data_ptr(), t[3].data_ptr(),
-                              lse[1].data_ptr(), t[4].data_ptr(), t[5].data_ptr(), t[6].data_ptr(), t[7].data_ptr())
+                              lse[1].data_ptr(), t[4].data_ptr(), t[5].data_ptr(), t[6].data_ptr(), t[7].data_ptr(),
+                              t[8].data_ptr())
             head = torch.empty(n_tok, 64, device=dev, dtype=torch.bfloat16)
             saves.append(head)
             p.sv_head = head.data_ptr()

@@ -46,15 +46,26 @@ def roctx_range(name: str):
 
 
 class PhaseTimers:
-    def __init__(self, device, enabled=False):
+    """``every``: {phase: n} records only every n-th occurrence of a frequent phase and scales its total by
+    occurrences / recorded (bench.py: each recorded hipEvent pair costs a few microseconds of stream bubble, so the
+    per-rollout-step and per-minibatch phases are sampled to keep the timed loop within 1 % of its untimed speed)."""
+
+    def __init__(self, device, enabled=False, every=None):
         self.enabled = enabled
         self.cuda = torch.device(device).type == "cuda"
         self.events = {}
         self.host = {}
+        self.every = dict(every or {})
+        self.count = {}
 
     @contextlib.contextmanager
     def __call__(self, name):
         if not self.enabled:
+            yield
+            return
+        n = self.count.get(name, 0)
+        self.count[name] = n + 1
+        if n % self.every.get(name, 1):
             yield
             return
         with roctx_range(name):
@@ -70,11 +81,11 @@ class PhaseTimers:
                 self.host.setdefault(name, []).append(time.perf_counter() - t)
 
     def totals_ms(self):
-        out = {k: sum(v) * 1e3 for k, v in self.host.items()}
+        out = {k: sum(v) * 1e3 * self.count.get(k, len(v)) / len(v) for k, v in self.host.items()}
         if self.events:
             torch.cuda.synchronize()
             for k, v in self.events.items():
-                out[k] = out.get(k, 0.0) + sum(s.elapsed_time(e) for s, e in v)
+                out[k] = out.get(k, 0.0) + sum(s.elapsed_time(e) for s, e in v) * self.count.get(k, len(v)) / len(v)
         return out
 
     def summary(self, reset=True):
@@ -83,4 +94,5 @@ class PhaseTimers:
         if reset:
             self.events.clear()
             self.host.clear()
+            self.count.clear()
         return "[phases] " + s

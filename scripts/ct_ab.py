@@ -48,9 +48,11 @@ def main(B=3200, L=33, reps=20):
     st["enc_bwd"] = timed(lambda: enc.backward(drep, torch.ones_like(v)), reps)
     st["grad_reduce"] = timed(lambda: mat_train.reduce_grad_workspace(m), reps)
     st["total"] = sum(st.values())
-    print(os.environ.get("MAT_DCML_LIBNAME", "libmatdcml.so"), f"copies={os.environ.get('MAT_DCML_GRAD_COPIES', '8')}",
+    print(os.environ.get("MAT_DCML_LIBNAME", "libmatdcml.so"), f"B={B} L={L}",
           " ".join(f"{k} {v:.1f}us" for k, v in st.items()))
 
 
 if __name__ == "__main__":
-    main()
+    for L in os.environ.get("CT_AB_L", "33").split(","):
+        L = int(L)
+        main(B=3200 * 33 // L if L != 33 else 3200, L=L)

@@ -48,7 +48,8 @@ def test_bench_self_launches_two_ranks():
     ph = out["phase_ms_per_step"]
     assert {"decode", "env", "insert", "update", "train_fwd", "train_bwd"} <= set(ph) and all(v > 0 for v in ph.values())
     assert ph["train_fwd"] + ph["train_bwd"] <= ph["update"]
-    assert sum(ph[k] for k in ("decode", "env", "insert", "update")) <= out["ms_per_step"] * 1.001
+    # decode / env / insert are sampled (every 10th step) and scaled: an estimate, not a partition of the step
+    assert sum(ph[k] for k in ("decode", "env", "insert", "update")) <= out["ms_per_step"] * 1.25
     tk = out["train_kernels_ms_per_minibatch"]
     assert set(tk) == {"fwd", "bwd"} and abs(tk["fwd"] - ph["train_fwd"]) < 1e-2   # 1 epoch x 1 minibatch
 
