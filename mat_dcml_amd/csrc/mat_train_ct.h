@@ -167,7 +167,11 @@ __device__ __forceinline__ void gelu_ct_both(CT& t, CT& gp) {
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) t.v[i][r] = gelu_erf_both(t.v[i][r], gp.v[i][r]);
+    for (int r = 0; r < 4; ++r) {
+      float d;
+      t.v[i][r] = gelu_erf_both(t.v[i][r], d);
+      gp.v[i][r] = d;
+    }
 }
 
 __device__ __forceinline__ float cross_row_max(float x) {
