@@ -244,8 +244,11 @@ __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, C
   __syncthreads();
   CP_MARK(9);
   wgrad64(c.DQ, c.QB, m[4], c);
-  wgrad64(c.KB, c.XB, m[5], c);
-  wgrad64(c.VB, c.XB, m[6], c);
+  {
+    const bf16_t* const ys[2] = {c.KB, c.VB};
+    const Mat* const ms[2] = {&m[5], &m[6]};
+    wgrad64_shared_x<2>(ys, c.XB, ms, c);
+  }
   __syncthreads();
   CP_MARK(10);
 }

@@ -414,6 +414,62 @@ __device__ __forceinline__ void wgrad64(const bf16_t* Y, const bf16_t* X, const 
   wgrad_g(Y, X, c.KP, c.g(m.dW), 64, 64, 64, c.g(m.db), c.wave, c.lane);
 }
 
+// The weight gradients of TWO or THREE 64x64 matrices that share their input X (dW_q / dW_k / dW_v of an attention,
+// dW_k / dW_v of the cross attention): one pass over the token axis reads each X fragment once for all of them
+// (wgrad64 per matrix re-read X: 6 transposed LDS reads per 2 MFMAs; here 2 + 2 NM per 2 NM).
+template <int NM>
+__device__ __forceinline__ void wgrad64_shared_x(const bf16_t* const (&Y)[NM], const bf16_t* X, const Mat* const (&m)[NM],
+                                                 const Ctx& c) {
+  static_assert(NW % 4 == 0, "row block per wave");
+  constexpr int NCT = (16 + NW - 1) / NW;
+  const int wave = c.wave, lane = c.lane, KP = c.KP;
+  const int rb = wave & 3;
+  const bool bias = wave < 4;
+  const int g = lane >> 4, c16 = lane & 15;
+  f32x4 acc[NM][NCT], accb[NM];
+#pragma unroll
+  for (int i = 0; i < NM; ++i) {
+    accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < NCT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const bf16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
+  for (int k0 = 0; k0 < KP; k0 += 32) {
+    bf16x8 xb[NCT];
+#pragma unroll
+    for (int j = 0; j < NCT; ++j) {
+      const int bj = wave + NW * j;
+      if (bj < 16) xb[j] = ld_frag_T(X, k0, 16 * (bj >> 2), lane);
+    }
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+      const bf16x8 a = ld_frag_T(Y[i], k0, 16 * rb, lane);
+#pragma unroll
+      for (int j = 0; j < NCT; ++j)
+        if (wave + NW * j < 16) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, xb[j], acc[i][j], 0, 0, 0);
+      if (bias) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ones, accb[i], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NM; ++i) {
+    float* dW = c.g(m[i]->dW);
+    float* db = c.g(m[i]->db);
+    if (dW) {
+#pragma unroll
+      for (int j = 0; j < NCT; ++j) {
+        const int bj = wave + NW * j, ct = bj >> 2;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (bj < 16) atomicAdd(dW + (16 * rb + 4 * g + r) * 64 + 16 * ct + c16, acc[i][j][r]);
+      }
+    }
+    if (bias && db && c16 < 4) {
+      const float v = c16 == 0 ? accb[i][0] : c16 == 1 ? accb[i][1] : c16 == 2 ? accb[i][2] : accb[i][3];
+      atomicAdd(db + 16 * rb + 4 * g + c16, v);
+    }
+  }
+}
+
 // q / k / v projections of the packed tiles xp (one weight matrix live at a time) -> QB / KB / VB; m0 = index of
 // the query matrix (0: self attention; the cross attention has its own q input)
 __device__ __forceinline__ void proj3(const Mat* m, int m0, const CTr* xp, const Ctx& c) {
@@ -910,9 +966,11 @@ __device__ __forceinline__ void self_attn_bwd_ct(const Mat* m, const LNp& ln, CT
   CP_MARK(15);
   proj3_bwd(m, 0, c.DQ, c.KB, c.VB, dx, dx, c);   // before the weight gradients: its weight loads do not queue
   CP_MARK(16);                                     // behind their atomics
-  wgrad64(c.DQ, c.XB, m[0], c);
-  wgrad64(c.KB, c.XB, m[1], c);
-  wgrad64(c.VB, c.XB, m[2], c);
+  {
+    const bf16_t* const ys[3] = {c.DQ, c.KB, c.VB};
+    const Mat* const ms[3] = {&m[0], &m[1], &m[2]};
+    wgrad64_shared_x<3>(ys, c.XB, ms, c);
+  }
   __syncthreads();
   CP_MARK(17);
 }
