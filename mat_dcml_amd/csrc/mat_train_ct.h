@@ -297,28 +297,31 @@ __device__ __forceinline__ float ln_fwd_ct(const CT& x, CT& xh, CT& y, const CT&
   return rstd;
 }
 #endif
-// dx from dy (tokens with ok == false contribute nothing); per-lane gamma / beta gradient partials in dg / db
-__device__ __forceinline__ void ln_bwd_ct(const CT& dy, const CT& xh, float rstd, const CT& gam, bool ok, CT& dx, CT& dg,
-                                          CT& db) {
+// dx from dy; per-lane gamma / beta gradient partials in dg / db.  Padded token rows (row >= NR) need no mask here:
+// every backward input is zero on them (the loss gradients, the saved activations and every LDS operand are
+// stored masked, and xh of a padded row is the finite LN of its bias), so they contribute exactly zero.
+// dx = rstd (gy - mean(gy) - xh mean(gy xh)) as two FMAs per element.
+__device__ __forceinline__ void ln_bwd_ct(const CT& dy, const CT& xh, float rstd, const CT& gam, bool /*ok*/, CT& dx,
+                                          CT& dg, CT& db) {
   CT gy;
   float a = 0.f, b = 0.f;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float d = ok ? dy.v[i][r] : 0.f;
+      const float d = dy.v[i][r];
       gy.v[i][r] = d * gam.v[i][r];
       a += gy.v[i][r];
-      b += gy.v[i][r] * xh.v[i][r];
-      dg.v[i][r] += d * xh.v[i][r];
+      b = fmaf(gy.v[i][r], xh.v[i][r], b);
+      dg.v[i][r] = fmaf(d, xh.v[i][r], dg.v[i][r]);
       db.v[i][r] += d;
     }
-  a = cross_row_sum(a) * (1.f / 64.f);
-  b = cross_row_sum(b) * (1.f / 64.f);
+  const float A = cross_row_sum(a) * (rstd * (1.f / 64.f));
+  const float B = cross_row_sum(b) * (rstd * (1.f / 64.f));
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) dx.v[i][r] = (gy.v[i][r] - a - xh.v[i][r] * b) * rstd;
+    for (int r = 0; r < 4; ++r) dx.v[i][r] = fmaf(-xh.v[i][r], B, fmaf(gy.v[i][r], rstd, -A));
 }
 
 // per-lane feature partials (summed over the tokens the lane saw) -> one atomic per feature: reduce over the 16
