@@ -49,6 +49,39 @@ __device__ __forceinline__ CT dec_embed_pre_ct(const DecP& p, int rt, int& tokid
   return pre;
 }
 
+// Action-embedding table (discrete tokens): x0 = LN_dec(GELU(W_a[:, t])) depends only on the token id t in [0, A]
+// (ma_transformer.py:194-195,224 on the one-hot shifted action), so its A + 1 rows — and for the backward x-hat,
+// rstd and GELU' — are computed once per tile chunk, one wave per token row (lane = feature), instead of a W_a
+// gather, an erf and a LayerNorm per token row.  fwd: X = x0; bwd: X = x-hat, GP = GELU'(pre), RS = rstd.
+__device__ __forceinline__ void emb_table(const DecP& p, float* X, float* GP, float* RS, bool fwd, const Ctx& c) {
+  const int f = c.lane;
+  for (int t = c.wave; t <= p.A; t += NW) {
+    float gp;
+    const float e = gelu_erf_both(p.wa[f * (p.A + 1) + t], gp);
+    const float mean = wave_sum(e) * (1.f / 64.f);
+    const float d = e - mean;
+    const float rstd = rsqrtf(wave_sum(d * d) * (1.f / 64.f) + 1e-5f);
+    const float xh = d * rstd;
+    if (fwd) {
+      X[t * 64 + f] = fmaf(xh, p.lnd_g[f], p.lnd_b[f]);
+    } else {
+      X[t * 64 + f] = xh;
+      GP[t * 64 + f] = gp;
+      if (f == 0) RS[t] = rstd;
+    }
+  }
+}
+__device__ __forceinline__ CT emb_row(const float* T, int tok, int lane) {
+  const int g = lane >> 4;
+  CT x;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) x.v[mt] = *(const f32x4*)(T + tok * 64 + 16 * mt + 4 * g);
+  return x;
+}
+// the tables fit the (free at that point) Q buffer (forward) / Q + K buffers (backward)
+__device__ __forceinline__ bool emb_tab_fwd_ok(const DecP& p) { return (p.A + 1) * 64 * 4 <= p.NRP * 128; }
+__device__ __forceinline__ bool emb_tab_bwd_ok(const DecP& p) { return (p.A + 1) * (2 * 64 + 1) * 4 <= 2 * p.NRP * 128; }
+
 // ------------------------------------------------------------------------------------------ cross attention
 // cross-attention projections: q = W_q rep (from global f32), k / v = W_k x1, W_v x1 (x1 = xr, or the saved x1 when
 // xr is null) -> QB / KB / VB; x1 optionally saved (forward) or staged into XB (backward, X of dW_k / dW_v)
@@ -600,12 +633,25 @@ template <int NB, bool SAVE, int MA, bool CONT>
 __device__ __forceinline__ void dec_fwd_tile(const DecP& p, char* smem, int seq0, int nseq) {
   const Ctx c = make_ctx(p, smem, seq0, nseq);
   if (c.nseq <= 0) return;
-  zero_lds(smem, ct_fwd_lds_bytes(p.NRP), c.tid);
+  zero_pad_rows_fwd(c);
   __syncthreads();
   CP_MARK(0);
   const int lane = c.lane;
   CT xr[MAXRT];
-  {
+  if (!CONT && emb_tab_fwd_ok(p)) {   // x0 rows from the per-token table (in QB until the first projection)
+    float* X0 = (float*)c.QB;
+    emb_table(p, X0, nullptr, nullptr, true, c);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {
+      const int rt = c.wave + NW * k;
+      if (rt < c.NT) {
+        const int row = rt * 16 + (lane & 15);
+        const int tk = row < c.NR ? dec_token_ct(p, c.tok0 + row, row % c.L) : 0;
+        xr[k] = emb_row(X0, tk, lane);
+      }
+    }
+  } else {
     const CT gam = ld_vec(p.lnd_g, lane), bet = ld_vec(p.lnd_b, lane);
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
@@ -674,15 +720,33 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
     ct_zero(dlb);
     const CT gam = ld_vec(p.lnd_g, lane), bet = ld_vec(p.lnd_b, lane);
     const int g = lane >> 4;
+    const bool tab = emb_tab_bwd_ok(p);   // x-hat / GELU' / rstd per token id in QB + KB (free after the blocks)
+    float* XT = (float*)c.QB;
+    float* GT = XT + (p.A + 1) * 64;
+    float* RT = GT + (p.A + 1) * 64;
+    if (tab) {
+      emb_table(p, XT, GT, RT, false, c);
+      __syncthreads();
+    }
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
       const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         const bool ok = tok_ok(rt, c);
         int tk;
-        CT e = dec_embed_pre_ct<CONT>(p, rt, tk, c), egp, xh, yy, de;
-        gelu_ct_both(e, egp);
-        const float rs = ln_fwd_ct(e, xh, yy, gam, bet);
+        CT egp, xh, de;
+        float rs;
+        if (tab) {
+          const int row = rt * 16 + (lane & 15);
+          tk = row < c.NR ? dec_token_ct(p, c.tok0 + row, row % c.L) : 0;
+          xh = emb_row(XT, tk, lane);
+          egp = emb_row(GT, tk, lane);
+          rs = RT[tk];
+        } else {
+          CT e = dec_embed_pre_ct<CONT>(p, rt, tk, c), yy;
+          gelu_ct_both(e, egp);
+          rs = ln_fwd_ct(e, xh, yy, gam, bet);
+        }
         ln_bwd_ct(dx[k], xh, rs, gam, ok, de, dlg, dlb);
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt)
@@ -717,15 +781,33 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
     ct_zero(dlb);
     const CT gam = ld_vec(p.lnd_g, lane), bet = ld_vec(p.lnd_b, lane);
     const int g = lane >> 4;
+    const bool tab = emb_tab_bwd_ok(p);   // x-hat / GELU' / rstd per token id in QB + KB (free after the blocks)
+    float* XT = (float*)c.QB;
+    float* GT = XT + (p.A + 1) * 64;
+    float* RT = GT + (p.A + 1) * 64;
+    if (tab) {
+      emb_table(p, XT, GT, RT, false, c);
+      __syncthreads();
+    }
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
       const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         const bool ok = tok_ok(rt, c);
         int tk;
-        CT e = dec_embed_pre_ct<CONT>(p, rt, tk, c), egp, xh, yy, de;
-        gelu_ct_both(e, egp);
-        const float rs = ln_fwd_ct(e, xh, yy, gam, bet);
+        CT egp, xh, de;
+        float rs;
+        if (tab) {
+          const int row = rt * 16 + (lane & 15);
+          tk = row < c.NR ? dec_token_ct(p, c.tok0 + row, row % c.L) : 0;
+          xh = emb_row(XT, tk, lane);
+          egp = emb_row(GT, tk, lane);
+          rs = RT[tk];
+        } else {
+          CT e = dec_embed_pre_ct<CONT>(p, rt, tk, c), yy;
+          gelu_ct_both(e, egp);
+          rs = ln_fwd_ct(e, xh, yy, gam, bet);
+        }
         ln_bwd_ct(dx[k], xh, rs, gam, ok, de, dlg, dlb);
         if (ok) {   // EMB[k][f] += d pre_f * a_prev_k (k < A), EMB[A][f] += d pre_f (bias)
           const int row = rt * 16 + (lane & 15);

@@ -94,7 +94,7 @@ template <int NB, bool SAVE>
 __device__ __forceinline__ void enc_fwd_tile(const EncP& p, const EncX& ex, char* smem, int seq0, int nseq) {
   const Ctx c = make_ctx(p, smem, seq0, nseq);
   if (c.nseq <= 0) return;
-  zero_lds(smem, ct_fwd_lds_bytes(p.NRP), c.tid);
+  zero_pad_rows_fwd(c);
   __syncthreads();
   CP_MARK(0);
   const int lane = c.lane, g = lane >> 4;
