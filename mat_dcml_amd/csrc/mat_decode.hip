@@ -212,19 +212,20 @@ __device__ __forceinline__ void attention_mfma(const bf16_t* KV, int rowK, int r
       for (int i = 0; i < 4; ++i) sc[4 * t + i] = r[i];
     }
     float cm = -INFINITY;
+    const int d0 = iq - kb - 8 * g;   // key j visible iff j <= d0
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      sc[j] = kb + 8 * g + j <= iq ? sc[j] * SL2 : -INFINITY;
+      sc[j] = j <= d0 ? sc[j] : -INFINITY;   // raw scores; the scale goes into the exp2 argument (one FMA)
       cm = fmaxf(cm, sc[j]);
     }
-    const float nm = fmaxf(m, xrow_max(cm));
+    const float nm = fmaxf(m, xrow_max(cm) * SL2);
     const float mr = nm == -INFINITY ? 0.f : nm;
-    const float alpha = exp2f(m - mr);
+    const float alpha = fast_exp2(m - mr);   // raw v_exp_f32 (exp2f's denormal-safe sequence is 7 VALU)
     float ps = 0.f;
     uint32_t hi[4], lo[4];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      sc[j] = exp2f(sc[j] - mr);
+      sc[j] = fast_exp2(fmaf(sc[j], SL2, -mr));
       ps += sc[j];
     }
 #pragma unroll
