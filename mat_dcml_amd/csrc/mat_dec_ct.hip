@@ -781,33 +781,15 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
     ct_zero(dlb);
     const CT gam = ld_vec(p.lnd_g, lane), bet = ld_vec(p.lnd_b, lane);
     const int g = lane >> 4;
-    const bool tab = emb_tab_bwd_ok(p);   // x-hat / GELU' / rstd per token id in QB + KB (free after the blocks)
-    float* XT = (float*)c.QB;
-    float* GT = XT + (p.A + 1) * 64;
-    float* RT = GT + (p.A + 1) * 64;
-    if (tab) {
-      emb_table(p, XT, GT, RT, false, c);
-      __syncthreads();
-    }
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
       const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         const bool ok = tok_ok(rt, c);
         int tk;
-        CT egp, xh, de;
-        float rs;
-        if (tab) {
-          const int row = rt * 16 + (lane & 15);
-          tk = row < c.NR ? dec_token_ct(p, c.tok0 + row, row % c.L) : 0;
-          xh = emb_row(XT, tk, lane);
-          egp = emb_row(GT, tk, lane);
-          rs = RT[tk];
-        } else {
-          CT e = dec_embed_pre_ct<CONT>(p, rt, tk, c), yy;
-          gelu_ct_both(e, egp);
-          rs = ln_fwd_ct(e, xh, yy, gam, bet);
-        }
+        CT e = dec_embed_pre_ct<CONT>(p, rt, tk, c), egp, xh, yy, de;
+        gelu_ct_both(e, egp);
+        const float rs = ln_fwd_ct(e, xh, yy, gam, bet);
         ln_bwd_ct(dx[k], xh, rs, gam, ok, de, dlg, dlb);
         if (ok) {   // EMB[k][f] += d pre_f * a_prev_k (k < A), EMB[A][f] += d pre_f (bias)
           const int row = rt * 16 + (lane & 15);
