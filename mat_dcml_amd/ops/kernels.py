@@ -93,7 +93,7 @@ def lib():
             if why is not None:
                 _load_error = f"native library still stale after a rebuild: {why}"
                 raise RuntimeError(_load_error)
-        BUILD_ID = build_identity(L)[0]
+        BUILD_ID = (build_identity(L) or ("unidentified",))[0]   # A/B variants may predate the identity
         _lib = L
         _declare(_lib)
     return _lib
