@@ -5,43 +5,93 @@ With ``--smac_backend sc2`` the SMAC runner drives real StarCraft II through ``s
 (``envs/vec/process_pool.py``), with the reference's per-agent obs / state / availability contract.  Neither
 package nor the game is installable in this image, so constructing it raises with instructions; the synthetic
 device env (``synthetic.py``) is the default backend.
+
+Protocol-error recovery (``StarCraft2_Env.py:422-423,468-472,507-530``): a ``ProtocolError`` / ``ConnectionError`` of
+the SC2 client during ``reset`` or ``step`` closes the game process and launches a new one (``full_restart``); a
+step that hit it ends the episode (every agent done, zero reward), and every info dict carries the running
+``restarts`` count as the reference's does (``:521,603``).  ``SC2Game`` takes the env constructor and the error
+types as arguments, so the recovery path is tested without the game (``tests/test_smac.py``).
 """
 from __future__ import annotations
+
+import numpy as np
+
+
+def _protocol_errors():
+    try:
+        from pysc2.lib import protocol  # noqa: WPS433 — present only on SC2 hosts
+        return (protocol.ProtocolError, protocol.ConnectionError)
+    except ImportError:
+        return (ConnectionError,)
+
+
+class SC2Game:
+    """One SMAC game with the reference's restart semantics.  ``make_env()`` builds a ``smac`` ``StarCraft2Env``
+    (or a stand-in with its API: get_env_info / reset / step / get_obs / get_state / get_avail_actions / close)."""
+
+    def __init__(self, make_env, errors=None, max_restarts_per_call=3):
+        self.make_env = make_env
+        self.errors = tuple(errors) if errors is not None else _protocol_errors()
+        self.max_restarts_per_call = max_restarts_per_call
+        self.force_restarts = 0
+        self.env = make_env()
+        info = self.env.get_env_info()
+        self.n_agents = info["n_agents"]
+        self.observation_space = [[info["obs_shape"]]] * self.n_agents
+        self.share_observation_space = [[info["state_shape"]]] * self.n_agents
+        from .synthetic import Discrete
+        self.action_space = [Discrete(info["n_actions"])] * self.n_agents
+
+    def full_restart(self):
+        """Close the game process and launch a new one (StarCraft2_Env.full_restart)."""
+        try:
+            self.env.close()
+        except Exception:   # noqa: BLE001 — the process is already gone
+            pass
+        self.env = self.make_env()
+        self.force_restarts += 1
+
+    def _observe(self):
+        obs = np.array(self.env.get_obs())
+        state = np.tile(self.env.get_state(), (self.n_agents, 1))
+        ava = np.array(self.env.get_avail_actions())
+        return obs, state, ava
+
+    def reset(self):
+        for attempt in range(self.max_restarts_per_call + 1):
+            try:
+                self.env.reset()
+                return self._observe()
+            except self.errors:
+                if attempt == self.max_restarts_per_call:
+                    raise
+                self.full_restart()
+
+    def step(self, actions):
+        acts = [int(a) for a in np.asarray(actions).reshape(-1)]
+        try:
+            r, done, info = self.env.step(acts)
+            obs, state, ava = self._observe()
+        except self.errors:
+            # the reference ends the episode on a protocol error after a full restart (StarCraft2_Env.py:507-530)
+            self.full_restart()
+            obs, state, ava = self.reset()
+            r, done, info = 0.0, True, {}
+        info = dict(info or {})
+        info["restarts"] = self.force_restarts
+        dones = np.array([bool(done)] * self.n_agents)
+        return obs, state, np.full((self.n_agents, 1), float(r)), dones, [dict(info) for _ in range(self.n_agents)], ava
+
+    def close(self):
+        self.env.close()
 
 
 def _sc2_env_factory(map_name, seed):
     def make():
-        from smac.env import StarCraft2Env  # noqa: WPS433 — external dependency, present only on SC2 hosts
-
-        class _Wrap:
-            def __init__(self):
-                self.env = StarCraft2Env(map_name=map_name, seed=seed)
-                info = self.env.get_env_info()
-                self.n_agents = info["n_agents"]
-                self.observation_space = [[info["obs_shape"]]] * self.n_agents
-                self.share_observation_space = [[info["state_shape"]]] * self.n_agents
-                from .synthetic import Discrete
-                self.action_space = [Discrete(info["n_actions"])] * self.n_agents
-
-            def reset(self):
-                import numpy as np
-                self.env.reset()
-                obs = np.array(self.env.get_obs())
-                state = np.tile(self.env.get_state(), (self.n_agents, 1))
-                ava = np.array(self.env.get_avail_actions())
-                return obs, state, ava
-
-            def step(self, actions):
-                import numpy as np
-                r, done, info = self.env.step([int(a) for a in np.asarray(actions).reshape(-1)])
-                obs, state, ava = np.array(self.env.get_obs()), np.tile(self.env.get_state(), (self.n_agents, 1)), \
-                    np.array(self.env.get_avail_actions())
-                dones = np.array([done] * self.n_agents)
-                return obs, state, np.full((self.n_agents, 1), r), dones, [info] * self.n_agents, ava
-
-            def close(self):
-                self.env.close()
-        return _Wrap()
+        def make_env():
+            from smac.env import StarCraft2Env  # noqa: WPS433 — external dependency, present only on SC2 hosts
+            return StarCraft2Env(map_name=map_name, seed=seed)
+        return SC2Game(make_env)
     return make
 
 

@@ -79,3 +79,57 @@ def test_process_pool_vec_env():
         assert done.all() and torch.allclose(obs[:, 0, 0], torch.arange(5.0))   # auto-reset after 3 steps
     finally:
         pool.close()
+
+
+class _FlakySC2:
+    """Stand-in for smac's StarCraft2Env: raises a protocol error on chosen step calls (per game instance)."""
+    launches = 0
+
+    def __init__(self, fail_on=()):
+        _FlakySC2.launches += 1
+        self.fail_on, self.t = set(fail_on), 0
+
+    def get_env_info(self):
+        return {"n_agents": 3, "obs_shape": 5, "state_shape": 7, "n_actions": 4}
+
+    def reset(self):
+        self.t = 0
+
+    def step(self, actions):
+        self.t += 1
+        if self.t in self.fail_on:
+            raise ConnectionError("SC2 protocol error")
+        return 1.0, False, {"battle_won": False}
+
+    def get_obs(self):
+        return [np.full(5, self.t, np.float32)] * 3
+
+    def get_state(self):
+        return np.zeros(7, np.float32)
+
+    def get_avail_actions(self):
+        return [[1, 1, 1, 1]] * 3
+
+    def close(self):
+        pass
+
+
+def test_sc2_protocol_error_full_restart():
+    """StarCraft2_Env.py:468-472,507-530: a protocol error in step relaunches the game, ends the episode (every agent
+    done, zero reward) and the running restart count is in every info dict."""
+    from mat_dcml_amd.envs.smac.adapter import SC2Game
+    made = []
+
+    def make_env():
+        made.append(_FlakySC2(fail_on=(2,) if not made else ()))
+        return made[-1]
+    g = SC2Game(make_env, errors=(ConnectionError,))
+    obs, state, ava = g.reset()
+    assert obs.shape == (3, 5) and state.shape == (3, 7) and ava.shape == (3, 4)
+    o, s, r, d, info, a = g.step([0, 1, 2])
+    assert not d.any() and r[0, 0] == 1.0 and info[0]["restarts"] == 0
+    o, s, r, d, info, a = g.step([0, 1, 2])          # the first game fails on its 2nd step
+    assert d.all() and r[0, 0] == 0.0 and all(i["restarts"] == 1 for i in info) and len(made) == 2
+    assert (o == 0).all()                             # a fresh episode of the relaunched game
+    o, s, r, d, info, a = g.step([0, 1, 2])
+    assert not d.any() and info[0]["restarts"] == 1
