@@ -121,7 +121,6 @@ def main():
     runner = DCMLRunner({"all_args": args, "device": comm.device, "run_dir": None, "comm": comm})
     runner.warmup()
     dev = comm.device
-    paths = kernel_report(runner)
 
     def sync():
         if dev.type == "cuda":
@@ -129,6 +128,7 @@ def main():
 
     for _ in range(a.warmup):
         runner.train_iteration()
+    paths = kernel_report(runner)   # after the warm-up: the decode entry names the kernel its calls ran on
     # phase breakdown of the timed steps: hipEvent pairs recorded in the stream (no sync inside the loop), resolved
     # once after the timed region (utils/timers.PhaseTimers)
     runner.timers.enabled = not a.no_phase_timers

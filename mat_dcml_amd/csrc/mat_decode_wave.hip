@@ -1,0 +1,598 @@
+// mat_decode_wave — the rollout's autoregressive action decode with ONE wave per env (gfx950 / CDNA4).
+//
+// Reference hot loop: L decoder passes per env step (mat_src/mat/algorithms/utils/transformer_act.py:76-99), here one
+// agent row per pass against K / V caches of the earlier rows (exact: row i depends only on the shifted actions 0..i).
+//
+// Why one wave: the 4-wave kernel (mat_decode.hip) splits every 64x64 product over the waves of a workgroup and so
+// needs an LDS exchange + workgroup barrier between consecutive products — ~9 barrier-separated phases per decoder
+// block; its waves spent 53 % of their cycles waiting (profiles/r3_check1/decode_pmc.txt).  Here one wave owns an
+// env and runs the whole chain in registers, in the token-on-lane ("CT") layout of the training kernels
+// (mat_train_ct.h): Yᵀ = W·Xᵀ with the weight as the MFMA A operand in a permuted k order, so each product's C
+// registers, packed to bf16, ARE the next product's B operand — linear → bias → residual → LayerNorm → linear chains
+// never leave the registers and no barrier exists anywhere in the agent loop.
+//
+// The live agent row is replicated over the 16 token columns of the tile, which buys two things:
+//  * attention of BOTH heads in one instruction stream: columns 0..7 carry head 0's query (k-step 0 = dims 0..31),
+//    columns 8..15 head 1's (k-step 1), so one online-softmax pass serves both heads; a bank-masked DPP row_ror:8
+//    then hands each column the other head's half of O;
+//  * elementwise work split over the row: for GELU, lane c evaluates ONE of its 16 features (feature 16(c>>2) + 4g +
+//    (c&3)) and 16 DPP row_newbcast moves give every lane all 16 results (1 erf per lane instead of 16).
+// Weights: the 64x64 A fragments (the training kernels' "fa" pack) live in LDS — the last NREG of the agent loop's
+// matrices in registers when LDS is short (n_block 2) — biases / LayerNorm vectors / token tables in LDS, the K / V
+// caches of every block in one token-major swizzled LDS array (tile.h tmo) as in the 4-wave kernel.  Block 0's
+// self-attention q / K / V come from the per-token table (they depend only on the previous action), the
+// cross-attention queries W_q2 rep_i are precomputed before the agent loop, the head LayerNorm is folded into the
+// logit product (DecParams.hfold), sampling noise comes from in-kernel Philox (same streams as mat_decode.hip).
+#define MDL_LN_ONEPASS
+#include "mat_train_ct.h"
+#include "decode_params.h"
+
+namespace {
+
+// Debug build (-DMDL_WAVE_DEBUG): the replicated CT vectors of env 0 at row g_wdbg_row after every stage -> g_wdbg
+// (read back by mdl_wave_debug_read; scripts/wave_debug.py compares them with the torch decoder)
+#ifdef MDL_WAVE_DEBUG
+__device__ float g_wdbg[16][64];
+__device__ int g_wdbg_row;
+__device__ __forceinline__ void wdbg(int stage, const CT& x, int i, int lane) {
+  if (blockIdx.x == 0 && i == g_wdbg_row && (lane & 15) == 0) {
+    const int g = lane >> 4;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) g_wdbg[stage][16 * mt + 4 * g + r] = x.v[mt][r];
+  }
+}
+#define WDBG(st, x) wdbg(st, x, i, lane)
+#else
+#define WDBG(st, x) do { } while (0)
+#endif
+
+// ------------------------------------------------------------------------------------------ weight slots
+// Matrices the agent loop multiplies by (block 0: proj1, k2, v2, proj2, mlp0, mlp2; block b > 0 adds q1, k1, v1;
+// then the head's first linear), in loop order.  Slot -> decoder linear index (ops/mat_train.decoder_linears: per
+// block q1 k1 v1 p1 q2 k2 v2 p2 m0 m2, then head[0]).
+__host__ __device__ constexpr int wv_nm(int NB) { return 6 + 9 * (NB - 1) + 1; }
+__host__ __device__ constexpr int wv_lin(int NB, int s) {
+  return s < 6 ? (s == 0 ? 3 : s + 4)
+               : (s == wv_nm(NB) - 1 ? 10 * NB
+                                     : 10 * (1 + (s - 6) / 9) + ((s - 6) % 9 < 4 ? (s - 6) % 9 : (s - 6) % 9 + 1));
+}
+__host__ __device__ constexpr int wv_slot(int b, int k) {   // k = linear within block b (never 4 = q2; b = 0: k >= 3)
+  return b == 0 ? (k == 3 ? 0 : k - 4) : 6 + 9 * (b - 1) + (k < 4 ? k : k - 1);
+}
+
+struct WvLds { int w, kv, q2, qt, et, bi, lp, sc, total; };   // byte offsets of the LDS carve
+__host__ __device__ inline WvLds wv_lds(int NB, int L, int n_tok, int nlds) {
+  WvLds o;
+  int off = 0;
+  auto take = [&](int bytes) { const int r = off; off += (bytes + 15) & ~15; return r; };
+  o.w = take(nlds * 8192);                   // [slot][4096] bf16 A fragments
+  o.kv = take((NB * 4 * L + 32) * 128);      // K / V caches (+ 32 zero rows: 32-key chunks read past the last cache)
+  o.q2 = take(NB * L * 128);                 // [block][row][64] bf16 cross-attention queries
+  o.qt = take(n_tok * 3 * 128);              // [token][q, k, v][64] bf16 block-0 self-attention operands
+  o.et = take(n_tok * 256);                  // [token][64] f32 embedded decoder input rows (the block-0 residual)
+  o.bi = take((10 * NB + 1) * 256);          // biases
+  o.lp = take((3 * NB + 1) * 512);           // LayerNorm gamma / beta
+  o.sc = take(64 * 4);                       // logits of the wide head
+  o.total = off;
+  return o;
+}
+
+__device__ __forceinline__ int wv_kvrow(int b, int kind, int j, int L) { return (b * 4 + kind) * L + j; }
+
+template <int N>
+struct RegW { AFr w[N > 0 ? N : 1]; };
+
+template <int S, int NLDS, int NREG>
+__device__ __forceinline__ void wv_getw(AFr& w, const RegW<NREG>& rw, const bf16_t* W, int lane) {
+  if constexpr (S >= NLDS) {
+    w = rw.w[S - NLDS];
+  } else {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) w.f[mt][s] = *(const bf16x8*)(W + (size_t)S * 4096 + ((mt * 2 + s) * 64 + lane) * 8);
+  }
+}
+
+// 8 bytes (4 bf16) of a token-major swizzled row
+__device__ __forceinline__ uint2 kv_ld2(const bf16_t* KV, int row, int col) { return *(const uint2*)(KV + tmo(row, col)); }
+// this lane's CT pieces of a token row -> swizzled KV row (the live row is replicated over the columns: column 0 writes)
+__device__ __forceinline__ void kv_st_row(bf16_t* KV, int row, const CTr& x, int lane) {
+  if ((lane & 15) == 0) {
+    const int g = lane >> 4;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) *(uint2*)(KV + tmo(row, 16 * mt + 4 * g)) = x.q[mt];
+  }
+}
+
+template <int N>
+__device__ __forceinline__ float row_bcast(float x) {   // lane N of each 16-lane row -> the whole row
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x150 + N, 0xF, 0xF, false));
+}
+// lanes of the enabled banks take lane (c + 8) & 15's value, the others keep their own.  Elements go through a
+// scalar: hipcc lowers __builtin_bit_cast(int, v[r]) of an ext-vector element as element 0 for every r (all four
+// results became element 0's), so never bit_cast a subscripted vector element.
+template <int BANKS>
+__device__ __forceinline__ float ror8_bank(float x) {
+  const int a = __builtin_bit_cast(int, x);
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(a, a, 0x128, 0xF, BANKS, false));
+}
+template <int BANKS>
+__device__ __forceinline__ f32x4 ror8_banks(f32x4 v) {
+  return f32x4{ror8_bank<BANKS>(v.x), ror8_bank<BANKS>(v.y), ror8_bank<BANKS>(v.z), ror8_bank<BANKS>(v.w)};
+}
+
+// GELU of a replicated CT vector with one erf per lane: lane c evaluates feature 16(c>>2) + 4g + (c&3), the row
+// broadcasts hand every lane its 16 results
+__device__ __forceinline__ CT gelu_dist(const CT& h, int lane) {
+  const int c = lane & 15;
+  const f32x4 a = (c & 4) ? h.v[1] : h.v[0];
+  const f32x4 b = (c & 4) ? h.v[3] : h.v[2];
+  const f32x4 v = (c & 8) ? b : a;
+  const float lo = (c & 1) ? v[1] : v[0], hi = (c & 1) ? v[3] : v[2];
+  const float ge = gelu_erf((c & 2) ? hi : lo);
+  CT o;
+  o.v[0] = f32x4{row_bcast<0>(ge), row_bcast<1>(ge), row_bcast<2>(ge), row_bcast<3>(ge)};
+  o.v[1] = f32x4{row_bcast<4>(ge), row_bcast<5>(ge), row_bcast<6>(ge), row_bcast<7>(ge)};
+  o.v[2] = f32x4{row_bcast<8>(ge), row_bcast<9>(ge), row_bcast<10>(ge), row_bcast<11>(ge)};
+  o.v[3] = f32x4{row_bcast<12>(ge), row_bcast<13>(ge), row_bcast<14>(ge), row_bcast<15>(ge)};
+  return o;
+}
+
+// Causal attention of the live row i over cache rows 0..i (K rows rK + j, V rows rV + j), both heads at once:
+// column c carries head c >> 3.  Scores Sᵀ = K·Qᵀ per 16-key half t (A rows = keys kb + pi_row(t, m), k = the
+// head's 32 dims in the CT permuted order, so the query is its CT registers), online softmax in log2 units, P as a
+// hi/lo bf16 pair, Oᵀ = Vᵀ·Pᵀ with Vᵀ from ds_read_b64_tr_b16; O returned in CT layout (replicated).
+__device__ __forceinline__ CT wv_attn(const bf16_t* KV, int rK, int rV, const CTr& qr, int i, int lane) {
+  const int g = lane >> 4, c = lane & 15;
+  const bool h1 = c >= 8;
+  const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+  const bf16x8 qb0 = h1 ? z8 : rb(qr, 0), qb1 = h1 ? rb(qr, 1) : z8;
+  float m = -INFINITY, l = 0.f;
+  f32x4 o[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) o[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int kb = 0; kb <= i; kb += 32) {
+    float sc[8];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int key = rK + kb + pi_row(t, c);
+      const uint2 p0 = kv_ld2(KV, key, 4 * g), p1 = kv_ld2(KV, key, 16 + 4 * g);
+      const uint2 p2 = kv_ld2(KV, key, 32 + 4 * g), p3 = kv_ld2(KV, key, 48 + 4 * g);
+      f32x4 r = __builtin_amdgcn_mfma_f32_16x16x32_bf16(mk8(p0.x, p0.y, p1.x, p1.y), qb0, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      r = __builtin_amdgcn_mfma_f32_16x16x32_bf16(mk8(p2.x, p2.y, p3.x, p3.y), qb1, r, 0, 0, 0);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) sc[4 * t + rr] = r[rr];
+    }
+    const int d0 = i - kb - 8 * g;   // key kb + 8g + j is visible iff j <= d0
+    float cm = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sc[j] = j <= d0 ? sc[j] : -INFINITY;
+      cm = fmaxf(cm, sc[j]);
+    }
+    const float nm = fmaxf(m, cross_row_max(cm) * ATT_L2);   // finite: key kb <= i is visible
+    const float alpha = fast_exp2(m - nm);
+    float ps = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sc[j] = fast_exp2(fmaf(sc[j], ATT_L2, -nm));
+      ps += sc[j];
+    }
+    l = l * alpha + ps;
+    bf16x8 ph, pl;
+    split8v(sc, ph, pl);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const bf16x8 va = ld_frag_T(KV, rV + kb, 16 * mt, lane);
+      o[mt] *= alpha;
+      o[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, ph, o[mt], 0, 0, 0);
+      o[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pl, o[mt], 0, 0, 0);
+    }
+    m = nm;
+  }
+  const float il = 1.f / cross_row_sum(l);
+#ifdef MDL_WAVE_DEBUG
+  if (rK == 0) {   // block 0 self attention: the cached V row 0 (CT read) and O before the head exchange
+    CT vr, pre;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const uint2 u = kv_ld2(KV, rV, 16 * mt + 4 * g);
+      vr.v[mt] = f32x4{blo(u.x), bhi(u.x), blo(u.y), bhi(u.y)};
+      pre.v[mt] = o[mt] * il;
+    }
+    wdbg(14, vr, i, lane);
+    wdbg(15, pre, i, lane);
+  }
+#endif
+  CT O;
+  // columns c < 8 hold head 0 (dims 0..31 = mt 0, 1), c >= 8 head 1 (mt 2, 3): each takes the other half from c ^ 8
+  O.v[0] = ror8_banks<0xC>(o[0] * il);
+  O.v[1] = ror8_banks<0xC>(o[1] * il);
+  O.v[2] = ror8_banks<0x3>(o[2] * il);
+  O.v[3] = ror8_banks<0x3>(o[3] * il);
+  return O;
+}
+
+struct WvCtx {
+  bf16_t *W, *KV, *Q2, *QT;
+  float *ET, *BI, *LP;
+  int lane, L;
+};
+
+// one decoder block for the live row i (ma_transformer.py:95-98): x <- LN1(x + attn1(x)); x <- LN2(rep_i + attn2(q =
+// rep_i, k = v = x)); x <- LN3(x + mlp(x)).  Block 0's q / K / V of x come from the token table (x = ET[tok]).
+template <int B, int NB, int NLDS, int NREG>
+__device__ __forceinline__ void wv_block(CT& x, const WvCtx& k, const RegW<NREG>& rw, int i, int tok, const CT& repi) {
+  const int lane = k.lane, g = lane >> 4, L = k.L;
+  CT xh;
+  AFr w;
+  CTr qr;
+  if constexpr (B == 0) {
+    const bf16_t* t = k.QT + tok * 192;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) qr.q[mt] = *(const uint2*)(t + 16 * mt + 4 * g);
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        *(uint2*)(k.KV + tmo(wv_kvrow(0, 0, i, L), 16 * mt + 4 * g)) = *(const uint2*)(t + 64 + 16 * mt + 4 * g);
+        *(uint2*)(k.KV + tmo(wv_kvrow(0, 1, i, L), 16 * mt + 4 * g)) = *(const uint2*)(t + 128 + 16 * mt + 4 * g);
+      }
+    }
+    x = ld_vec(k.ET + tok * 64, lane);
+  } else {
+    const CTr xp = ct_pack(x);
+    CT q = ld_vec(k.BI + 64 * (10 * B + 0), lane), kk = ld_vec(k.BI + 64 * (10 * B + 1), lane);
+    CT vv = ld_vec(k.BI + 64 * (10 * B + 2), lane);
+    wv_getw<wv_slot(B, 0), NLDS, NREG>(w, rw, k.W, lane);
+    mm(q, w, xp);
+    wv_getw<wv_slot(B, 1), NLDS, NREG>(w, rw, k.W, lane);
+    mm(kk, w, xp);
+    wv_getw<wv_slot(B, 2), NLDS, NREG>(w, rw, k.W, lane);
+    mm(vv, w, xp);
+    qr = ct_pack(q);
+    kv_st_row(k.KV, wv_kvrow(B, 0, i, L), ct_pack(kk), lane);
+    kv_st_row(k.KV, wv_kvrow(B, 1, i, L), ct_pack(vv), lane);
+  }
+  asm volatile("" ::: "memory");   // the cache row above is read back by other lanes below (LDS is in order per wave)
+  WDBG(6 * B + 0, x);
+  {
+    const CT O = wv_attn(k.KV, wv_kvrow(B, 0, 0, L), wv_kvrow(B, 1, 0, L), qr, i, lane);
+    WDBG(6 * B + 1, O);
+    wv_getw<wv_slot(B, 3), NLDS, NREG>(w, rw, k.W, lane);
+    CT t = ct_add(ld_vec(k.BI + 64 * (10 * B + 3), lane), x);
+    mm(t, w, ct_pack(O));
+    ln_fwd_ct(t, xh, x, ld_vec(k.LP + (3 * B + 0) * 128, lane), ld_vec(k.LP + (3 * B + 0) * 128 + 64, lane));
+  }
+  {   // cross-attention K / V of x1
+    const CTr xp = ct_pack(x);
+    CT kk = ld_vec(k.BI + 64 * (10 * B + 5), lane), vv = ld_vec(k.BI + 64 * (10 * B + 6), lane);
+    wv_getw<wv_slot(B, 5), NLDS, NREG>(w, rw, k.W, lane);
+    mm(kk, w, xp);
+    wv_getw<wv_slot(B, 6), NLDS, NREG>(w, rw, k.W, lane);
+    mm(vv, w, xp);
+    kv_st_row(k.KV, wv_kvrow(B, 2, i, L), ct_pack(kk), lane);
+    kv_st_row(k.KV, wv_kvrow(B, 3, i, L), ct_pack(vv), lane);
+  }
+  asm volatile("" ::: "memory");
+  {
+    CTr q2;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) q2.q[mt] = *(const uint2*)(k.Q2 + (size_t)(B * L + i) * 64 + 16 * mt + 4 * g);
+    WDBG(6 * B + 2, x);
+    const CT O = wv_attn(k.KV, wv_kvrow(B, 2, 0, L), wv_kvrow(B, 3, 0, L), q2, i, lane);
+    WDBG(6 * B + 3, O);
+    wv_getw<wv_slot(B, 7), NLDS, NREG>(w, rw, k.W, lane);
+    CT t = ct_add(ld_vec(k.BI + 64 * (10 * B + 7), lane), repi);
+    mm(t, w, ct_pack(O));
+    ln_fwd_ct(t, xh, x, ld_vec(k.LP + (3 * B + 1) * 128, lane), ld_vec(k.LP + (3 * B + 1) * 128 + 64, lane));
+  }
+  {   // MLP
+    CT h = ld_vec(k.BI + 64 * (10 * B + 8), lane);
+    wv_getw<wv_slot(B, 8), NLDS, NREG>(w, rw, k.W, lane);
+    mm(h, w, ct_pack(x));
+    WDBG(6 * B + 4, x);
+    const CTr hp = ct_pack(gelu_dist(h, lane));
+    wv_getw<wv_slot(B, 9), NLDS, NREG>(w, rw, k.W, lane);
+    CT t = ct_add(ld_vec(k.BI + 64 * (10 * B + 9), lane), x);
+    mm(t, w, hp);
+    ln_fwd_ct(t, xh, x, ld_vec(k.LP + (3 * B + 2) * 128, lane), ld_vec(k.LP + (3 * B + 2) * 128 + 64, lane));
+    WDBG(6 * B + 5, x);
+  }
+}
+
+// inclusive prefix sum over the 64 lanes (DPP row shifts, then the lower rows' totals)
+__device__ __forceinline__ float wv_incl_scan(float x, int lane) {
+  x += dppf<0x111>(x);
+  x += dppf<0x112>(x);
+  x += dppf<0x114>(x);
+  x += dppf<0x118>(x);
+  const float t0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 15));
+  const float t1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 31));
+  const float t2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 47));
+  const int r = lane >> 4;
+  return x + ((r >= 1 ? t0 : 0.f) + (r >= 2 ? t1 : 0.f) + (r >= 3 ? t2 : 0.f));
+}
+__device__ __forceinline__ float rdlane(float x, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
+}
+
+template <int NB, int NREG, bool WIDE>
+__global__ __launch_bounds__(64, 1) void mat_decode_wave_kernel(DecParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NM = wv_nm(NB), NLDS = NM - NREG;
+  constexpr int MA = WIDE ? 4 : 1;   // logit tiles (A <= 4: one tile, the logits sit in lanes g = 0)
+  const int lane = threadIdx.x, g = lane >> 4, c = lane & 15;
+  const int env = blockIdx.x, L = p.L, A = p.act_dim;
+  const WvLds lo = wv_lds(NB, L, p.n_tok, NLDS);
+  bf16_t* W = (bf16_t*)(smem + lo.w);
+  bf16_t* KV = (bf16_t*)(smem + lo.kv);
+  bf16_t* Q2 = (bf16_t*)(smem + lo.q2);
+  bf16_t* QT = (bf16_t*)(smem + lo.qt);
+  float* ET = (float*)(smem + lo.et);
+  float* BI = (float*)(smem + lo.bi);
+  float* LP = (float*)(smem + lo.lp);
+  float* SC = (float*)(smem + lo.sc);
+
+  // ---------------------------------------------------------------- setup: weights, tables, caches
+#pragma unroll 1
+  for (int s = 0; s < NLDS; ++s) {
+    const uint4* src = (const uint4*)(p.wfa + (size_t)wv_lin(NB, s) * 4096);
+    uint4* dst = (uint4*)(W + (size_t)s * 4096);
+    uint4 t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = src[lane + 64 * j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dst[lane + 64 * j] = t[j];
+  }
+  RegW<NREG> rw;
+#pragma unroll
+  for (int r = 0; r < NREG; ++r) loadA(rw.w[r], p.wfa + (size_t)wv_lin(NB, NLDS + r) * 4096, lane);
+  for (int i = lane; i < p.n_tok * 192; i += 64) QT[i] = f2bf(p.qkv0[i]);
+  for (int i = lane; i < p.n_tok * 64; i += 64) ET[i] = p.emb[i];
+  for (int i = lane; i < (10 * NB + 1) * 64; i += 64) BI[i] = p.bias[i];
+  for (int i = lane; i < (3 * NB + 1) * 128; i += 64) LP[i] = p.lnp[i];
+  for (int i = lane * 8; i < (NB * 4 * L + 32) * 64; i += 512) *(uint4*)(KV + i) = make_uint4(0, 0, 0, 0);
+  // folded head: W' = W_h2 diag(gamma_h) as hi / lo A fragments (rows = actions 16 ma + c, k in the CT order), and
+  // G_a = Σ W'[a], C_a = W_h2 beta_h + b_h2 for this lane's logit slots a = 16 ma + 4 g + r
+  bf16x8 HH[MA][2], HL[MA][2];
+  f32x4 HG[MA], HC[MA];
+#pragma unroll
+  for (int ma = 0; ma < MA; ++ma) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int a = 16 * ma + c, kk = 32 * s + 16 * (j >> 2) + 4 * g + (j & 3);
+        const float wv = a < A ? p.hfold[(a < A ? a : 0) * 64 + kk] : 0.f;
+        const bf16_t h = f2bf(wv);
+        HH[ma][s][j] = (short)h;
+        HL[ma][s][j] = (short)f2bf(wv - bf2f(h));
+      }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int a = 16 * ma + 4 * g + r;
+      HG[ma][r] = a < A ? p.hfold[A * 64 + a] : 0.f;
+      HC[ma][r] = a < A ? p.hfold[A * 65 + a] : 0.f;
+    }
+  }
+  // cross-attention queries of every row and block: q2 = W_q2 rep + b (bf16, as the 4-wave kernel rounds them)
+  const float* rep = p.rep + (size_t)env * L * 64;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    AFr wq;
+    loadA(wq, p.wfa + (size_t)(10 * b + 4) * 4096, lane);
+    const CT bq = ld_vec(p.bias + (10 * b + 4) * 64, lane);
+    for (int t0 = 0; t0 < L; t0 += 16) {
+      const int row = t0 + c;
+      CT xr;
+      if (row < L) xr = ld_vec(rep + (size_t)row * 64, lane); else ct_zero(xr);
+      CT q = bq;
+      mm(q, wq, ct_pack(xr));
+      const CTr qp = ct_pack(q);
+      if (row < L) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) *(uint2*)(Q2 + (size_t)(b * L + row) * 64 + 16 * mt + 4 * g) = qp.q[mt];
+      }
+    }
+  }
+  // sampling noise of every row: lane j holds row j (+ 64, + 128); the Normal draw of the semi-discrete last row
+  const int n_disc = p.n_disc;
+  const bool det = p.deterministic != 0;
+  float U[3] = {0.f, 0.f, 0.f};
+  float zlast = 0.f;
+  if (!det) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int row = lane + 64 * q;
+      if (row < n_disc) U[q] = p.gen ? draw_u(p, env, row) : p.rnd_u[(size_t)env * L + row];
+    }
+    if (n_disc < L) zlast = p.gen ? draw_n(p, env, L - 1, A - 1) : p.rnd_n[((size_t)env * L + L - 1) * A + A - 1];
+  }
+  __syncthreads();
+
+  // ---------------------------------------------------------------- agent loop
+  const WvCtx k{W, KV, Q2, QT, ET, BI, LP, lane, L};
+  const float* ava = p.ava ? p.ava + (size_t)env * L * A : nullptr;
+  int tok = p.tok_start;
+#pragma unroll 1
+  for (int i = 0; i < L; ++i) {
+    // per-row inputs, requested before the block chain that hides their latency: rep_i (residual of the cross
+    // attention), the availability row (lane a = action a)
+    const CT repi = ld_vec(rep + (size_t)i * 64, lane);
+    const float avl = (ava && lane < A) ? ava[(size_t)i * A + lane] : 1.f;
+    CT x;
+    wv_block<0, NB, NLDS, NREG>(x, k, rw, i, tok, repi);
+    if constexpr (NB > 1) wv_block<1, NB, NLDS, NREG>(x, k, rw, i, tok, repi);
+    // ---- head: GELU(W_h1 x + b) -> folded LayerNorm -> logits (hi / lo MFMA products: fp32-like)
+    CT h = ld_vec(BI + 64 * (10 * NB), lane);
+    {
+      AFr w;
+      wv_getw<NM - 1, NLDS, NREG>(w, rw, W, lane);
+      mm(h, w, ct_pack(x));
+    }
+    h = gelu_dist(h, lane);
+    WDBG(12, h);
+    f32x4 s4 = (h.v[0] + h.v[1]) + (h.v[2] + h.v[3]);
+    f32x4 q4 = h.v[0] * h.v[0];
+#pragma unroll
+    for (int mt = 1; mt < 4; ++mt) q4 = h.v[mt] * h.v[mt] + q4;
+    const float mean = cross_row_sum((s4[0] + s4[1]) + (s4[2] + s4[3])) * (1.f / 64.f);
+    const float rstd = rsqrtf(fmaxf(cross_row_sum((q4[0] + q4[1]) + (q4[2] + q4[3])) * (1.f / 64.f) - mean * mean, 0.f) + 1e-5f);
+    CTr nh, nl;
+    ct_split(h, nh, nl);
+    f32x4 lg[MA];
+#pragma unroll
+    for (int ma = 0; ma < MA; ++ma) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(HH[ma][s], rb(nh, s), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(HH[ma][s], rb(nl, s), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(HL[ma][s], rb(nh, s), acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) lg[ma][r] = rstd * (acc[r] - mean * HG[ma][r]) + HC[ma][r];
+    }
+#ifdef MDL_WAVE_DEBUG
+    {
+      CT lgc;
+#pragma unroll
+      for (int ma = 0; ma < 4; ++ma) lgc.v[ma] = ma < MA ? lg[ma < MA ? ma : 0] : f32x4{0.f, 0.f, 0.f, 0.f};
+      WDBG(13, lgc);
+    }
+#endif
+    // ---- sample (transformer_act.py:86-97: masked categorical / the ratio agent's Normal), every lane alike
+    const size_t oi = (size_t)env * L + i;
+    float a_out, lp_out;
+    if constexpr (!WIDE) {   // A <= 4: the logits are registers r < A of lanes g = 0
+      float l[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) l[a] = rdlane(lg[0][a], 0);
+      if (i < n_disc) {
+        float mx = -INFINITY;
+        int amax = 0;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          l[a] = a < A ? (rdlane(avl, a) == 0.f ? -1e10f : l[a]) : -INFINITY;
+          if (l[a] > mx) { mx = l[a]; amax = a; }
+        }
+        float e[4], se = 0.f;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) { e[a] = a < A ? __expf(l[a] - mx) : 0.f; se += e[a]; }
+        const float lse = mx + __logf(se);
+        int act = amax;
+        if (!det) {
+          const float uu = rdlane(i < 64 ? U[0] : i < 128 ? U[1] : U[2], i & 63);
+          const float inv = 1.f / se;
+          float cdf = 0.f;
+          int cnt = 0;
+#pragma unroll
+          for (int a = 0; a < 4; ++a) {
+            cdf += e[a] * inv;
+            cnt += (a < A) & (cdf < uu);
+          }
+          act = min(cnt, A - 1);
+        }
+        float la = l[0];
+#pragma unroll
+        for (int a = 1; a < 4; ++a) la = act == a ? l[a] : la;
+        a_out = (float)act;
+        lp_out = la - lse;
+        tok = 1 + act;
+      } else {
+        const float mu = A == 1 ? l[0] : A == 2 ? l[1] : A == 3 ? l[2] : l[3];
+        const float sd = p.stdv[A - 1];
+        a_out = det ? mu : mu + sd * zlast;
+        const float z = (a_out - mu) / sd;
+        lp_out = -0.5f * z * z - __logf(sd) - 0.91893853320467274f;
+      }
+    } else {   // 4 < A <= 64: logits through LDS, lane a = action a
+      if (c == 0) {
+#pragma unroll
+        for (int ma = 0; ma < MA; ++ma) *(f32x4*)(SC + 16 * ma + 4 * g) = lg[ma];
+      }
+      asm volatile("" ::: "memory");
+      const bool aok = lane < A;
+      const float raw = SC[lane];
+      asm volatile("" ::: "memory");   // the next row's writes stay behind these reads
+      if (i < n_disc) {
+        const float l = aok ? (avl == 0.f ? -1e10f : raw) : -INFINITY;
+        const float mx = wave_max(l);
+        int act = __ffsll((unsigned long long)__ballot(l == mx)) - 1;   // first maximum (argmax)
+        const float lse = mx + __logf(wave_sum(aok ? __expf(l - mx) : 0.f));
+        if (!det) {   // inverse CDF: the number of actions whose running probability is below u
+          const float cdf = wv_incl_scan(aok ? __expf(l - lse) : 0.f, lane);
+          const float uu = rdlane(i < 64 ? U[0] : i < 128 ? U[1] : U[2], i & 63);
+          act = min((int)__popcll((unsigned long long)__ballot(aok && cdf < uu)), A - 1);
+        }
+        act = __builtin_amdgcn_readfirstlane(act);
+        a_out = (float)act;
+        lp_out = rdlane(l, act) - lse;
+        tok = 1 + act;
+      } else {
+        const float mu = rdlane(raw, A - 1), sd = p.stdv[A - 1];
+        a_out = det ? mu : mu + sd * zlast;
+        const float z = (a_out - mu) / sd;
+        lp_out = -0.5f * z * z - __logf(sd) - 0.91893853320467274f;
+      }
+    }
+    if (lane == 0) {
+      p.out_a[oi] = a_out;
+      p.out_lp[oi] = lp_out;
+    }
+  }
+}
+
+template <int NB, int NREG>
+int wv_launch(const DecParams* p, bool wide, size_t lds, hipStream_t st) {
+  const void* f = wide ? (const void*)mat_decode_wave_kernel<NB, NREG, true> : (const void*)mat_decode_wave_kernel<NB, NREG, false>;
+  hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return -(int)e;
+  if (wide) hipLaunchKernelGGL((mat_decode_wave_kernel<NB, NREG, true>), dim3(p->B), dim3(64), lds, st, *p);
+  else hipLaunchKernelGGL((mat_decode_wave_kernel<NB, NREG, false>), dim3(p->B), dim3(64), lds, st, *p);
+  e = hipGetLastError();
+  return e == hipSuccess ? 0 : -(int)e;
+}
+
+}  // namespace
+
+#ifdef MDL_WAVE_DEBUG
+MDL_API int mdl_wave_debug_read(float* out, int row) {
+  if (row >= 0) return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_wdbg_row), &row, sizeof(int));
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wdbg), sizeof(float) * 16 * 64, 0, hipMemcpyDeviceToHost);
+}
+#endif
+
+// The one-wave path: one-row token passes (stride 1: every stochastic rollout step; deterministic decisions with
+// stride 1) of the Discrete / Semi_Discrete(-1) action types with the block-0 token table and the folded head,
+// n_block 1 or 2, L up to what the LDS carve holds (weights beyond it in registers, at most 6 matrices).
+// Returns the number of register-resident weight matrices of the launch it would make, or -1 (not on this path).
+MDL_API int mdl_decode_wave_plan(const DecParams* p, int NB) {
+  if (!p->wfa || p->cont || p->avail_cont || !p->qkv0 || !p->hfold || !p->rep || p->epw != 1) return -1;
+  if (NB < 1 || NB > 2 || p->act_dim < 1 || p->act_dim > 64 || p->stride != 1 || p->L < 1 || p->L > 192) return -1;
+  if (p->n_disc != p->L && p->n_disc != p->L - 1) return -1;
+  if (!p->deterministic && !p->gen && (!p->rnd_u || (p->n_disc < p->L && !p->rnd_n))) return -1;
+  for (int nreg = 0; nreg <= (NB == 1 ? 4 : 6); nreg += 2)
+    if (wv_lds(NB, p->L, p->n_tok, wv_nm(NB) - nreg).total <= 160 * 1024) return nreg;
+  return -1;
+}
+
+int mdl_decode_wave(const DecParams* p, int NB, hipStream_t st) {
+  const int nreg = mdl_decode_wave_plan(p, NB);
+  if (nreg < 0) return 1;
+  if (p->B <= 0) return 0;
+  const bool wide = p->act_dim > 4;
+  const size_t lds = (size_t)wv_lds(NB, p->L, p->n_tok, wv_nm(NB) - nreg).total;
+  if (NB == 1) {
+    if (nreg == 0) return wv_launch<1, 0>(p, wide, lds, st);
+    if (nreg == 2) return wv_launch<1, 2>(p, wide, lds, st);
+    return wv_launch<1, 4>(p, wide, lds, st);
+  }
+  if (nreg == 0) return wv_launch<2, 0>(p, wide, lds, st);
+  if (nreg == 2) return wv_launch<2, 2>(p, wide, lds, st);
+  if (nreg == 4) return wv_launch<2, 4>(p, wide, lds, st);
+  return wv_launch<2, 6>(p, wide, lds, st);
+}

@@ -29,11 +29,12 @@ class DecParams(ctypes.Structure):
                [(n, ctypes.c_void_p) for n in ("wa", "ba", "lnd")] + \
                [("gen", ctypes.c_int)] + [(n, ctypes.c_uint32) for n in ("rk0", "rk1", "rctr")] + \
                [("avail_cont", ctypes.c_int), ("qkv0", ctypes.c_void_p), ("q2pre", ctypes.c_int),
-                ("genv0", ctypes.c_uint32), ("hfold", ctypes.c_void_p)]
+                ("genv0", ctypes.c_uint32), ("hfold", ctypes.c_void_p), ("wfa", ctypes.c_void_p)]
 
 
 sig("mdl_mat_decode", ctypes.POINTER(DecParams), i32, vp)
 sig("mdl_mat_decode_geometry", i32, i32, i32)
+sig("mdl_decode_wave_plan", ctypes.POINTER(DecParams), i32)
 
 
 def _is_cont(model):
@@ -78,6 +79,10 @@ def unsupported_reasons(model, L=None) -> list:
 def supports(model, L=None) -> bool:
     return not unsupported_reasons(model, L)
 
+
+# One-wave decode (csrc/mat_decode_wave.hip) for one-row token passes; False (or MAT_DCML_DECODE_WAVE=0) keeps every
+# decode on the 4-wave kernel (csrc/mat_decode.hip) — the A/B switch and the parity tests' reference.
+WAVE_DECODE = os.environ.get("MAT_DCML_DECODE_WAVE", "1") != "0"
 
 # envs per decode workgroup: the kernel runs one env per workgroup (its MFMA attention shares the K / V operand
 # over the tile's query rows); the geometry query still takes the cap for its signature.
@@ -131,7 +136,7 @@ def decoder_pack(model):
         tok_start, tok_zero = 0, A + 1
     emb = dec.ln(dec.action_encoder(toks)).float()
     std = model.action_std().float() if model.action_type != "Discrete" else torch.ones(A, device=dev)
-    pack = dict(wpack=mp.decoder_fw, bias=torch.stack([l.bias.detach() for l in lins]).float().contiguous(),
+    pack = dict(wpack=mp.decoder_fw, wfa=mp.fa, bias=torch.stack([l.bias.detach() for l in lins]).float().contiguous(),
                 lnp=torch.stack(lns).float().contiguous(), emb=emb.contiguous(),
                 wh2=dec.head[3].weight.detach().float().contiguous(), bh2=dec.head[3].bias.detach().float().contiguous(),
                 stdv=std.contiguous(), n_tok=toks.shape[0], tok_start=tok_start, tok_zero=tok_zero,
@@ -256,9 +261,17 @@ def decode(model, rep, ava=None, deterministic=False, stride=1, rand=None):
                     pk["n_tok"], pk["tok_start"], pk["tok_zero"], 0, cont,
                     P(pk.get("wa")).value, P(pk.get("ba")).value, P(pk.get("lnd")).value, int(gen), rk0, rk1, rctr,
                     avail, P(pk.get("qkv0")).value, 0, int(getattr(model, "_mdl_env0", 0)) & 0xFFFFFFFF,
-                    P(pk.get("hfold")).value)
+                    P(pk.get("hfold")).value, P(pk.get("wfa") if WAVE_DECODE else None).value)
+    model._mdl_decode_path = wave_path(prm, model.n_block)
     check(lib().mdl_mat_decode(ctypes.byref(prm), model.n_block, kernels._stream()), "mat_decode")
     return out_a, out_lp
+
+
+def wave_path(prm, n_block):
+    """'wave(nreg=k)' when the decode call runs on the one-wave kernel (k weight matrices register-resident), else
+    '4wave'."""
+    k = lib().mdl_decode_wave_plan(ctypes.byref(prm), n_block)
+    return f"wave(nreg={k})" if k >= 0 else "4wave"
 
 
 def _encode(model, obs):

@@ -60,6 +60,8 @@ def kernel_report(runner) -> dict:
     else:
         out["encoder"] = _hip("mat_enc_fwd", reason or mat_train.encoder_unsupported_reasons(m))
         out["decode"] = _hip("mat_decode", reason or mat_fused.unsupported_reasons(m))
+        if hasattr(m, "_mdl_decode_path") and out["decode"].startswith("hip:"):   # set by the last decode call
+            out["decode"] += f"[{m._mdl_decode_path}]"
         tr = getattr(runner, "trainer", None)
         if tr is not None and getattr(tr, "fused", False):
             out["train"] = "hip:mat_enc_fwd/bwd+mat_dec_fwd/bwd+ppo_loss+adam"

@@ -219,3 +219,102 @@ def test_decode_available_continuous_matches_torch(gpu, L, A, B, det):
         lp_tf, _ = act.parallel_act(m, rep, obs, a_k, ava)
     err = (lp_tf - lp_k).abs()
     assert err.mean().item() < 2e-2 and err.max().item() < 0.2, (err.mean().item(), err.max().item())
+
+
+def _both_kernels(m, rep, ava, det, rand):
+    """The same decode call on the one-wave kernel (csrc/mat_decode_wave.hip) and on the 4-wave kernel."""
+    saved = mat_fused.WAVE_DECODE
+    try:
+        mat_fused.WAVE_DECODE = True
+        a_w, lp_w = mat_fused.decode(m, rep, ava, det, 1, rand)
+        path = m._mdl_decode_path
+        mat_fused.WAVE_DECODE = False
+        a_4, lp_4 = mat_fused.decode(m, rep, ava, det, 1, rand)
+    finally:
+        mat_fused.WAVE_DECODE = saved
+    torch.cuda.synchronize()
+    return path, a_w, lp_w, a_4, lp_4
+
+
+@pytest.mark.parametrize("L,B,nb,atype,A", [(33, 256, 2, "Semi_Discrete", 2), (33, 64, 1, "Semi_Discrete", 2),
+                                            (5, 64, 2, "Semi_Discrete", 2), (101, 16, 1, "Semi_Discrete", 2),
+                                            (27, 32, 2, "Discrete", 36), (9, 48, 1, "Discrete", 3)])
+@pytest.mark.parametrize("det", [False, True])
+def test_wave_decode_matches_4wave_and_torch(gpu, L, B, nb, atype, A, det):
+    """One-wave decode vs the 4-wave kernel and the fp32 torch decode on the same draws: decisions taken from the same
+    prefix agree (bf16 near-ties aside), the kernel's log-probs are the teacher-forced log-probs of its own actions,
+    masked actions are never taken, and the launch really is the one-wave kernel."""
+    m = make(L, gpu, atype=atype, A=A, seed=11, nb=nb)
+    obs, ava, rep, rand = inputs(m, B, L, gpu, A=A)
+    if A > 2:
+        g = torch.Generator(device=gpu).manual_seed(3)
+        ava = (torch.rand(B, L, A, device=gpu, generator=g) < 0.6).float()
+        ava[..., 0] = 1.0
+    path, a_w, lp_w, a_4, lp_4 = _both_kernels(m, rep, ava, det, rand)
+    assert path.startswith("wave"), path
+    a_ref, _ = act.autoregressive_act(m, rep, obs, ava, det, 1, rand)
+    n_disc = L if atype == "Discrete" else L - 1
+    for other in (a_4, a_ref):
+        eq = (other[:, :n_disc] == a_w[:, :n_disc]).squeeze(-1).float()
+        same_prefix = torch.cat([torch.ones_like(eq[:, :1]), torch.cumprod(eq, 1)[:, :-1]], 1)
+        rate = ((1 - eq) * same_prefix).sum().item() / same_prefix.sum().item()
+        assert rate < 0.02, rate
+    assert (ava[:, :n_disc].gather(-1, a_w[:, :n_disc].long()) == 1).all()
+    with torch.no_grad():
+        lp_tf, _ = act.parallel_act(m, rep, obs, a_w, ava)
+    err = (lp_tf - lp_w).abs()
+    assert err.mean().item() < 2e-2 and err.max().item() < 0.2, (err.mean().item(), err.max().item())
+    if n_disc < L:   # the ratio agent: same Normal draw, mean within bf16 noise of the 4-wave kernel
+        same = (a_4[:, :n_disc] == a_w[:, :n_disc]).all(1).squeeze(-1)
+        assert (a_4[same, -1] - a_w[same, -1]).abs().max().item() < 5e-2
+
+
+def test_wave_decode_inkernel_draws_match_4wave(gpu):
+    """rand=None (in-kernel Philox keyed by env / row / call counter): both kernels draw the same noise, so with the
+    same key they take the same decisions except at bf16 near-ties."""
+    L, B = 33, 256
+    m = make(L, gpu, seed=4)
+    obs, ava, rep, _ = inputs(m, B, L, gpu)
+    mat_fused.set_sampling_key(m, 123)
+    saved = mat_fused.WAVE_DECODE
+    try:
+        mat_fused.WAVE_DECODE = True
+        a_w, _ = mat_fused.decode(m, rep, ava, False, 1, None)
+        mat_fused.set_sampling_key(m, 123)
+        mat_fused.WAVE_DECODE = False
+        a_4, _ = mat_fused.decode(m, rep, ava, False, 1, None)
+    finally:
+        mat_fused.WAVE_DECODE = saved
+    eq = (a_4[:, :L - 1] == a_w[:, :L - 1]).squeeze(-1).float()   # discrete rows (the last is the ratio agent)
+    same_prefix = torch.cat([torch.ones_like(eq[:, :1]), torch.cumprod(eq, 1)[:, :-1]], 1)
+    rate = ((1 - eq) * same_prefix).sum().item() / same_prefix.sum().item()
+    assert rate < 0.02, rate
+    same = eq.all(1)
+    assert (a_4[same, -1] - a_w[same, -1]).abs().max().item() < 5e-2   # same Normal draw for the ratio agent
+
+
+@pytest.mark.parametrize("L,nb,A,B", [(33, 2, 2, 256), (101, 1, 2, 256), (27, 2, 36, 32)])
+def test_wave_decode_latency(gpu, L, nb, A, B):
+    """Per-env-step decode time of both kernels at the rollout shapes (printed; the one-wave kernel must not be
+    slower than the 4-wave one)."""
+    m = make(L, gpu, nb=nb, A=A, atype="Discrete" if A > 2 else "Semi_Discrete")
+    obs, ava, rep, rand = inputs(m, B, L, gpu, A=A)
+    saved = mat_fused.WAVE_DECODE
+    res = {}
+    try:
+        for wave in (True, False):
+            mat_fused.WAVE_DECODE = wave
+            for _ in range(3):
+                mat_fused.decode(m, rep, ava, False, 1, None)
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(20):
+                mat_fused.decode(m, rep, ava, False, 1, None)
+            e.record()
+            torch.cuda.synchronize()
+            res[wave] = s.elapsed_time(e) / 20 * 1e3
+    finally:
+        mat_fused.WAVE_DECODE = saved
+    print(f"decode B={B} L={L} n_block={nb} A={A}: one-wave {res[True]:.1f} us, 4-wave {res[False]:.1f} us per env step")
+    assert res[True] < res[False] * 1.05, res
