@@ -123,7 +123,8 @@ __device__ __forceinline__ void cross_proj(const Mat* m, const CT* xr, const bf1
 // x <- LN(rep + proj(attn(q = W_q rep, k = W_k x, v = W_v x)))   (ma_transformer.py:114)
 template <bool SAVE>
 __device__ __forceinline__ void cross_attn_fwd_ct(const Mat* m, const LNp& ln, CT* xr, const float* rep, bf16_t* sv_x1,
-                                                  bf16_t* sv_a, bf16_t* sv_alo, float* sv_lse, const Ctx& c) {
+                                                  bf16_t* sv_a, bf16_t* sv_alo, float* sv_lse, bf16_t* sv_xh,
+                                                  float* sv_rs, const Ctx& c) {
   const int lane = c.lane;
   __syncthreads();   // every wave done reading the self-attention's K / V
   cross_proj<true>(m, xr, nullptr, rep, SAVE ? sv_x1 : nullptr, c);
@@ -153,7 +154,11 @@ __device__ __forceinline__ void cross_attn_fwd_ct(const Mat* m, const LNp& ln, C
       }
       CT t = ct_add(bp, rp[k]), xh;
       mm(t, Wp, a);
-      ln_fwd_ct(t, xh, xr[k], gam, bet);
+      const float rs = ln_fwd_ct(t, xh, xr[k], gam, bet);
+      if (SAVE) {
+        st_g(sv_xh, c.tok0, rt, c.NR, ct_pack(xh), lane);
+        st_tokf(sv_rs, rt, rs, c);
+      }
     }
   }  CP_MARK(26);
 }
@@ -161,7 +166,8 @@ __device__ __forceinline__ void cross_attn_fwd_ct(const Mat* m, const LNp& ln, C
 // backward: dx (w.r.t. the sublayer output) -> d x1 (returned in dx); d rep accumulated into global drep
 __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, CT* dx, const float* rep, float* drep,
                                                   const bf16_t* sv_x1, const bf16_t* sv_a, const bf16_t* sv_alo,
-                                                  const float* sv_lse, bool first, const Ctx& c) {
+                                                  const float* sv_lse, const bf16_t* sv_xh, const float* sv_rs,
+                                                  bool first, const Ctx& c) {
   const int lane = c.lane;
   const LseR lse = lse_fetch(sv_lse, c);   // consumed after the recompute phase (latency hidden by passes 1-2)
   CT dres[MAXRT];
@@ -169,17 +175,17 @@ __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, C
     CT dlg, dlb;
     ct_zero(dlg);
     ct_zero(dlb);
-    {   // pass 1 (Wp): LN backward -> ds ; DQ = dY of Wp, XB = X of Wp
-      AFr Wpf;
-      loadA(Wpf, m[7].fa, lane);
-      const CT bp = ld_vec(m[7].b, lane), gam = ld_vec(ln.g, lane), bet = ld_vec(ln.b, lane);
-      CTr as[MAXRT];
+    {   // pass 1: LN backward from the saved x-hat / rstd -> ds ; DQ = dY of Wp, XB = X of Wp
+      const CT gam = ld_vec(ln.g, lane);
+      CTr as[MAXRT], xhs[MAXRT];
+      float rsv[MAXRT];
 #pragma unroll
       for (int k = 0; k < MAXRT; ++k) {
         const int rt = c.wave + NW * k;
         if (rt < c.NT) {
           as[k] = ld_g(sv_a, c.tok0, rt, c.NR, lane);
-          dres[k] = ld_gf(rep, c.tok0, rt, c.NR, lane);   // rep (the residual input) parked in dres until used
+          xhs[k] = ld_g(sv_xh, c.tok0, rt, c.NR, lane);
+          rsv[k] = ld_tokf(sv_rs, rt, c);
         }
       }
 #pragma unroll
@@ -187,10 +193,8 @@ __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, C
         const int rt = c.wave + NW * k;
         if (rt < c.NT) {
           const bool ok = tok_ok(rt, c);
-          CT s = ct_add(bp, dres[k]), xh, yy, ds;
-          mm(s, Wpf, as[k]);
-          const float rs = ln_fwd_ct(s, xh, yy, gam, bet);
-          ln_bwd_ct(dx[k], xh, rs, gam, ok, ds, dlg, dlb);
+          CT ds;
+          ln_bwd_ct(dx[k], ct_unpack(xhs[k]), rsv[k], gam, ok, ds, dlg, dlb);
           st_lds(c.DQ, rt, ct_pack(ds), ok, lane);   // dY of Wp
           st_lds(c.XB, rt, as[k], ok, lane);         // X of Wp
           dres[k] = ds;                              // residual path -> d rep
@@ -419,8 +423,17 @@ __device__ __forceinline__ void head_fwd_ct(const DecP& p, const CT* xr, bool sa
       if (save) st_g(p.sv_head, c.tok0, rt, c.NR, x, lane);
       CT hh = bh, xh, n;
       mm(hh, H, x);
-      gelu_ct(hh);
-      ln_fwd_ct(hh, xh, n, gam, bet);
+      if (save && p.hs.xh) {   // x-hat, GELU'(h), rstd for the backward
+        CT gp;
+        gelu_ct_both(hh, gp);
+        const float rs = ln_fwd_ct(hh, xh, n, gam, bet);
+        st_g(p.hs.xh, c.tok0, rt, c.NR, ct_pack(xh), lane);
+        st_g(p.hs.gp, c.tok0, rt, c.NR, ct_pack(gp), lane);
+        st_tokf(p.hs.rs, rt, rs, c);
+      } else {
+        gelu_ct(hh);
+        ln_fwd_ct(hh, xh, n, gam, bet);
+      }
       f32x4 L[MA];
       head_logits_ct<MA>(p, W, n, L, lane);
       if (CONT) {   // per-dimension Normal(mean, std): this lane's dims a = 16ma + 4g + r
@@ -486,20 +499,25 @@ __device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c)
             WT[mt][s][j] = (short)f2bf(w);
           }
     }
-    CT hhs[MAXRT];   // head1 pre-activations (first pass: W_h1 and its bias are dead before the softmax work)
+    // the forward's x-hat, GELU'(h) and rstd of the head (no W_h1 product, GELU or LayerNorm forward here)
+    CTr hxh[MAXRT], hgp[MAXRT];
+    float hrs[MAXRT];
     {
-      AFr Hf;
-      loadA(Hf, p.h1.fa, lane);
-      const CT bh = ld_vec(p.h1.b, lane);
+      CTr xs[MAXRT];
 #pragma unroll
       for (int k = 0; k < MAXRT; ++k) {
         const int rt = c.wave + NW * k;
         if (rt < c.NT) {
-          const CTr x = ld_g(p.sv_head, c.tok0, rt, c.NR, lane);
-          st_lds(c.KB, rt, x, tok_ok(rt, c), lane);   // X of W_h1
-          hhs[k] = bh;
-          mm(hhs[k], Hf, x);
+          xs[k] = ld_g(p.sv_head, c.tok0, rt, c.NR, lane);
+          hxh[k] = ld_g(p.hs.xh, c.tok0, rt, c.NR, lane);
+          hgp[k] = ld_g(p.hs.gp, c.tok0, rt, c.NR, lane);
+          hrs[k] = ld_tokf(p.hs.rs, rt, c);
         }
+      }
+#pragma unroll
+      for (int k = 0; k < MAXRT; ++k) {
+        const int rt = c.wave + NW * k;
+        if (rt < c.NT) st_lds(c.KB, rt, xs[k], tok_ok(rt, c), lane);   // X of W_h1
       }
     }
     const CT gam = ld_vec(p.lnh.g, lane), bet = ld_vec(p.lnh.b, lane);
@@ -513,9 +531,11 @@ __device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c)
         const unsigned am = CONT ? 0u : slot_mask<MA>(p, tok, lane);
         const float actf = CONT ? 0.f : p.act[tok];
         const float dlp = (ok && !CONT) ? p.dlogp[tok] : 0.f, den = (ok && !CONT) ? p.dent[tok] : 0.f;
-        CT gl = hhs[k], ggp, xh, n;   // GELU and GELU' of the head pre-activation from one erf
-        gelu_ct_both(gl, ggp);
-        const float rs = ln_fwd_ct(gl, xh, n, gam, bet);
+        const CT xh = ct_unpack(hxh[k]), ggp = ct_unpack(hgp[k]);
+        const float rs = hrs[k];
+        CT n;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) n.v[i] = xh.v[i] * gam.v[i] + bet.v[i];
         f32x4 L[MA];
         head_logits_ct<MA>(p, W, n, L, lane);
         const bool disc = !CONT && (row % c.L) < p.n_disc;
@@ -586,9 +606,7 @@ __device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c)
         CT dgg;
         ln_bwd_ct(dn, xh, rs, gam, ok, dgg, dlg, dlb);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) dgg.v[i][q] = ok ? dgg.v[i][q] * ggp.v[i][q] : 0.f;
+        for (int i = 0; i < 4; ++i) dgg.v[i] *= ggp.v[i];   // padded rows: x-hat, GELU' and rstd are zero
         st_lds(c.DQ, rt, ct_pack(dgg), ok, lane);   // dY of W_h1
       }
     }
@@ -669,9 +687,11 @@ __device__ __forceinline__ void dec_fwd_tile(const DecP& p, char* smem, int seq0
     const Blk& B = p.blk[b];
     Ctx cc = c;
     asm volatile("" : "+v"(cc.lane), "+v"(cc.tid));
-    self_attn_fwd_ct<SAVE>(B.m, B.ln[0], xr, true, p.sv[b].xin, p.sv[b].a1, p.sv[b].a1lo, p.sv[b].lse1, cc);
-    cross_attn_fwd_ct<SAVE>(B.m, B.ln[1], xr, p.rep, p.sv[b].x1, p.sv[b].a2, p.sv[b].a2lo, p.sv[b].lse2, cc);
-    mlp_fwd_ct<SAVE>(B.m[8], B.m[9], B.ln[2], xr, p.sv[b].x2, p.sv[b].g, p.sv[b].gp, cc);
+    self_attn_fwd_ct<SAVE>(B.m, B.ln[0], xr, true, p.sv[b].xin, p.sv[b].a1, p.sv[b].a1lo, p.sv[b].lse1,
+                           p.sv[b].xh[0], p.sv[b].rs + 0 * (size_t)p.Bs * p.L, cc);
+    cross_attn_fwd_ct<SAVE>(B.m, B.ln[1], xr, p.rep, p.sv[b].x1, p.sv[b].a2, p.sv[b].a2lo, p.sv[b].lse2,
+                            p.sv[b].xh[1], p.sv[b].rs + 1 * (size_t)p.Bs * p.L, cc);
+    mlp_fwd_ct<SAVE>(B.m[8], B.m[9], B.ln[2], xr, p.sv[b].x2, p.sv[b].g, p.sv[b].gp, p.sv[b].xh[2], p.sv[b].rs + 2 * (size_t)p.Bs * p.L, cc);
   }
   head_fwd_ct<MA, CONT>(p, xr, SAVE, c);
   CP_MARK(27);
@@ -705,10 +725,11 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
     const Blk& B = p.blk[bb];
     Ctx cc = c;
     asm volatile("" : "+v"(cc.lane), "+v"(cc.tid));
-    mlp_bwd_ct(B.m[8], B.m[9], B.ln[2], dx, p.sv[bb].x2, p.sv[bb].g, p.sv[bb].gp, cc);
+    mlp_bwd_ct(B.m[8], B.m[9], B.ln[2], dx, p.sv[bb].x2, p.sv[bb].g, p.sv[bb].gp, p.sv[bb].xh[2], p.sv[bb].rs + 2 * (size_t)p.Bs * p.L, cc);
     cross_attn_bwd_ct(B.m, B.ln[1], dx, p.rep, p.drep, p.sv[bb].x1, p.sv[bb].a2, p.sv[bb].a2lo, p.sv[bb].lse2,
-                      bb == NB - 1, cc);
-    self_attn_bwd_ct(B.m, B.ln[0], dx, p.sv[bb].xin, p.sv[bb].a1, p.sv[bb].a1lo, p.sv[bb].lse1, true, cc);
+                      p.sv[bb].xh[1], p.sv[bb].rs + 1 * (size_t)p.Bs * p.L, bb == NB - 1, cc);
+    self_attn_bwd_ct(B.m, B.ln[0], dx, p.sv[bb].xin, p.sv[bb].a1, p.sv[bb].a1lo, p.sv[bb].lse1, p.sv[bb].xh[0],
+                     p.sv[bb].rs + 0 * (size_t)p.Bs * p.L, true, cc);
   }
   // ---------------- embedding backward: dW_a[:, token] += d pre ; LN_dec params
   if (!CONT) {

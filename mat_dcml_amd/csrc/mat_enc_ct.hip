@@ -109,8 +109,17 @@ __device__ __forceinline__ void enc_fwd_tile(const EncP& p, const EncX& ex, char
       if (rt < c.NT) {
         float oh[4], hat[4];
         CT pre = embed_pre(p, ex, rt, W, oh, hat, c), xh;
-        gelu_ct(pre);
-        ln_fwd_ct(pre, xh, xr[k], gam, bet);
+        if (SAVE) {   // x-hat, GELU'(pre), rstd for the backward (which recomputes none of the embedding forward)
+          CT gp;
+          gelu_ct_both(pre, gp);
+          const float rs = ln_fwd_ct(pre, xh, xr[k], gam, bet);
+          st_g(p.es.xh, c.tok0, rt, c.NR, ct_pack(xh), lane);
+          st_g(p.es.gp, c.tok0, rt, c.NR, ct_pack(gp), lane);
+          st_tokf(p.es.rs, rt, rs, c);
+        } else {
+          gelu_ct(pre);
+          ln_fwd_ct(pre, xh, xr[k], gam, bet);
+        }
       }
     }
   }
@@ -120,8 +129,9 @@ __device__ __forceinline__ void enc_fwd_tile(const EncP& p, const EncX& ex, char
     const Blk& B = p.blk[b];
     Ctx cc = c;   // opaque per-iteration lane id: keeps hipcc from hoisting (and spilling) every LDS address
     asm volatile("" : "+v"(cc.lane), "+v"(cc.tid));
-    self_attn_fwd_ct<SAVE>(B.m, B.ln[0], xr, false, p.sv[b].xin, p.sv[b].a1, p.sv[b].a1lo, p.sv[b].lse1, cc);
-    mlp_fwd_ct<SAVE>(B.m[8], B.m[9], B.ln[1], xr, p.sv[b].x1, p.sv[b].g, p.sv[b].gp, cc);
+    self_attn_fwd_ct<SAVE>(B.m, B.ln[0], xr, false, p.sv[b].xin, p.sv[b].a1, p.sv[b].a1lo, p.sv[b].lse1,
+                           p.sv[b].xh[0], p.sv[b].rs + 0 * (size_t)p.Bs * p.L, cc);
+    mlp_fwd_ct<SAVE>(B.m[8], B.m[9], B.ln[1], xr, p.sv[b].x1, p.sv[b].g, p.sv[b].gp, p.sv[b].xh[1], p.sv[b].rs + 1 * (size_t)p.Bs * p.L, cc);
   }
   // value head: v = W_v2 · LN(GELU(W_v1 · rep + b)) + b   (ma_transformer.py:138-139,152)
   AFr H;
@@ -138,8 +148,17 @@ __device__ __forceinline__ void enc_fwd_tile(const EncP& p, const EncX& ex, char
       if (p.rep) st_gf(p.rep, c.tok0, rt, c.NR, xr[k], lane);
       CT hh = bh, xh, n;
       mm(hh, H, ct_pack(xr[k]));
-      gelu_ct(hh);
-      ln_fwd_ct(hh, xh, n, gam, bet);
+      if (SAVE) {   // x-hat, GELU'(h), rstd for the backward
+        CT gp;
+        gelu_ct_both(hh, gp);
+        const float rs = ln_fwd_ct(hh, xh, n, gam, bet);
+        st_g(p.hs.xh, c.tok0, rt, c.NR, ct_pack(xh), lane);
+        st_g(p.hs.gp, c.tok0, rt, c.NR, ct_pack(gp), lane);
+        st_tokf(p.hs.rs, rt, rs, c);
+      } else {
+        gelu_ct(hh);
+        ln_fwd_ct(hh, xh, n, gam, bet);
+      }
       float s0 = 0.f, s1 = 0.f;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -188,26 +207,30 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
     ct_zero(dlb);
     ct_zero(dw0);
     ct_zero(dw1);
-    CT hhs[MAXRT];   // head1 pre-activations (first pass: W_h1 and its bias are dead before the LN work)
+    // the forward's x-hat, GELU'(h) and rstd of the head (no W_h1 product, GELU or LayerNorm forward here); every
+    // tile's loads requested up front (one latency, not three)
+    CTr hxh[MAXRT], hgp[MAXRT];
+    float hrs[MAXRT], dv0s[MAXRT], dv1s[MAXRT];
     {
-      AFr Hf;
-      loadA(Hf, p.h1.fa, lane);
-      const CT bh = ld_vec(p.h1.b, lane);
       CT reps[MAXRT];
-#pragma unroll
-      for (int k = 0; k < MAXRT; ++k) {   // every tile's encoder output requested up front (one latency, not three)
-        const int rt = c.wave + NW * k;
-        if (rt < c.NT) reps[k] = ld_gf(p.rep, c.tok0, rt, c.NR, lane);
-      }
 #pragma unroll
       for (int k = 0; k < MAXRT; ++k) {
         const int rt = c.wave + NW * k;
         if (rt < c.NT) {
-          const CTr r = ct_pack(reps[k]);
-          st_lds(c.XB, rt, r, tok_ok(rt, c), lane);   // X of W_h1
-          hhs[k] = bh;
-          mm(hhs[k], Hf, r);
+          reps[k] = ld_gf(p.rep, c.tok0, rt, c.NR, lane);
+          hxh[k] = ld_g(p.hs.xh, c.tok0, rt, c.NR, lane);
+          hgp[k] = ld_g(p.hs.gp, c.tok0, rt, c.NR, lane);
+          hrs[k] = ld_tokf(p.hs.rs, rt, c);
+          const bool ok = tok_ok(rt, c);
+          const size_t tok = (size_t)(c.tok0 + (ok ? rt * 16 + (lane & 15) : 0));
+          dv0s[k] = ok ? p.dv[tok * p.n_obj] : 0.f;
+          dv1s[k] = (ok && p.n_obj > 1) ? p.dv[tok * p.n_obj + 1] : 0.f;
         }
+      }
+#pragma unroll
+      for (int k = 0; k < MAXRT; ++k) {
+        const int rt = c.wave + NW * k;
+        if (rt < c.NT) st_lds(c.XB, rt, ct_pack(reps[k]), tok_ok(rt, c), lane);   // X of W_h1
       }
     }
     const CT gam = ld_vec(p.lnh.g, lane), bet = ld_vec(p.lnh.b, lane);
@@ -220,27 +243,21 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
       const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         const bool ok = tok_ok(rt, c);
-        const size_t tok = (size_t)(c.tok0 + (ok ? rt * 16 + (lane & 15) : 0));
-        const float dv0 = ok ? p.dv[tok * p.n_obj] : 0.f;
-        const float dv1 = (ok && p.n_obj > 1) ? p.dv[tok * p.n_obj + 1] : 0.f;
+        const float dv0 = dv0s[k], dv1 = dv1s[k];
         sdv0 += dv0;
         sdv1 += dv1;
-        CT gl = hhs[k], ggp, xh, n, dn, dg;   // GELU and GELU' of the head pre-activation from one erf
-        gelu_ct_both(gl, ggp);
-        const float rs = ln_fwd_ct(gl, xh, n, gam, bet);
+        const CT xh = ct_unpack(hxh[k]), ggp = ct_unpack(hgp[k]);
+        CT n, dn, dg;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i) {
+          n.v[i] = xh.v[i] * gam.v[i] + bet.v[i];
+          dn.v[i] = dv0 * w0.v[i] + dv1 * w1.v[i];
+          dw0.v[i] += dv0 * n.v[i];
+          dw1.v[i] += dv1 * n.v[i];
+        }
+        ln_bwd_ct(dn, xh, hrs[k], gam, ok, dg, dlg, dlb);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            dn.v[i][q] = dv0 * w0.v[i][q] + dv1 * w1.v[i][q];
-            dw0.v[i][q] += dv0 * n.v[i][q];
-            dw1.v[i][q] += dv1 * n.v[i][q];
-          }
-        ln_bwd_ct(dn, xh, rs, gam, ok, dg, dlg, dlb);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) dg.v[i][q] = ok ? dg.v[i][q] * ggp.v[i][q] : 0.f;
+        for (int i = 0; i < 4; ++i) dg.v[i] *= ggp.v[i];   // padded rows: x-hat, GELU' and rstd are zero
         st_lds(c.DQ, rt, ct_pack(dg), ok, lane);   // dY of W_h1
       }
     }
@@ -279,8 +296,9 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
     const Blk& B = p.blk[bb];
     Ctx cc = c;
     asm volatile("" : "+v"(cc.lane), "+v"(cc.tid));
-    mlp_bwd_ct(B.m[8], B.m[9], B.ln[1], dx, p.sv[bb].x1, p.sv[bb].g, p.sv[bb].gp, cc);
-    self_attn_bwd_ct(B.m, B.ln[0], dx, p.sv[bb].xin, p.sv[bb].a1, p.sv[bb].a1lo, p.sv[bb].lse1, false, cc);
+    mlp_bwd_ct(B.m[8], B.m[9], B.ln[1], dx, p.sv[bb].x1, p.sv[bb].g, p.sv[bb].gp, p.sv[bb].xh[1], p.sv[bb].rs + 1 * (size_t)p.Bs * p.L, cc);
+    self_attn_bwd_ct(B.m, B.ln[0], dx, p.sv[bb].xin, p.sv[bb].a1, p.sv[bb].a1lo, p.sv[bb].lse1, p.sv[bb].xh[0],
+                     p.sv[bb].rs + 0 * (size_t)p.Bs * p.L, false, cc);
   }
   // ---------------- embedding backward: x0 = LN0(GELU(pre)), pre = W_e · LN_obs(obs) + b_e
   {
@@ -289,26 +307,22 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
     ct_zero(dlb);
     ct_zero(dbe);
     f32x4 dog = {0.f, 0.f, 0.f, 0.f}, dob = {0.f, 0.f, 0.f, 0.f};
-    bf16x8 W[4], WT[2];
-    if (!ex.pre_in) {
-      we_frags(p, W, lane);
-      weT_frags(p, WT, lane);
-    }
-    const CT gam = ld_vec(p.ln0_g, lane), bet = ld_vec(p.ln0_b, lane);
+    bf16x8 WT[2];
+    if (!ex.pre_in) weT_frags(p, WT, lane);
+    const CT gam = ld_vec(p.ln0_g, lane);
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
       const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         const bool ok = tok_ok(rt, c);
         float oh[4] = {0.f, 0.f, 0.f, 0.f}, hat[4] = {0.f, 0.f, 0.f, 0.f};
-        CT e = embed_pre(p, ex, rt, W, oh, hat, c), egp, xh, yy, de;
-        gelu_ct_both(e, egp);
-        const float rs = ln_fwd_ct(e, xh, yy, gam, bet);
-        ln_bwd_ct(dx[k], xh, rs, gam, ok, de, dlg, dlb);
+        if (!ex.pre_in) obs_ln(p, rt, c, oh, hat);   // X of W_e and the LN_obs backward (od <= 16 dims in-lane)
+        // the forward's x-hat, GELU'(pre) and rstd (no embedding product, GELU or LayerNorm forward here)
+        const CT xh = ct_unpack(ld_g(p.es.xh, c.tok0, rt, c.NR, lane)), egp = ct_unpack(ld_g(p.es.gp, c.tok0, rt, c.NR, lane));
+        CT de;
+        ln_bwd_ct(dx[k], xh, ld_tokf(p.es.rs, rt, c), gam, ok, de, dlg, dlb);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) de.v[i][q] = ok ? de.v[i][q] * egp.v[i][q] : 0.f;
+        for (int i = 0; i < 4; ++i) de.v[i] *= egp.v[i];   // padded rows: zero
         if (ex.pre_in) {
           st_gf(ex.dpre_out, c.tok0, rt, c.NR, de, lane);
           continue;

@@ -37,8 +37,14 @@ struct Blk { Mat m[10]; LNp ln[3]; };
 // backward's delta = rowsum(dO O) sees O to ~16 significant bits (bf16 O alone put 10-40 % errors on dK / dQ);
 // g / gp = the MLP's GELU(h) (the exact bf16 operand the forward fed to W2) and GELU'(h): the backward evaluates
 // no erf for the MLP (round 3 recomputed GELU and GELU' from h: two erf per element)
+// xh[k] / rs = x-hat (bf16) and rstd (f32, [3][tok], slot k) of the block's k-th LayerNorm as the forward computed
+// them: the backward's LayerNorm passes read them instead of recomputing the producing linear + LayerNorm forward
+// (round 4: no weight fragments, bias / residual loads or LN statistics in those passes)
 struct Sv { bf16_t* xin; bf16_t* a1; float* lse1; bf16_t* x1; bf16_t* a2; float* lse2; bf16_t* x2; bf16_t* g;
-            bf16_t* a1lo; bf16_t* a2lo; bf16_t* gp; };
+            bf16_t* a1lo; bf16_t* a2lo; bf16_t* gp; bf16_t* xh[3]; float* rs; };
+// the same for a GELU -> LayerNorm stage outside the blocks (value / action head, observation embedding): x-hat,
+// GELU'(pre-activation) (bf16) and rstd ([tok] f32); null = not saved (rollout passes)
+struct HSv { bf16_t* xh; bf16_t* gp; float* rs; };
 
 struct EncP {
   int Bs, L, od, SQ, NRP, n_obj;
@@ -59,6 +65,7 @@ struct EncP {
   long long g_delta, g_stride;   // dW workspace: copy k of a gradient lives at grad + g_delta + k * g_stride
   int g_copies;                  // 0: atomics straight into the gradients
   float* d_bh2;                  // value-head bias gradient Σ dv (round-2 backward; null: summed by the caller)
+  HSv hs, es;                    // value head, observation embedding (round 4)
 };
 
 struct DecP {
@@ -94,6 +101,7 @@ struct DecP {
   int cont;
   const float* ba;
   float* d_ba;
+  HSv hs;                // action head (round 4)
 };
 
 struct Ctx {

@@ -198,25 +198,28 @@ __device__ __forceinline__ CTr ld_lds(const bf16_t* buf, int rt, int lane) {
   for (int mt = 0; mt < 4; ++mt) x.q[mt] = *(const uint2*)(buf + tmo(row, 16 * mt + 4 * g));
   return x;
 }
-// plain global [tok][64] bf16 (rows >= NR read as zero / not written)
+// Saved activations (written by the forward, read only by the backward): one 128-byte record per token in the
+// token-on-lane order — feature 16mt + 4g + r at element 16g + 4mt + r — so lane (g, c) owns 32 contiguous bytes of
+// token c (two 16-byte accesses; a [tok][64] row-major record took four scattered 8-byte pieces per lane, and the
+// forward's saves were store-issue bound).  Rows >= NR read as zero / are not written.
 __device__ __forceinline__ CTr ld_g(const bf16_t* src, int tok0, int rt, int NR, int lane) {
   const int g = lane >> 4, row = rt * 16 + (lane & 15);
   const bool ok = row < NR;
-  const bf16_t* base = src + (size_t)(tok0 + (ok ? row : 0)) * 64 + 4 * g;
+  const uint4* base = (const uint4*)(src + (size_t)(tok0 + (ok ? row : 0)) * 64 + 16 * g);
+  const uint4 a = base[0], b = base[1];
   CTr x;
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-    const uint2 v = *(const uint2*)(base + 16 * mt);
-    x.q[mt] = ok ? v : make_uint2(0u, 0u);
-  }
+  x.q[0] = ok ? make_uint2(a.x, a.y) : make_uint2(0u, 0u);
+  x.q[1] = ok ? make_uint2(a.z, a.w) : make_uint2(0u, 0u);
+  x.q[2] = ok ? make_uint2(b.x, b.y) : make_uint2(0u, 0u);
+  x.q[3] = ok ? make_uint2(b.z, b.w) : make_uint2(0u, 0u);
   return x;
 }
 __device__ __forceinline__ void st_g(bf16_t* dst, int tok0, int rt, int NR, const CTr& x, int lane) {
   const int g = lane >> 4, row = rt * 16 + (lane & 15);
   if (row < NR) {
-    bf16_t* base = dst + (size_t)(tok0 + row) * 64 + 4 * g;
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) *(uint2*)(base + 16 * mt) = x.q[mt];
+    uint4* base = (uint4*)(dst + (size_t)(tok0 + row) * 64 + 16 * g);
+    base[0] = make_uint4(x.q[0].x, x.q[0].y, x.q[1].x, x.q[1].y);
+    base[1] = make_uint4(x.q[2].x, x.q[2].y, x.q[3].x, x.q[3].y);
   }
 }
 // plain global [tok][64] f32
@@ -239,6 +242,17 @@ __device__ __forceinline__ void st_gf(float* dst, int tok0, int rt, int NR, cons
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) *(f32x4*)(base + 16 * mt) = x.v[mt];
   }
+}
+
+// per-token f32 scalars ([tok]): LayerNorm rstd saved by the forward for the backward (lanes g = 0 write 16
+// consecutive tokens)
+__device__ __forceinline__ void st_tokf(float* dst, int rt, float v, const Ctx& c) {
+  const int row = rt * 16 + (c.lane & 15);
+  if ((c.lane >> 4) == 0 && row < c.NR) dst[(size_t)(c.tok0 + row)] = v;
+}
+__device__ __forceinline__ float ld_tokf(const float* src, int rt, const Ctx& c) {
+  const int row = rt * 16 + (c.lane & 15);
+  return row < c.NR ? src[(size_t)(c.tok0 + row)] : 0.f;   // padded rows: rstd 0 -> zero gradient
 }
 
 // ------------------------------------------------------------------------------------------ LayerNorm (per token)
@@ -728,7 +742,8 @@ __device__ __forceinline__ void attn_bwd_kv_ct(const bf16_t* Q, bf16_t* K, bf16_
 // self attention: x <- LN(x + proj(attn(q(x), k(x), v(x))))   (ma_transformer.py:89-92,112)
 template <bool SAVE>
 __device__ __forceinline__ void self_attn_fwd_ct(const Mat* m, const LNp& ln, CT* xr, bool causal, bf16_t* sv_xin,
-                                                 bf16_t* sv_a, bf16_t* sv_alo, float* sv_lse, const Ctx& c) {
+                                                 bf16_t* sv_a, bf16_t* sv_alo, float* sv_lse, bf16_t* sv_xh,
+                                                 float* sv_rs, const Ctx& c) {
   const int lane = c.lane;
   {
     CTr xp[MAXRT];
@@ -763,7 +778,11 @@ __device__ __forceinline__ void self_attn_fwd_ct(const Mat* m, const LNp& ln, CT
       }
       CT t = ct_add(bp, xr[k]), xh;
       mm(t, Wp, a);
-      ln_fwd_ct(t, xh, xr[k], gam, bet);
+      const float rs = ln_fwd_ct(t, xh, xr[k], gam, bet);
+      if (SAVE) {
+        st_g(sv_xh, c.tok0, rt, c.NR, ct_pack(xh), lane);
+        st_tokf(sv_rs, rt, rs, c);
+      }
     }
   }  CP_MARK(22);
 }
@@ -771,7 +790,7 @@ __device__ __forceinline__ void self_attn_fwd_ct(const Mat* m, const LNp& ln, CT
 // MLP: x <- LN(x + W2 GELU(W1 x + b1) + b2)   (ma_transformer.py:84-86,91-92)
 template <bool SAVE>
 __device__ __forceinline__ void mlp_fwd_ct(const Mat& m1, const Mat& m2, const LNp& ln, CT* xr, bf16_t* sv_x, bf16_t* sv_g,
-                                           bf16_t* sv_gp, const Ctx& c) {
+                                           bf16_t* sv_gp, bf16_t* sv_xh, float* sv_rs, const Ctx& c) {
   const int lane = c.lane;
   AFr W1, W2;
   loadA(W1, m1.fa, lane);
@@ -798,7 +817,11 @@ __device__ __forceinline__ void mlp_fwd_ct(const Mat& m1, const Mat& m2, const L
       }
       CT mo = ct_add(b2, xr[k]), xh;
       mm(mo, W2, gr);
-      ln_fwd_ct(mo, xh, xr[k], gam, bet);
+      const float rs = ln_fwd_ct(mo, xh, xr[k], gam, bet);
+      if (SAVE) {
+        st_g(sv_xh, c.tok0, rt, c.NR, ct_pack(xh), lane);
+        st_tokf(sv_rs, rt, rs, c);
+      }
     }
   }
   CP_MARK(23);
@@ -809,22 +832,24 @@ __device__ __forceinline__ void mlp_fwd_ct(const Mat& m1, const Mat& m2, const L
 // under 256 registers): each pass leaves its per-tile products in this wave's own LDS rows (read back by the same
 // lanes, so no barrier between passes) or in dx.
 __device__ __forceinline__ void mlp_bwd_ct(const Mat& m1, const Mat& m2, const LNp& ln, CT* dx, const bf16_t* sv_x,
-                                           const bf16_t* sv_g, const bf16_t* sv_gp, const Ctx& c) {
+                                           const bf16_t* sv_g, const bf16_t* sv_gp, const bf16_t* sv_xh,
+                                           const float* sv_rs, const Ctx& c) {
   const int lane = c.lane;
-  {   // pass 1 (W2): LN backward -> ds (dx) ; DA = dY of W2, XB = X of W2 (GELU(h))
+  {   // pass 1: LN backward from the saved x-hat / rstd -> ds (dx) ; DA = dY of W2, XB = X of W2 (GELU(h))
     CT dlg, dlb;
     ct_zero(dlg);
     ct_zero(dlb);
-    AFr W2f;
-    loadA(W2f, m2.fa, lane);
-    const CT b2 = ld_vec(m2.b, lane), gam = ld_vec(ln.g, lane), bet = ld_vec(ln.b, lane);
-    CTr xs[MAXRT], hs[MAXRT];
+    const CT gam = ld_vec(ln.g, lane);
+    CTr xs[MAXRT], hs[MAXRT], xhs[MAXRT];
+    float rsv[MAXRT];
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {   // every saved-activation load of the wave issued up front
       const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         xs[k] = ld_g(sv_x, c.tok0, rt, c.NR, lane);
         hs[k] = ld_g(sv_g, c.tok0, rt, c.NR, lane);
+        xhs[k] = ld_g(sv_xh, c.tok0, rt, c.NR, lane);
+        rsv[k] = ld_tokf(sv_rs, rt, c);
       }
     }
 #pragma unroll
@@ -833,10 +858,8 @@ __device__ __forceinline__ void mlp_bwd_ct(const Mat& m1, const Mat& m2, const L
       if (rt < c.NT) {
         const bool ok = tok_ok(rt, c);
         const CTr glr = hs[k];   // GELU(h): the forward's own W2 operand
-        CT mo = ct_add(b2, ct_unpack(xs[k])), xh, yy, ds;
-        mm(mo, W2f, glr);
-        const float rs = ln_fwd_ct(mo, xh, yy, gam, bet);
-        ln_bwd_ct(dx[k], xh, rs, gam, ok, ds, dlg, dlb);
+        CT ds;
+        ln_bwd_ct(dx[k], ct_unpack(xhs[k]), rsv[k], gam, ok, ds, dlg, dlb);
         st_lds(c.DA, rt, ct_pack(ds), ok, lane);   // dY of W2
         st_lds(c.XB, rt, glr, ok, lane);           // X of W2
         st_lds(c.QB, rt, xs[k], ok, lane);         // X of W1
@@ -888,7 +911,8 @@ __device__ __forceinline__ void mlp_bwd_ct(const Mat& m1, const Mat& m2, const L
 // gradient dO must already be in DA.
 __device__ __forceinline__ void self_attn_bwd_ct(const Mat* m, const LNp& ln, CT* dx, const bf16_t* sv_xin,
                                                  const bf16_t* sv_a, const bf16_t* sv_alo, const float* sv_lse,
-                                                 bool causal, const Ctx& c) {
+                                                 const bf16_t* sv_xh, const float* sv_rs, bool causal,
+                                                 const Ctx& c) {
   const int lane = c.lane;
   const LseR lse = lse_fetch(sv_lse, c);   // consumed after the recompute phase (latency hidden by passes 1-2)
   CTr xin[MAXRT];
@@ -896,17 +920,18 @@ __device__ __forceinline__ void self_attn_bwd_ct(const Mat* m, const LNp& ln, CT
     CT dlg, dlb;
     ct_zero(dlg);
     ct_zero(dlb);
-    {   // pass 1 (Wp): LN backward -> ds (dx) ; DQ = dY of Wp, XB = X of Wp
-      AFr Wpf;
-      loadA(Wpf, m[3].fa, lane);
-      const CT bp = ld_vec(m[3].b, lane), gam = ld_vec(ln.g, lane), bet = ld_vec(ln.b, lane);
-      CTr as[MAXRT];
+    {   // pass 1: LN backward from the saved x-hat / rstd -> ds (dx) ; DQ = dY of Wp, XB = X of Wp
+      const CT gam = ld_vec(ln.g, lane);
+      CTr as[MAXRT], xhs[MAXRT];
+      float rsv[MAXRT];
 #pragma unroll
       for (int k = 0; k < MAXRT; ++k) {
         const int rt = c.wave + NW * k;
         if (rt < c.NT) {
           as[k] = ld_g(sv_a, c.tok0, rt, c.NR, lane);
           xin[k] = ld_g(sv_xin, c.tok0, rt, c.NR, lane);
+          xhs[k] = ld_g(sv_xh, c.tok0, rt, c.NR, lane);
+          rsv[k] = ld_tokf(sv_rs, rt, c);
         }
       }
 #pragma unroll
@@ -914,10 +939,8 @@ __device__ __forceinline__ void self_attn_bwd_ct(const Mat* m, const LNp& ln, CT
         const int rt = c.wave + NW * k;
         if (rt < c.NT) {
           const bool ok = tok_ok(rt, c);
-          CT s = ct_add(bp, ct_unpack(xin[k])), xh, yy, ds;
-          mm(s, Wpf, as[k]);
-          const float rs = ln_fwd_ct(s, xh, yy, gam, bet);
-          ln_bwd_ct(dx[k], xh, rs, gam, ok, ds, dlg, dlb);
+          CT ds;
+          ln_bwd_ct(dx[k], ct_unpack(xhs[k]), rsv[k], gam, ok, ds, dlg, dlb);
           st_lds(c.DQ, rt, ct_pack(ds), ok, lane);   // dY of Wp
           st_lds(c.XB, rt, as[k], ok, lane);         // X of Wp
           dx[k] = ds;                                // residual path

@@ -34,8 +34,15 @@ class Blk(ctypes.Structure):
 
 
 class Sv(ctypes.Structure):
-    # g / gp: the MLP's GELU(h) and GELU'(h) as bf16 (the backward recomputes neither)
-    _fields_ = [(n, VP) for n in ("xin", "a1", "lse1", "x1", "a2", "lse2", "x2", "g", "a1lo", "a2lo", "gp")]
+    # g / gp: the MLP's GELU(h) and GELU'(h) as bf16 (the backward recomputes neither); xh0..2 / rs: x-hat (bf16) and
+    # rstd ([tok][4] f32) of the block's LayerNorms (the backward recomputes no LayerNorm forward)
+    _fields_ = [(n, VP) for n in ("xin", "a1", "lse1", "x1", "a2", "lse2", "x2", "g", "a1lo", "a2lo", "gp", "xh0", "xh1",
+                                  "xh2", "rs")]
+
+
+class HSv(ctypes.Structure):
+    # x-hat, GELU'(pre-activation) (bf16 [tok][64]) and rstd ([tok] f32) of a GELU -> LayerNorm head / embedding
+    _fields_ = [("xh", VP), ("gp", VP), ("rs", VP)]
 
 
 class EncP(ctypes.Structure):
@@ -44,7 +51,7 @@ class EncP(ctypes.Structure):
                                   "d_be", "d_ln0_g", "d_ln0_b")] + \
                [("blk", Blk * 3), ("h1", Mat), ("lnh", LNp), ("wh2", VP), ("bh2", VP), ("d_wh2", VP), ("rep", VP),
                 ("v", VP), ("sv", Sv * 3), ("drep", VP), ("dv", VP), ("g_delta", ctypes.c_longlong),
-                ("g_stride", ctypes.c_longlong), ("g_copies", ctypes.c_int), ("d_bh2", VP)]
+                ("g_stride", ctypes.c_longlong), ("g_copies", ctypes.c_int), ("d_bh2", VP), ("hs", HSv), ("es", HSv)]
 
 
 class DecP(ctypes.Structure):
@@ -55,7 +62,7 @@ class DecP(ctypes.Structure):
                                   "ent")] + \
                [("sv", Sv * 3)] + [(n, VP) for n in ("dlogp", "dent", "drep", "sv_head")] + \
                [("g_delta", ctypes.c_longlong), ("g_stride", ctypes.c_longlong), ("g_copies", ctypes.c_int)] + \
-               [("cont", ctypes.c_int), ("ba", VP), ("d_ba", VP)]
+               [("cont", ctypes.c_int), ("ba", VP), ("d_ba", VP), ("hs", HSv)]
 
 
 # Training kernels (csrc/mat_train_ct.h): token-on-lane tiles, weight A fragments in permuted k order, register-
@@ -351,20 +358,31 @@ class EncoderFused:
         saves = []
         if save:
             for bi in range(m.n_block):
-                t = torch.empty(6, n_tok, 64, device=dev, dtype=torch.bfloat16)
+                t = torch.empty(8, n_tok, 64, device=dev, dtype=torch.bfloat16)
                 lse = torch.empty(n_tok, 2, device=dev)
-                saves += [t, lse]
+                rs = torch.empty(3, n_tok, device=dev)   # LayerNorm rstd, slot-major
+                saves += [t, lse, rs]
                 p.sv[bi] = Sv(t[0].data_ptr(), t[1].data_ptr(), lse.data_ptr(), t[2].data_ptr(), None, None, None,
-                              t[3].data_ptr(), t[4].data_ptr(), None, t[5].data_ptr())
+                              t[3].data_ptr(), t[4].data_ptr(), None, t[5].data_ptr(), t[6].data_ptr(), t[7].data_ptr(),
+                              None, rs.data_ptr())
+            hv = torch.empty(4, n_tok, 64, device=dev, dtype=torch.bfloat16)   # head / embedding x-hat, GELU'
+            hr = torch.empty(2, n_tok, device=dev)                              # head / embedding rstd
+            saves += [hv, hr]
+            p.hs = HSv(hv[0].data_ptr(), hv[1].data_ptr(), hr[0].data_ptr())
+            p.es = HSv(hv[2].data_ptr(), hv[3].data_ptr(), hr[1].data_ptr())
+        else:
+            p.hs, p.es = HSv(), HSv()
         check(_enc_fwd(sfx, p, _ptr(pre), m.n_block, save), "mat_enc_fwd")
-        self.ctx = (obs, rep, v, saves, [Sv.from_buffer_copy(p.sv[i]) for i in range(m.n_block)], pre, stat)
+        self.ctx = (obs, rep, v, saves, [Sv.from_buffer_copy(p.sv[i]) for i in range(m.n_block)], pre, stat,
+                    HSv.from_buffer_copy(p.hs), HSv.from_buffer_copy(p.es))
         return v, rep
 
     def backward(self, drep, dv):
         m = self.model
-        obs, rep, v, saves, svs, pre, stat = self.ctx
+        obs, rep, v, saves, svs, pre, stat, hs, es = self.ctx
         self._build()
         p = self.p
+        p.hs, p.es = hs, es
         drep = drep.float().contiguous()
         dv = dv.float().contiguous()
         B, L, od = obs.shape
@@ -463,23 +481,28 @@ class DecoderFused:
         saves = []
         if save:
             for bi in range(m.n_block):
-                t = torch.empty(9, n_tok, 64, device=dev, dtype=torch.bfloat16)
+                t = torch.empty(12, n_tok, 64, device=dev, dtype=torch.bfloat16)
                 lse = torch.empty(2, n_tok, 2, device=dev)
-                saves += [t, lse]
+                rs = torch.empty(3, n_tok, device=dev)   # LayerNorm rstd, slot-major
+                saves += [t, lse, rs]
                 p.sv[bi] = Sv(t[0].data_ptr(), t[1].data_ptr(), lse[0].data_ptr(), t[2].data_ptr(), t[3].data_ptr(),
                               lse[1].data_ptr(), t[4].data_ptr(), t[5].data_ptr(), t[6].data_ptr(), t[7].data_ptr(),
-                              t[8].data_ptr())
-            head = torch.empty(n_tok, 64, device=dev, dtype=torch.bfloat16)
-            saves.append(head)
-            p.sv_head = head.data_ptr()
+                              t[8].data_ptr(), t[9].data_ptr(), t[10].data_ptr(), t[11].data_ptr(), rs.data_ptr())
+            head = torch.empty(3, n_tok, 64, device=dev, dtype=torch.bfloat16)   # head input, x-hat, GELU'
+            hr = torch.empty(n_tok, device=dev)
+            saves += [head, hr]
+            p.sv_head = head[0].data_ptr()
+            p.hs = HSv(head[1].data_ptr(), head[2].data_ptr(), hr.data_ptr())
+        else:
+            p.hs = HSv()
         check(getattr(lib(), "mdl_mat_dec_fwd" + sfx)(ctypes.byref(p), m.n_block, int(save), kernels._stream()), "mat_dec_fwd")
         self.ctx = (rep, act, ava_c, logp, ent, saves, [Sv.from_buffer_copy(p.sv[i]) for i in range(m.n_block)],
-                    p.sv_head)
+                    p.sv_head, HSv.from_buffer_copy(p.hs))
         return logp, ent
 
     def backward(self, dlogp, dent):
         m = self.model
-        rep, act, ava_c, logp, ent, saves, svs, head = self.ctx
+        rep, act, ava_c, logp, ent, saves, svs, head, hs = self.ctx
         self._build()
         B, L = act.shape[:2]
         sfx = self._geom(B, L)
@@ -490,6 +513,7 @@ class DecoderFused:
         drep = torch.empty_like(rep)
         p.act, p.ava, p.rep = act.data_ptr(), _ptr(ava_c), rep.data_ptr()
         p.dlogp, p.dent, p.drep, p.sv_head = dlogp.data_ptr(), dent.data_ptr(), drep.data_ptr(), head
+        p.hs = hs
         for i, s in enumerate(svs):
             p.sv[i] = s
         p.g_delta, p.g_stride, p.g_copies = m._mdl_gws if getattr(m, "_mdl_gws_active", False) else (0, 0, 0)
