@@ -15,5 +15,6 @@ for cfg in ${TRAIN_CFGS:-"c5e4:51200000:--lr,5e-4,--critic_lr,5e-4" "d5e4:512000
   grep -E "FPS" $O/train_$name.log | tail -n 1
   cp $(find $O/$name -name summary.json | head -1) $O/summary_$name.json 2>/dev/null
 done
+[ -n "$NO_EVAL" ] && exit 0
 cks=$(find $O -name "transformer_*.pt" | sort -V)
 timeout -k 10 400 python -u scripts/eval_ckpts.py --n_workers 32 --json $O/eval_ckpts.json $cks | tee $O/eval_ckpts.md || exit 2
