@@ -211,7 +211,8 @@ def _native_build():
     return kernels.BUILD_ID
 
 
-DEFAULT_CKPT = {32: "profiles/r1_train32/transformer_799.pt"}
+# 32 workers: trained by the round-4 code (linear LR decay, 44.8 M env steps; profiles/r4_train32/README.md)
+DEFAULT_CKPT = {32: "profiles/r4_train32/transformer_3500_lrdecay.pt"}
 
 
 def eval_block(a, args, runner, dev):

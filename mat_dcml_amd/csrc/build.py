@@ -29,11 +29,21 @@ PER_FILE_FLAGS = {
     # the SMAC env must round every product / sum like the torch path: hip's __fmul_rn / __fadd_rn are plain
     # operators that -ffp-contract=fast still fuses into FMAs (battle positions drifted by an ulp)
     "smac_env.hip": ["-ffp-contract=off"],
+    # MFMA results written straight to VGPRs: by default hipcc accumulates in AGPRs and copies every result to a VGPR
+    # for the VALU work that follows (847 v_accvgpr moves per agent step in the one-wave decode, 131 with this form)
+    "mat_decode_wave.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
+    "mat_decode.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
 }
 
 
+FWD_TUS = ("mat_enc_ct.hip", "mat_dec_ct.hip")   # the training forward translation units
+
+
 def _flags(src):
-    extra = os.environ.get("MAT_DCML_BWD_FLAGS", "").split() if src.endswith("_bwd.hip") else []   # A/B variants
+    # A/B variants: extra flags for the training backward / forward translation units only
+    extra = os.environ.get("MAT_DCML_BWD_FLAGS", "").split() if src.endswith("_bwd.hip") else []
+    if os.path.basename(src) in FWD_TUS:
+        extra = os.environ.get("MAT_DCML_FWD_FLAGS", "").split()
     return FLAGS + PER_FILE_FLAGS.get(os.path.basename(src), []) + extra
 
 

@@ -389,7 +389,7 @@ __global__ __launch_bounds__(NTHR, WGPC) void mat_enc_bwd_ct(EncP p, EncX ex) {
 // ============================================================================================== host API
 #ifndef MDL_CT_BWD_TU
 MDL_API int mdl_mat_train_geometry_ct(int L) {
-  const int MAXROWS = 64 * MAXRT;
+  const int MAXROWS = 16 * NW * MAXRT;   // row tiles of one round of the forward's waves
   int SQ = MAXROWS / L;
   if (SQ < 1) return 0;
   int NRP = ((SQ * L + 31) / 32) * 32;

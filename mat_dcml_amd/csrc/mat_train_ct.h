@@ -54,7 +54,10 @@ __shared__ unsigned long long cp_acc[64];
 
 // Forward kernels keep only Q / K / V in LDS (3 of the 6 token-major buffers): 74 KB at 192 rows, so TWO
 // workgroups fit per CU (8 waves, 2 per SIMD: one workgroup's load / barrier stalls overlap the other's compute).
-constexpr int FWD_WGPC = 2;
+#ifndef MDL_FWD_WGPC
+#define MDL_FWD_WGPC 2
+#endif
+constexpr int FWD_WGPC = MDL_FWD_WGPC;
 __host__ __device__ inline size_t ct_fwd_lds_bytes(int NRP) { return (size_t)NRP * 64 * 2 * 3; }
 
 template <typename K, typename PT, typename... X>

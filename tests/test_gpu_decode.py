@@ -141,7 +141,10 @@ def test_decode_latency(gpu, L):
         mat_fused.decode(m, rep, ava, False, 1, rand)
     e.record()
     torch.cuda.synchronize()
-    print(f"mat_decode B=256 L={L}: {s.elapsed_time(e) / 20 * 1e3:.1f} us per env step")
+    us = s.elapsed_time(e) / 20 * 1e3
+    print(f"mat_decode B=256 L={L}: {us:.1f} us per env step")
+    # regression bounds (~1.4x the round-4 measurement: 282 us one-wave at L = 33, 1,072 us 4-wave at L = 101)
+    assert us < {33: 400.0, 101: 1500.0}[L], us
 
 
 @pytest.mark.parametrize("L,A,B", [(6, 1, 64), (2, 6, 40), (17, 3, 16), (33, 2, 8)])

@@ -368,3 +368,36 @@ def test_mat_dec_runner_trains_through_the_hybrid_path(gpu):
     torch.cuda.synchronize()
     assert all(torch.isfinite(torch.as_tensor(float(v))) for v in infos.values()), infos
     assert r.policy.transformer._mdl_train_state[0].ctx is None   # every fused encoder forward got its backward
+
+
+def test_training_kernels_time_bound(gpu):
+    """The four fused training kernels at the bench minibatch (3,200 sequences x 33 agents, n_block 2): hipEvent time
+    per minibatch (printed) under a regression bound of ~1.4x the round-4 measurement (1.17 ms)."""
+    B, L = 3200, 33
+    m = make(L, gpu, seed=0, scale=0.05)
+    obs = torch.rand(B, L, 7, device=gpu)
+    ava = torch.ones(B, L, 2, device=gpu)
+    actions = (torch.rand(B, L, 1, device=gpu) < 0.5).float()
+    for p in m.parameters():
+        p.grad = torch.zeros_like(p)
+    enc, dec = mat_train.EncoderFused(m), mat_train.DecoderFused(m)
+
+    def step():
+        v, rep = enc.forward(obs)
+        lp, ent = dec.forward(rep, actions, ava)
+        drep = dec.backward(torch.ones_like(lp), torch.ones_like(ent))
+        enc.backward(drep, torch.ones_like(v))
+
+    step()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(10):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        step()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b))
+    ms = sorted(ts)[len(ts) // 2]
+    print(f"four training kernels, 3200 x 33: {ms:.3f} ms per minibatch")
+    assert ms < 1.65, ms
