@@ -79,7 +79,9 @@ __host__ __device__ inline WvLds wv_lds(int NB, int L, int n_tok, int nlds) {
   return o;
 }
 
-__device__ __forceinline__ int wv_kvrow(int b, int kind, int j, int L) { return (b * 4 + kind) * L + j; }
+// K / V cache (block b, kind: 0 self K, 1 self V, 2 cross K, 3 cross V) = rows [(4b + kind) L, (4b + kind + 1) L)
+// of the KV array; rows inside a cache are swizzled relative to its first row (wv_attn)
+__device__ __forceinline__ bf16_t* wv_cache(bf16_t* KV, int b, int kind, int L) { return KV + (size_t)(b * 4 + kind) * L * 64; }
 
 template <int N>
 struct RegW { AFr w[N > 0 ? N : 1]; };
@@ -145,7 +147,10 @@ __device__ __forceinline__ CT gelu_dist(const CT& h, int lane) {
 // column c carries head c >> 3.  Scores Sᵀ = K·Qᵀ per 16-key half t (A rows = keys kb + pi_row(t, m), k = the
 // head's 32 dims in the CT permuted order, so the query is its CT registers), online softmax in log2 units, P as a
 // hi/lo bf16 pair, Oᵀ = Vᵀ·Pᵀ with Vᵀ from ds_read_b64_tr_b16; O returned in CT layout (replicated).
-__device__ __forceinline__ CT wv_attn(const bf16_t* KV, int rK, int rV, const CTr& qr, int i, int lane) {
+// Rows are addressed relative to each cache's first row (K = Kc, V = Vc: the swizzle only has to agree between the
+// row's writer and readers), so every lane's swizzled offsets are the same for all caches and agent steps (hoisted
+// out of the agent loop) and a 32-row key chunk only adds kb * 64 (a 32-row step keeps the (row >> 1) & 7 swizzle).
+__device__ __forceinline__ CT wv_attn(const bf16_t* Kc, const bf16_t* Vc, const CTr& qr, int i, int lane) {
   const int g = lane >> 4, c = lane & 15;
   const bool h1 = c >= 8;
   const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -158,9 +163,10 @@ __device__ __forceinline__ CT wv_attn(const bf16_t* KV, int rK, int rV, const CT
     float sc[8];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      const int key = rK + kb + pi_row(t, c);
-      const uint2 p0 = kv_ld2(KV, key, 4 * g), p1 = kv_ld2(KV, key, 16 + 4 * g);
-      const uint2 p2 = kv_ld2(KV, key, 32 + 4 * g), p3 = kv_ld2(KV, key, 48 + 4 * g);
+      const bf16_t* Kk = Kc + kb * 64;
+      const int key = pi_row(t, c);
+      const uint2 p0 = kv_ld2(Kk, key, 4 * g), p1 = kv_ld2(Kk, key, 16 + 4 * g);
+      const uint2 p2 = kv_ld2(Kk, key, 32 + 4 * g), p3 = kv_ld2(Kk, key, 48 + 4 * g);
       f32x4 r = __builtin_amdgcn_mfma_f32_16x16x32_bf16(mk8(p0.x, p0.y, p1.x, p1.y), qb0, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
       r = __builtin_amdgcn_mfma_f32_16x16x32_bf16(mk8(p2.x, p2.y, p3.x, p3.y), qb1, r, 0, 0, 0);
 #pragma unroll
@@ -186,7 +192,7 @@ __device__ __forceinline__ CT wv_attn(const bf16_t* KV, int rK, int rV, const CT
     split8v(sc, ph, pl);
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
-      const bf16x8 va = ld_frag_T(KV, rV + kb, 16 * mt, lane);
+      const bf16x8 va = ld_frag_T(Vc + kb * 64, 0, 16 * mt, lane);
       o[mt] *= alpha;
       o[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, ph, o[mt], 0, 0, 0);
       o[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pl, o[mt], 0, 0, 0);
@@ -194,19 +200,6 @@ __device__ __forceinline__ CT wv_attn(const bf16_t* KV, int rK, int rV, const CT
     m = nm;
   }
   const float il = 1.f / cross_row_sum(l);
-#ifdef MDL_WAVE_DEBUG
-  if (rK == 0) {   // block 0 self attention: the cached V row 0 (CT read) and O before the head exchange
-    CT vr, pre;
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const uint2 u = kv_ld2(KV, rV, 16 * mt + 4 * g);
-      vr.v[mt] = f32x4{blo(u.x), bhi(u.x), blo(u.y), bhi(u.y)};
-      pre.v[mt] = o[mt] * il;
-    }
-    wdbg(14, vr, i, lane);
-    wdbg(15, pre, i, lane);
-  }
-#endif
   CT O;
   // columns c < 8 hold head 0 (dims 0..31 = mt 0, 1), c >= 8 head 1 (mt 2, 3): each takes the other half from c ^ 8
   O.v[0] = ror8_banks<0xC>(o[0] * il);
@@ -237,8 +230,8 @@ __device__ __forceinline__ void wv_block(CT& x, const WvCtx& k, const RegW<NREG>
     if ((lane & 15) == 0) {
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
-        *(uint2*)(k.KV + tmo(wv_kvrow(0, 0, i, L), 16 * mt + 4 * g)) = *(const uint2*)(t + 64 + 16 * mt + 4 * g);
-        *(uint2*)(k.KV + tmo(wv_kvrow(0, 1, i, L), 16 * mt + 4 * g)) = *(const uint2*)(t + 128 + 16 * mt + 4 * g);
+        *(uint2*)(wv_cache(k.KV, 0, 0, L) + tmo(i, 16 * mt + 4 * g)) = *(const uint2*)(t + 64 + 16 * mt + 4 * g);
+        *(uint2*)(wv_cache(k.KV, 0, 1, L) + tmo(i, 16 * mt + 4 * g)) = *(const uint2*)(t + 128 + 16 * mt + 4 * g);
       }
     }
     x = ld_vec(k.ET + tok * 64, lane);
@@ -253,13 +246,13 @@ __device__ __forceinline__ void wv_block(CT& x, const WvCtx& k, const RegW<NREG>
     wv_getw<wv_slot(B, 2), NLDS, NREG>(w, rw, k.W, lane);
     mm(vv, w, xp);
     qr = ct_pack(q);
-    kv_st_row(k.KV, wv_kvrow(B, 0, i, L), ct_pack(kk), lane);
-    kv_st_row(k.KV, wv_kvrow(B, 1, i, L), ct_pack(vv), lane);
+    kv_st_row(wv_cache(k.KV, B, 0, L), i, ct_pack(kk), lane);
+    kv_st_row(wv_cache(k.KV, B, 1, L), i, ct_pack(vv), lane);
   }
   asm volatile("" ::: "memory");   // the cache row above is read back by other lanes below (LDS is in order per wave)
   WDBG(6 * B + 0, x);
   {
-    const CT O = wv_attn(k.KV, wv_kvrow(B, 0, 0, L), wv_kvrow(B, 1, 0, L), qr, i, lane);
+    const CT O = wv_attn(wv_cache(k.KV, B, 0, L), wv_cache(k.KV, B, 1, L), qr, i, lane);
     WDBG(6 * B + 1, O);
     wv_getw<wv_slot(B, 3), NLDS, NREG>(w, rw, k.W, lane);
     CT t = ct_add(ld_vec(k.BI + 64 * (10 * B + 3), lane), x);
@@ -273,8 +266,8 @@ __device__ __forceinline__ void wv_block(CT& x, const WvCtx& k, const RegW<NREG>
     mm(kk, w, xp);
     wv_getw<wv_slot(B, 6), NLDS, NREG>(w, rw, k.W, lane);
     mm(vv, w, xp);
-    kv_st_row(k.KV, wv_kvrow(B, 2, i, L), ct_pack(kk), lane);
-    kv_st_row(k.KV, wv_kvrow(B, 3, i, L), ct_pack(vv), lane);
+    kv_st_row(wv_cache(k.KV, B, 2, L), i, ct_pack(kk), lane);
+    kv_st_row(wv_cache(k.KV, B, 3, L), i, ct_pack(vv), lane);
   }
   asm volatile("" ::: "memory");
   {
@@ -282,7 +275,7 @@ __device__ __forceinline__ void wv_block(CT& x, const WvCtx& k, const RegW<NREG>
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) q2.q[mt] = *(const uint2*)(k.Q2 + (size_t)(B * L + i) * 64 + 16 * mt + 4 * g);
     WDBG(6 * B + 2, x);
-    const CT O = wv_attn(k.KV, wv_kvrow(B, 2, 0, L), wv_kvrow(B, 3, 0, L), q2, i, lane);
+    const CT O = wv_attn(wv_cache(k.KV, B, 2, L), wv_cache(k.KV, B, 3, L), q2, i, lane);
     WDBG(6 * B + 3, O);
     wv_getw<wv_slot(B, 7), NLDS, NREG>(w, rw, k.W, lane);
     CT t = ct_add(ld_vec(k.BI + 64 * (10 * B + 7), lane), repi);
@@ -411,6 +404,8 @@ __global__ __launch_bounds__(64, 1) void mat_decode_wave_kernel(DecParams p) {
     }
     if (n_disc < L) zlast = p.gen ? draw_n(p, env, L - 1, A - 1) : p.rnd_n[((size_t)env * L + L - 1) * A + A - 1];
   }
+  // opaque: otherwise hipcc re-materialises the Philox rounds inside the agent loop (~80 VALU per agent step)
+  asm volatile("" : "+v"(U[0]), "+v"(U[1]), "+v"(U[2]), "+v"(zlast));
   __syncthreads();
 
   // ---------------------------------------------------------------- agent loop

@@ -84,13 +84,6 @@ def stages(L=33, nb=2, rows=(0,)):
                 kk = k[6 * b + j]
                 print(f"  b{b}.{nm:8s} max|ref| {r.abs().max().item():8.4f}  max|err| {(kk - r.cpu()).abs().max().item():9.5f}"
                       f"  first {kk[:4].tolist()} ref {r[:4].cpu().tolist()}")
-        if row == 0:
-            v0 = mat_fused.decoder_pack(m)["qkv0"][0, 2].cpu()
-            print("  v table   ", [round(x, 4) for x in v0[:12].tolist()])
-            print("  V cache   ", [round(x, 4) for x in k[14][:12].tolist()])
-            print("  O pre-swap", [round(x, 4) for x in k[15][:12].tolist()])
-            print("  O kernel  ", [round(x, 4) for x in k[1][:12].tolist()])
-            print("  O ref     ", [round(x, 4) for x in ref["b0.O_self"][:12].cpu().tolist()])
         r = ref["head.h"]
         print(f"  head.h     max|err| {(k[12] - r.cpu()).abs().max().item():9.5f}")
         r = ref["head.logits"]
