@@ -150,46 +150,52 @@ __device__ __forceinline__ CT gelu_dist(const CT& h, int lane) {
 // Rows are addressed relative to each cache's first row (K = Kc, V = Vc: the swizzle only has to agree between the
 // row's writer and readers), so every lane's swizzled offsets are the same for all caches and agent steps (hoisted
 // out of the agent loop) and a 32-row key chunk only adds kb * 64 (a 32-row step keeps the (row >> 1) & 7 swizzle).
-__device__ __forceinline__ CT wv_attn(const bf16_t* Kc, const bf16_t* Vc, const CTr& qr, int i, int lane) {
+// One 32-key chunk of the online softmax (FIRST: the chunk at key 0, which every row has — no running state to
+// rescale, so the common L <= 32 case runs no loop and carries no registers around one).
+template <bool FIRST>
+__device__ __forceinline__ void wv_attn_chunk(const bf16_t* Kc, const bf16_t* Vc, const bf16x8& qb0, const bf16x8& qb1,
+                                              int kb, int i, int lane, float& m, float& l, f32x4 (&o)[4]) {
   const int g = lane >> 4, c = lane & 15;
-  const bool h1 = c >= 8;
-  const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
-  const bf16x8 qb0 = h1 ? z8 : rb(qr, 0), qb1 = h1 ? rb(qr, 1) : z8;
-  float m = -INFINITY, l = 0.f;
-  f32x4 o[4];
+  float sc[8];
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt) o[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int kb = 0; kb <= i; kb += 32) {
-    float sc[8];
+  for (int t = 0; t < 2; ++t) {
+    const bf16_t* Kk = Kc + kb * 64;
+    const int key = pi_row(t, c);
+    const uint2 p0 = kv_ld2(Kk, key, 4 * g), p1 = kv_ld2(Kk, key, 16 + 4 * g);
+    const uint2 p2 = kv_ld2(Kk, key, 32 + 4 * g), p3 = kv_ld2(Kk, key, 48 + 4 * g);
+    f32x4 r = __builtin_amdgcn_mfma_f32_16x16x32_bf16(mk8(p0.x, p0.y, p1.x, p1.y), qb0, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    r = __builtin_amdgcn_mfma_f32_16x16x32_bf16(mk8(p2.x, p2.y, p3.x, p3.y), qb1, r, 0, 0, 0);
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const bf16_t* Kk = Kc + kb * 64;
-      const int key = pi_row(t, c);
-      const uint2 p0 = kv_ld2(Kk, key, 4 * g), p1 = kv_ld2(Kk, key, 16 + 4 * g);
-      const uint2 p2 = kv_ld2(Kk, key, 32 + 4 * g), p3 = kv_ld2(Kk, key, 48 + 4 * g);
-      f32x4 r = __builtin_amdgcn_mfma_f32_16x16x32_bf16(mk8(p0.x, p0.y, p1.x, p1.y), qb0, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      r = __builtin_amdgcn_mfma_f32_16x16x32_bf16(mk8(p2.x, p2.y, p3.x, p3.y), qb1, r, 0, 0, 0);
+    for (int rr = 0; rr < 4; ++rr) sc[4 * t + rr] = r[rr];
+  }
+  const int d0 = i - kb - 8 * g;   // key kb + 8g + j is visible iff j <= d0
+  float cm = -INFINITY;
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) sc[4 * t + rr] = r[rr];
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = j <= d0 ? sc[j] : -INFINITY;
+    cm = fmaxf(cm, sc[j]);
+  }
+  const float cmax = cross_row_max(cm) * ATT_L2;   // finite: key kb <= i is visible
+  const float nm = FIRST ? cmax : fmaxf(m, cmax);
+  float ps = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = fast_exp2(fmaf(sc[j], ATT_L2, -nm));
+    ps += sc[j];
+  }
+  bf16x8 ph, pl;
+  split8v(sc, ph, pl);
+  if constexpr (FIRST) {
+    l = ps;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const bf16x8 va = ld_frag_T(Vc, 0, 16 * mt, lane);
+      o[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, ph, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      o[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pl, o[mt], 0, 0, 0);
     }
-    const int d0 = i - kb - 8 * g;   // key kb + 8g + j is visible iff j <= d0
-    float cm = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      sc[j] = j <= d0 ? sc[j] : -INFINITY;
-      cm = fmaxf(cm, sc[j]);
-    }
-    const float nm = fmaxf(m, cross_row_max(cm) * ATT_L2);   // finite: key kb <= i is visible
+  } else {
     const float alpha = fast_exp2(m - nm);
-    float ps = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      sc[j] = fast_exp2(fmaf(sc[j], ATT_L2, -nm));
-      ps += sc[j];
-    }
     l = l * alpha + ps;
-    bf16x8 ph, pl;
-    split8v(sc, ph, pl);
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       const bf16x8 va = ld_frag_T(Vc + kb * 64, 0, 16 * mt, lane);
@@ -197,8 +203,27 @@ __device__ __forceinline__ CT wv_attn(const bf16_t* Kc, const bf16_t* Vc, const 
       o[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, ph, o[mt], 0, 0, 0);
       o[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pl, o[mt], 0, 0, 0);
     }
-    m = nm;
   }
+  m = nm;
+}
+
+__device__ __forceinline__ CT wv_attn(const bf16_t* Kc, const bf16_t* Vc, const CTr& qr, int i, int lane) {
+  const int c = lane & 15;
+  const bool h1 = c >= 8;
+  const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+  const bf16x8 qb0 = h1 ? z8 : rb(qr, 0), qb1 = h1 ? rb(qr, 1) : z8;
+  float m, l;
+  f32x4 o[4];
+#ifdef MDL_WV_NOPEEL
+  m = -INFINITY;
+  l = 0.f;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) o[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int kb = 0; kb <= i; kb += 32) wv_attn_chunk<false>(Kc, Vc, qb0, qb1, kb, i, lane, m, l, o);
+#else
+  wv_attn_chunk<true>(Kc, Vc, qb0, qb1, 0, i, lane, m, l, o);
+  for (int kb = 32; kb <= i; kb += 32) wv_attn_chunk<false>(Kc, Vc, qb0, qb1, kb, i, lane, m, l, o);
+#endif
   const float il = 1.f / cross_row_sum(l);
   CT O;
   // columns c < 8 hold head 0 (dims 0..31 = mt 0, 1), c >= 8 head 1 (mt 2, 3): each takes the other half from c ^ 8
