@@ -63,7 +63,10 @@ __host__ __device__ constexpr int wv_slot(int b, int k) {   // k = linear within
 }
 
 struct WvLds { int w, kv, q2, qt, et, bi, lp, sc, total; };   // byte offsets of the LDS carve
-__host__ __device__ inline WvLds wv_lds(int NB, int L, int n_tok, int nlds) {
+// wide heads (A > 4: SMAC's 38-token tables) read the embedded input rows straight from global memory (etg): the
+// load is issued before block 0's attention and consumed after it, and the 9.7 KB it frees in LDS keeps two more
+// weight matrices out of the register file (SMAC: 4 register matrices instead of 6, which spilled)
+__host__ __device__ inline WvLds wv_lds(int NB, int L, int n_tok, int nlds, bool etg) {
   WvLds o;
   int off = 0;
   auto take = [&](int bytes) { const int r = off; off += (bytes + 15) & ~15; return r; };
@@ -71,7 +74,7 @@ __host__ __device__ inline WvLds wv_lds(int NB, int L, int n_tok, int nlds) {
   o.kv = take((NB * 4 * L + 32) * 128);      // K / V caches (+ 32 zero rows: 32-key chunks read past the last cache)
   o.q2 = take(NB * L * 128);                 // [block][row][64] bf16 cross-attention queries
   o.qt = take(n_tok * 3 * 128);              // [token][q, k, v][64] bf16 block-0 self-attention operands
-  o.et = take(n_tok * 256);                  // [token][64] f32 embedded decoder input rows (the block-0 residual)
+  o.et = take(etg ? 0 : n_tok * 256);        // [token][64] f32 embedded decoder input rows (the block-0 residual)
   o.bi = take((10 * NB + 1) * 256);          // biases
   o.lp = take((3 * NB + 1) * 512);           // LayerNorm gamma / beta
   o.sc = take(64 * 4);                       // logits of the wide head
@@ -128,13 +131,29 @@ __device__ __forceinline__ f32x4 ror8_banks(f32x4 v) {
 
 // GELU of a replicated CT vector with one erf per lane: lane c evaluates feature 16(c>>2) + 4g + (c&3), the row
 // broadcasts hand every lane its 16 results
-__device__ __forceinline__ CT gelu_dist(const CT& h, int lane) {
+__device__ __forceinline__ float gelu_pick(const CT& h, int lane) {
   const int c = lane & 15;
   const f32x4 a = (c & 4) ? h.v[1] : h.v[0];
   const f32x4 b = (c & 4) ? h.v[3] : h.v[2];
   const f32x4 v = (c & 8) ? b : a;
   const float lo = (c & 1) ? v[1] : v[0], hi = (c & 1) ? v[3] : v[2];
-  const float ge = gelu_erf((c & 2) ? hi : lo);
+  return gelu_erf((c & 2) ? hi : lo);
+}
+// ... as the packed bf16 MFMA operand: even lanes pack their pair (features 4g + r, r + 1 of tile c >> 2) after one
+// pair-swap DPP, and 8 row broadcasts of the packed words replace 16 fp32 broadcasts + 8 conversions
+__device__ __forceinline__ CTr gelu_dist_pk(const CT& h, int lane) {
+  const float ge = gelu_pick(h, lane);
+  const float nb = dppf<DPP_XOR1>(ge);
+  const float pk = __builtin_bit_cast(float, pk2(ge, nb));   // valid on even lanes c
+  CTr o;
+  o.q[0] = make_uint2(__builtin_bit_cast(uint32_t, row_bcast<0>(pk)), __builtin_bit_cast(uint32_t, row_bcast<2>(pk)));
+  o.q[1] = make_uint2(__builtin_bit_cast(uint32_t, row_bcast<4>(pk)), __builtin_bit_cast(uint32_t, row_bcast<6>(pk)));
+  o.q[2] = make_uint2(__builtin_bit_cast(uint32_t, row_bcast<8>(pk)), __builtin_bit_cast(uint32_t, row_bcast<10>(pk)));
+  o.q[3] = make_uint2(__builtin_bit_cast(uint32_t, row_bcast<12>(pk)), __builtin_bit_cast(uint32_t, row_bcast<14>(pk)));
+  return o;
+}
+__device__ __forceinline__ CT gelu_dist(const CT& h, int lane) {
+  const float ge = gelu_pick(h, lane);
   CT o;
   o.v[0] = f32x4{row_bcast<0>(ge), row_bcast<1>(ge), row_bcast<2>(ge), row_bcast<3>(ge)};
   o.v[1] = f32x4{row_bcast<4>(ge), row_bcast<5>(ge), row_bcast<6>(ge), row_bcast<7>(ge)};
@@ -236,7 +255,8 @@ __device__ __forceinline__ CT wv_attn(const bf16_t* Kc, const bf16_t* Vc, const 
 
 struct WvCtx {
   bf16_t *W, *KV, *Q2, *QT;
-  float *ET, *BI, *LP;
+  const float* ET;
+  float *BI, *LP;
   int lane, L;
 };
 
@@ -312,7 +332,7 @@ __device__ __forceinline__ void wv_block(CT& x, const WvCtx& k, const RegW<NREG>
     wv_getw<wv_slot(B, 8), NLDS, NREG>(w, rw, k.W, lane);
     mm(h, w, ct_pack(x));
     WDBG(6 * B + 4, x);
-    const CTr hp = ct_pack(gelu_dist(h, lane));
+    const CTr hp = gelu_dist_pk(h, lane);
     wv_getw<wv_slot(B, 9), NLDS, NREG>(w, rw, k.W, lane);
     CT t = ct_add(ld_vec(k.BI + 64 * (10 * B + 9), lane), x);
     mm(t, w, hp);
@@ -344,12 +364,12 @@ __global__ __launch_bounds__(64, 1) void mat_decode_wave_kernel(DecParams p) {
   constexpr int MA = WIDE ? 4 : 1;   // logit tiles (A <= 4: one tile, the logits sit in lanes g = 0)
   const int lane = threadIdx.x, g = lane >> 4, c = lane & 15;
   const int env = blockIdx.x, L = p.L, A = p.act_dim;
-  const WvLds lo = wv_lds(NB, L, p.n_tok, NLDS);
+  const WvLds lo = wv_lds(NB, L, p.n_tok, NLDS, WIDE);
   bf16_t* W = (bf16_t*)(smem + lo.w);
   bf16_t* KV = (bf16_t*)(smem + lo.kv);
   bf16_t* Q2 = (bf16_t*)(smem + lo.q2);
   bf16_t* QT = (bf16_t*)(smem + lo.qt);
-  float* ET = (float*)(smem + lo.et);
+  const float* ET = WIDE ? p.emb : (const float*)(smem + lo.et);
   float* BI = (float*)(smem + lo.bi);
   float* LP = (float*)(smem + lo.lp);
   float* SC = (float*)(smem + lo.sc);
@@ -369,7 +389,8 @@ __global__ __launch_bounds__(64, 1) void mat_decode_wave_kernel(DecParams p) {
 #pragma unroll
   for (int r = 0; r < NREG; ++r) loadA(rw.w[r], p.wfa + (size_t)wv_lin(NB, NLDS + r) * 4096, lane);
   for (int i = lane; i < p.n_tok * 192; i += 64) QT[i] = f2bf(p.qkv0[i]);
-  for (int i = lane; i < p.n_tok * 64; i += 64) ET[i] = p.emb[i];
+  if constexpr (!WIDE)
+    for (int i = lane; i < p.n_tok * 64; i += 64) ((float*)(smem + lo.et))[i] = p.emb[i];
   for (int i = lane; i < (10 * NB + 1) * 64; i += 64) BI[i] = p.bias[i];
   for (int i = lane; i < (3 * NB + 1) * 128; i += 64) LP[i] = p.lnp[i];
   for (int i = lane * 8; i < (NB * 4 * L + 32) * 64; i += 512) *(uint4*)(KV + i) = make_uint4(0, 0, 0, 0);
@@ -596,7 +617,7 @@ MDL_API int mdl_decode_wave_plan(const DecParams* p, int NB) {
   if (p->n_disc != p->L && p->n_disc != p->L - 1) return -1;
   if (!p->deterministic && !p->gen && (!p->rnd_u || (p->n_disc < p->L && !p->rnd_n))) return -1;
   for (int nreg = 0; nreg <= (NB == 1 ? 4 : 6); nreg += 2)
-    if (wv_lds(NB, p->L, p->n_tok, wv_nm(NB) - nreg).total <= 160 * 1024) return nreg;
+    if (wv_lds(NB, p->L, p->n_tok, wv_nm(NB) - nreg, p->act_dim > 4).total <= 160 * 1024) return nreg;
   return -1;
 }
 
@@ -605,7 +626,7 @@ int mdl_decode_wave(const DecParams* p, int NB, hipStream_t st) {
   if (nreg < 0) return 1;
   if (p->B <= 0) return 0;
   const bool wide = p->act_dim > 4;
-  const size_t lds = (size_t)wv_lds(NB, p->L, p->n_tok, wv_nm(NB) - nreg).total;
+  const size_t lds = (size_t)wv_lds(NB, p->L, p->n_tok, wv_nm(NB) - nreg, wide).total;
   if (NB == 1) {
     if (nreg == 0) return wv_launch<1, 0>(p, wide, lds, st);
     if (nreg == 2) return wv_launch<1, 2>(p, wide, lds, st);

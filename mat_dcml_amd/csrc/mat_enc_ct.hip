@@ -13,36 +13,33 @@ struct EncX {   // EncP extension of the round-2 kernels (passed next to EncP)
   float* dpre_out;       // [tok][64] gradient w.r.t. pre_in (backward, when pre_in is used)
 };
 
-// LN_obs of this lane's token (all od <= 16 dims in-lane); the lane's 4 dims 4g .. 4g+3 of (LN output, x-hat)
+// LN_obs of this lane's token: lane (g, c) loads and normalises only its 4 dims 4g .. 4g+3 (od <= 16), the token's
+// mean / variance reduce across the 4 lane rows (two-pass, as torch's LayerNorm); -> this lane's 4 dims of the LN
+// output and x-hat.  Padded rows read zeros (finite x-hat 0, output = beta).
 __device__ __forceinline__ void obs_ln(const EncP& p, int rt, const Ctx& c, float oh[4], float hat[4]) {
   const int lane = c.lane, g = lane >> 4, od = p.od;
   const int row = rt * 16 + (lane & 15);
   const bool ok = row < c.NR;
   const float* src = p.obs + (size_t)(c.tok0 + (ok ? row : 0)) * od;
-  float o[16];
+  float o[4];
+  bool in[4];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) o[k] = src[k < od ? k : 0];
-  float mean = 0.f;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) mean += k < od ? o[k] : 0.f;
-  mean /= (float)od;
-  float var = 0.f;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const float d = o[k] - mean;
-    var += k < od ? d * d : 0.f;
+  for (int j = 0; j < 4; ++j) {
+    const int kk = 4 * g + j;
+    in[j] = kk < od;
+    o[j] = (ok && in[j]) ? src[kk] : 0.f;
   }
+  const float mean = cross_row_sum((o[0] + o[1]) + (o[2] + o[3])) / (float)od;
+  float d[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) d[j] = in[j] ? o[j] - mean : 0.f;
+  const float var = cross_row_sum((d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]));
   const float rstd = rsqrtf(var / (float)od + 1e-5f);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    float hv = 0.f;
-#pragma unroll
-    for (int gg = 0; gg < 4; ++gg) hv = g == gg ? (o[4 * gg + j] - mean) * rstd : hv;
-    const int kk = 4 * g + j;
-    const bool in = kk < od;
-    const int ks = in ? kk : 0;
-    hat[j] = in ? hv : 0.f;
-    oh[j] = in ? hv * p.lno_g[ks] + p.lno_b[ks] : 0.f;
+    const int ks = in[j] ? 4 * g + j : 0;
+    hat[j] = d[j] * rstd;
+    oh[j] = in[j] ? hat[j] * p.lno_g[ks] + p.lno_b[ks] : 0.f;
   }
 }
 
@@ -159,16 +156,24 @@ __device__ __forceinline__ void enc_fwd_tile(const EncP& p, const EncX& ex, char
         gelu_ct(hh);
         ln_fwd_ct(hh, xh, n, gam, bet);
       }
-      float s0 = 0.f, s1 = 0.f;
+      f32x4 t0 = n.v[0] * w0.v[0], t1 = n.v[0] * w1.v[0];   // packed pairs, then both row sums side by side
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          s0 += n.v[i][r] * w0.v[i][r];
-          s1 += n.v[i][r] * w1.v[i][r];
-        }
-      s0 = cross_row_sum(s0);
-      s1 = cross_row_sum(s1);
+      for (int i = 1; i < 4; ++i) {
+        t0 = n.v[i] * w0.v[i] + t0;
+        t1 = n.v[i] * w1.v[i] + t1;
+      }
+      float s0 = (t0[0] + t0[1]) + (t0[2] + t0[3]), s1 = (t1[0] + t1[1]) + (t1[2] + t1[3]);
+      {
+        float a0, a1, b0, b1;
+        swap16(s0, a0, a1);
+        swap16(s1, b0, b1);
+        s0 = a0 + a1;
+        s1 = b0 + b1;
+        swap32(s0, a0, a1);
+        swap32(s1, b0, b1);
+        s0 = a0 + a1;
+        s1 = b0 + b1;
+      }
       if (ok && g == 0) {
         const size_t tok = (size_t)(c.tok0 + rt * 16 + (lane & 15));
         p.v[tok * p.n_obj] = s0 + p.bh2[0];

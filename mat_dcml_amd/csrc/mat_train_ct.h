@@ -294,23 +294,19 @@ __device__ __forceinline__ float ln_fwd_ct(const CT& x, CT& xh, CT& y, const CT&
 // y = LN(x) * gamma + beta; returns rstd, xh = normalised x
 __device__ __forceinline__ float ln_fwd_ct(const CT& x, CT& xh, CT& y, const CT& gam, const CT& bet) {
   const float mean = tok_sum(x) * (1.f / 64.f);
-  float q = 0.f;
+  const f32x4 m4 = {mean, mean, mean, mean};
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 4; ++i) xh.v[i] = x.v[i] - m4;
+  f32x4 q4 = xh.v[0] * xh.v[0];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float d = x.v[i][r] - mean;
-      xh.v[i][r] = d;
-      q += d * d;
-    }
-  const float rstd = rsqrtf(cross_row_sum(q) * (1.f / 64.f) + 1e-5f);
+  for (int i = 1; i < 4; ++i) q4 = xh.v[i] * xh.v[i] + q4;
+  const float rstd = rsqrtf(cross_row_sum((q4[0] + q4[1]) + (q4[2] + q4[3])) * (1.f / 64.f) + 1e-5f);
+  const f32x4 r4 = {rstd, rstd, rstd, rstd};
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      xh.v[i][r] *= rstd;
-      y.v[i][r] = xh.v[i][r] * gam.v[i][r] + bet.v[i][r];
-    }
+  for (int i = 0; i < 4; ++i) {
+    xh.v[i] *= r4;
+    y.v[i] = xh.v[i] * gam.v[i] + bet.v[i];
+  }
   return rstd;
 }
 #endif
@@ -318,27 +314,34 @@ __device__ __forceinline__ float ln_fwd_ct(const CT& x, CT& xh, CT& y, const CT&
 // every backward input is zero on them (the loss gradients, the saved activations and every LDS operand are
 // stored masked, and xh of a padded row is the finite LN of its bias), so they contribute exactly zero.
 // dx = rstd (gy - mean(gy) - xh mean(gy xh)) as two FMAs per element.
+// Packed fp32 pairs throughout (f32x4 vector ops -> v_pk_*), the two row sums as trees, and their cross-row
+// exchanges side by side (one swap chain for both).
 __device__ __forceinline__ void ln_bwd_ct(const CT& dy, const CT& xh, float rstd, const CT& gam, bool /*ok*/, CT& dx,
                                           CT& dg, CT& db) {
   CT gy;
-  float a = 0.f, b = 0.f;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 4; ++i) {
+    gy.v[i] = dy.v[i] * gam.v[i];
+    dg.v[i] = dy.v[i] * xh.v[i] + dg.v[i];
+    db.v[i] += dy.v[i];
+  }
+  const f32x4 a4 = (gy.v[0] + gy.v[1]) + (gy.v[2] + gy.v[3]);
+  f32x4 b4 = gy.v[0] * xh.v[0];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float d = dy.v[i][r];
-      gy.v[i][r] = d * gam.v[i][r];
-      a += gy.v[i][r];
-      b = fmaf(gy.v[i][r], xh.v[i][r], b);
-      dg.v[i][r] = fmaf(d, xh.v[i][r], dg.v[i][r]);
-      db.v[i][r] += d;
-    }
-  const float A = cross_row_sum(a) * (rstd * (1.f / 64.f));
-  const float B = cross_row_sum(b) * (rstd * (1.f / 64.f));
+  for (int i = 1; i < 4; ++i) b4 = gy.v[i] * xh.v[i] + b4;
+  float a = (a4[0] + a4[1]) + (a4[2] + a4[3]), b = (b4[0] + b4[1]) + (b4[2] + b4[3]);
+  float a0, a1, b0, b1;
+  swap16(a, a0, a1);
+  swap16(b, b0, b1);
+  a = a0 + a1;
+  b = b0 + b1;
+  swap32(a, a0, a1);
+  swap32(b, b0, b1);
+  const float sc = rstd * (1.f / 64.f);
+  const float A = (a0 + a1) * sc, B = (b0 + b1) * sc;
+  const f32x4 r4 = {rstd, rstd, rstd, rstd}, mA = {-A, -A, -A, -A}, mB = {-B, -B, -B, -B};
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) dx.v[i][r] = fmaf(-xh.v[i][r], B, fmaf(gy.v[i][r], rstd, -A));
+  for (int i = 0; i < 4; ++i) dx.v[i] = xh.v[i] * mB + (gy.v[i] * r4 + mA);
 }
 
 // per-lane feature partials (summed over the tokens the lane saw) -> one atomic per feature: reduce over the 16
@@ -646,15 +649,24 @@ __device__ __forceinline__ void st_lds_head(bf16_t* buf, int rt, int h, f32x4 a,
 __device__ __forceinline__ void attn_delta_ct(const CTr& ohi, const CTr& olo, const CTr& dOr, int rt, bool ok,
                                               const Ctx& c) {
   const CT oh = ct_unpack(ohi), ol = ct_unpack(olo), dO = ct_unpack(dOr);
+  float d[2];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    float d = 0.f;
+  for (int h = 0; h < 2; ++h) {   // packed pairs, a tree per head
+    const f32x4 t = (oh.v[2 * h] + ol.v[2 * h]) * dO.v[2 * h] + (oh.v[2 * h + 1] + ol.v[2 * h + 1]) * dO.v[2 * h + 1];
+    d[h] = (t[0] + t[1]) + (t[2] + t[3]);
+  }
+  float a0, a1, b0, b1;   // both heads' cross-row sums side by side
+  swap16(d[0], a0, a1);
+  swap16(d[1], b0, b1);
+  d[0] = a0 + a1;
+  d[1] = b0 + b1;
+  swap32(d[0], a0, a1);
+  swap32(d[1], b0, b1);
+  d[0] = a0 + a1;
+  d[1] = b0 + b1;
+  if ((c.lane >> 4) == 0) {
 #pragma unroll
-    for (int mt = 2 * h; mt < 2 * h + 2; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) d += (oh.v[mt][r] + ol.v[mt][r]) * dO.v[mt][r];
-    d = cross_row_sum(d);
-    if ((c.lane >> 4) == 0) c.DEL[h * c.NRP + rt * 16 + (c.lane & 15)] = ok ? d : 0.f;
+    for (int h = 0; h < 2; ++h) c.DEL[h * c.NRP + rt * 16 + (c.lane & 15)] = ok ? d[h] : 0.f;
   }
 }
 
@@ -885,9 +897,7 @@ __device__ __forceinline__ void mlp_bwd_ct(const Mat& m1, const Mat& m2, const L
         ct_zero(dg);
         mm(dg, W2b, ld_lds(c.DA, rt, lane));
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) dg.v[i][r] = ok ? dg.v[i][r] * gp.v[i][r] : 0.f;
+        for (int i = 0; i < 4; ++i) dg.v[i] *= gp.v[i];   // padded rows: GELU' reads as zero, ds is finite
         st_lds(c.KB, rt, ct_pack(dg), ok, lane);
       }
     }
