@@ -66,47 +66,72 @@ __global__ __launch_bounds__(256) void obs_embed_pack_kernel(OEArgs a) {
   }
 }
 
-// forward: one 16-token tile per workgroup, the k-steps dealt round robin to the 4 waves (token on lane & 15,
+// forward: one 16-token tile per workgroup, the k-steps dealt round robin to its OE_WAVES waves (token on lane & 15,
 // features 16mt + 4g + r in registers), partial sums reduced through LDS in fixed wave order.  Round 2 gave each
 // wave its own 16 tokens and all 41 k-steps of SMAC's 1288-wide rows: the rollout's 864 tokens were 14 workgroups
-// of a 41-step dependent load chain (40 us per call).
-__global__ __launch_bounds__(256) void obs_embed_fwd_kernel(OEArgs a) {
-  __shared__ f32x4 part[3][4][64];
-  __shared__ float pst[3][2][64];
+// of a 41-step dependent load chain (40 us per call); round 3: 4 waves, one step's loads at a time (25 us).  Round 4:
+// 8 waves, and each wave requests the x rows and weight fragments of OE_PF steps before converting / multiplying
+// any of them (one load latency per OE_PF steps).
+constexpr int OE_WAVES = 8, OE_PF = 3;
+struct OEStep { float4 x0, x1; bf16x8 w[4]; };
+__device__ __forceinline__ void oe_mma(const OEArgs& a, const float (&v)[8], const bf16x8 (&w)[4], bool ok,
+                                       f32x4 (&acc)[4], float& sx, float& sxx) {
+  bf16x8 hi, lo;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float xv = ok ? v[j] : 0.f;
+    sx += xv;
+    sxx += xv * xv;
+    const uint16_t h = f2bf(xv);
+    hi[j] = (short)h;
+    lo[j] = (short)f2bf(xv - bf2f(h));
+  }
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[mt], hi, acc[mt], 0, 0, 0);
+    acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[mt], lo, acc[mt], 0, 0, 0);
+  }
+}
+__global__ __launch_bounds__(64 * OE_WAVES) void obs_embed_fwd_kernel(OEArgs a) {
+  __shared__ f32x4 part[OE_WAVES - 1][4][64];
+  __shared__ float pst[OE_WAVES - 1][2][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
   const int tok = blockIdx.x * OE_TOK + c;
   const bool ok = tok < a.N;
   const float* xr = a.x + (size_t)(ok ? tok : 0) * a.od;
   f32x4 acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   float sx = 0.f, sxx = 0.f;
-  const bool vec4 = (a.od & 3) == 0;
-  for (int s = wave; s < a.KS; s += 4) {
+  int s = wave;
+  if ((a.od & 3) == 0) {   // float4 rows: the steps whose 32 dims are all inside the row, OE_PF at a time
+    const int nfull = a.od >> 5;
+    for (; s + OE_WAVES * (OE_PF - 1) < nfull; s += OE_WAVES * OE_PF) {
+      OEStep st[OE_PF];
+#pragma unroll
+      for (int u = 0; u < OE_PF; ++u) {
+        const int k0 = 32 * (s + OE_WAVES * u) + 8 * g;
+        st[u].x0 = *(const float4*)(xr + k0);
+        st[u].x1 = *(const float4*)(xr + k0 + 4);
+        const bf16_t* wp = a.wpack + ((size_t)(s + OE_WAVES * u) * 4 * 64 + lane) * 8;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) st[u].w[mt] = *(const bf16x8*)(wp + (size_t)mt * 64 * 8);
+      }
+#pragma unroll
+      for (int u = 0; u < OE_PF; ++u) {
+        const float v[8] = {st[u].x0.x, st[u].x0.y, st[u].x0.z, st[u].x0.w, st[u].x1.x, st[u].x1.y, st[u].x1.z, st[u].x1.w};
+        oe_mma(a, v, st[u].w, ok, acc, sx, sxx);
+      }
+    }
+  }
+  for (; s < a.KS; s += OE_WAVES) {   // the rest (and rows that are not float4-aligned), one step at a time
     const int k0 = 32 * s + 8 * g;
     float v[8];
-    if (vec4 && k0 + 8 <= a.od) {
-      const float4 p = *(const float4*)(xr + k0), q = *(const float4*)(xr + k0 + 4);
-      v[0] = p.x; v[1] = p.y; v[2] = p.z; v[3] = p.w; v[4] = q.x; v[5] = q.y; v[6] = q.z; v[7] = q.w;
-    } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = k0 + j < a.od ? xr[k0 + j] : 0.f;
-    }
-    bf16x8 hi, lo;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float xv = ok ? v[j] : 0.f;
-      sx += xv;
-      sxx += xv * xv;
-      const uint16_t h = f2bf(xv);
-      hi[j] = (short)h;
-      lo[j] = (short)f2bf(xv - bf2f(h));
-    }
+    for (int j = 0; j < 8; ++j) v[j] = k0 + j < a.od ? xr[k0 + j] : 0.f;
+    bf16x8 w[4];
     const bf16_t* wp = a.wpack + ((size_t)s * 4 * 64 + lane) * 8;
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const bf16x8 w = *(const bf16x8*)(wp + (size_t)mt * 64 * 8);
-      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, hi, acc[mt], 0, 0, 0);
-      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, lo, acc[mt], 0, 0, 0);
-    }
+    for (int mt = 0; mt < 4; ++mt) w[mt] = *(const bf16x8*)(wp + (size_t)mt * 64 * 8);
+    oe_mma(a, v, w, ok, acc, sx, sxx);
   }
   if (wave > 0) {
 #pragma unroll
@@ -117,7 +142,7 @@ __global__ __launch_bounds__(256) void obs_embed_fwd_kernel(OEArgs a) {
   __syncthreads();
   if (wave > 0) return;
 #pragma unroll
-  for (int w = 0; w < 3; ++w) {
+  for (int w = 0; w < OE_WAVES - 1; ++w) {
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) acc[mt] += part[w][mt][lane];
     sx += pst[w][0][lane];
@@ -270,7 +295,7 @@ MDL_API int mdl_obs_embed_pack(const OEArgs* a, hipStream_t st) {
 
 MDL_API int mdl_obs_embed_fwd(const OEArgs* a, hipStream_t st) {
   if (a->N <= 0) return 0;
-  hipLaunchKernelGGL(obs_embed_fwd_kernel, dim3((a->N + OE_TOK - 1) / OE_TOK), dim3(256), 0, st, *a);
+  hipLaunchKernelGGL(obs_embed_fwd_kernel, dim3((a->N + OE_TOK - 1) / OE_TOK), dim3(64 * OE_WAVES), 0, st, *a);
   MDL_CHECK_LAUNCH();
   return 0;
 }

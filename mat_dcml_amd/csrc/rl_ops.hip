@@ -513,8 +513,10 @@ MDL_API int mdl_smac_insert(const SmacInsArgs* a, hipStream_t s) {
     if (a->seg[k].n < 0 || (a->seg[k].n > 0 && (!a->seg[k].src || !a->seg[k].dst))) return -2;
     most = a->seg[k].n > most ? a->seg[k].n : most;
   }
+  // one float4 per thread of the largest segment (SMAC's obs / state slots: ~1,100 workgroups): the copy is bound
+  // by bytes in flight, and a 256-workgroup cap left each thread a dependent 4-iteration loop (13.9 us per step)
   int gx = (most / 4 + 255) / 256;
-  gx = gx < 1 ? 1 : (gx > 256 ? 256 : gx);
+  gx = gx < 1 ? 1 : (gx > 2048 ? 2048 : gx);
   hipLaunchKernelGGL(smac_insert_kernel, dim3(gx + 1), dim3(256), 0, s, *a);
   MDL_CHECK_LAUNCH();
   return 0;

@@ -372,7 +372,8 @@ def test_mat_dec_runner_trains_through_the_hybrid_path(gpu):
 
 def test_training_kernels_time_bound(gpu):
     """The four fused training kernels at the bench minibatch (3,200 sequences x 33 agents, n_block 2): hipEvent time
-    per minibatch (printed) under a regression bound of ~1.4x the round-4 measurement (1.17 ms)."""
+    per minibatch (printed; launch gaps included: ~1.54 ms measured this way, 1.17 ms of kernel time under rocprofv3)
+    under a regression bound of ~1.2x."""
     B, L = 3200, 33
     m = make(L, gpu, seed=0, scale=0.05)
     obs = torch.rand(B, L, 7, device=gpu)
@@ -388,10 +389,11 @@ def test_training_kernels_time_bound(gpu):
         drep = dec.backward(torch.ones_like(lp), torch.ones_like(ent))
         enc.backward(drep, torch.ones_like(v))
 
-    step()
+    for _ in range(30):   # ~50 ms of back-to-back work first: after a suite of small launches the clocks ramp
+        step()
     torch.cuda.synchronize()
     ts = []
-    for _ in range(10):
+    for _ in range(20):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
         step()
@@ -400,4 +402,4 @@ def test_training_kernels_time_bound(gpu):
         ts.append(a.elapsed_time(b))
     ms = sorted(ts)[len(ts) // 2]
     print(f"four training kernels, 3200 x 33: {ms:.3f} ms per minibatch")
-    assert ms < 1.65, ms
+    assert ms < 1.85, ms
