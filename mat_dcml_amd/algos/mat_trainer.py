@@ -289,9 +289,12 @@ class MATTrainer:
                 if native and len(idx_list) == 1:
                     # one minibatch = the whole batch: the permutation only reorders the rows the loss averages
                     # over, so the buffer's rows are used in place (SMAC: no 2 x 445 MB gather copy per epoch);
-                    # only the advantages are standardised
+                    # only the advantages are standardised (one gather launch over the identity rows)
+                    n = adv_f.shape[0]
+                    if getattr(self, "_ident", None) is None or self._ident.numel() != n:
+                        self._ident = torch.arange(n, device=adv_f.device, dtype=torch.int64)
                     mb = dict(src)
-                    mb["adv"] = rl_ops.normalize_from_sums(adv_f, sums)
+                    mb["adv"] = kernels.gather_rows({"adv": adv_f}, self._ident, sums, ("adv",))["adv"]
                 elif native:
                     mb = kernels.gather_rows(src, idx, sums, ("adv",))
                 else:

@@ -70,9 +70,9 @@ __global__ __launch_bounds__(256) void obs_embed_pack_kernel(OEArgs a) {
 // features 16mt + 4g + r in registers), partial sums reduced through LDS in fixed wave order.  Round 2 gave each
 // wave its own 16 tokens and all 41 k-steps of SMAC's 1288-wide rows: the rollout's 864 tokens were 14 workgroups
 // of a 41-step dependent load chain (40 us per call); round 3: 4 waves, one step's loads at a time (25 us).  Round 4:
-// 8 waves, and each wave requests the x rows and weight fragments of OE_PF steps before converting / multiplying
-// any of them (one load latency per OE_PF steps).
-constexpr int OE_WAVES = 8, OE_PF = 3;
+// each wave requests the x rows and weight fragments of OE_PF steps before converting / multiplying any of them (one
+// load latency per OE_PF steps; 8 waves x 3 steps measured slower, 30.6 us: most of its steps fell to the tail).
+constexpr int OE_WAVES = 4, OE_PF = 5;
 struct OEStep { float4 x0, x1; bf16x8 w[4]; };
 __device__ __forceinline__ void oe_mma(const OEArgs& a, const float (&v)[8], const bf16x8 (&w)[4], bool ok,
                                        f32x4 (&acc)[4], float& sx, float& sxx) {
@@ -115,6 +115,7 @@ __global__ __launch_bounds__(64 * OE_WAVES) void obs_embed_fwd_kernel(OEArgs a) 
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) st[u].w[mt] = *(const bf16x8*)(wp + (size_t)mt * 64 * 8);
       }
+      __builtin_amdgcn_sched_barrier(0);   // every load above issues before the first conversion / MFMA
 #pragma unroll
       for (int u = 0; u < OE_PF; ++u) {
         const float v[8] = {st[u].x0.x, st[u].x0.y, st[u].x0.z, st[u].x0.w, st[u].x1.x, st[u].x1.y, st[u].x1.z, st[u].x1.w};
@@ -125,8 +126,13 @@ __global__ __launch_bounds__(64 * OE_WAVES) void obs_embed_fwd_kernel(OEArgs a) 
   for (; s < a.KS; s += OE_WAVES) {   // the rest (and rows that are not float4-aligned), one step at a time
     const int k0 = 32 * s + 8 * g;
     float v[8];
+    if ((a.od & 3) == 0 && k0 + 8 <= a.od) {
+      const float4 p = *(const float4*)(xr + k0), q = *(const float4*)(xr + k0 + 4);
+      v[0] = p.x; v[1] = p.y; v[2] = p.z; v[3] = p.w; v[4] = q.x; v[5] = q.y; v[6] = q.z; v[7] = q.w;
+    } else {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = k0 + j < a.od ? xr[k0 + j] : 0.f;
+      for (int j = 0; j < 8; ++j) v[j] = k0 + j < a.od ? xr[k0 + j] : 0.f;
+    }
     bf16x8 w[4];
     const bf16_t* wp = a.wpack + ((size_t)s * 4 * 64 + lane) * 8;
 #pragma unroll
