@@ -357,11 +357,13 @@ __device__ __forceinline__ float rdlane(float x, int l) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
 }
 
-template <int NB, int NREG, bool WIDE>
+// MA = logit tiles of the head: 1 (A <= 4: the logits sit in registers r < A of lanes g = 0), 3 (A <= 48: SMAC's
+// 36 actions — a 4th tile was 6 dead MFMAs and 24 registers of folded weights per agent step), 4 (A <= 64)
+template <int NB, int NREG, int MA>
 __global__ __launch_bounds__(64, 1) void mat_decode_wave_kernel(DecParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NM = wv_nm(NB), NLDS = NM - NREG;
-  constexpr int MA = WIDE ? 4 : 1;   // logit tiles (A <= 4: one tile, the logits sit in lanes g = 0)
+  constexpr bool WIDE = MA > 1;
   const int lane = threadIdx.x, g = lane >> 4, c = lane & 15;
   const int env = blockIdx.x, L = p.L, A = p.act_dim;
   const WvLds lo = wv_lds(NB, L, p.n_tok, NLDS, WIDE);
@@ -587,15 +589,19 @@ __global__ __launch_bounds__(64, 1) void mat_decode_wave_kernel(DecParams p) {
   }
 }
 
-template <int NB, int NREG>
-int wv_launch(const DecParams* p, bool wide, size_t lds, hipStream_t st) {
-  const void* f = wide ? (const void*)mat_decode_wave_kernel<NB, NREG, true> : (const void*)mat_decode_wave_kernel<NB, NREG, false>;
-  hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+template <int NB, int NREG, int MA>
+int wv_launch_ma(const DecParams* p, size_t lds, hipStream_t st) {
+  hipError_t e = hipFuncSetAttribute((const void*)mat_decode_wave_kernel<NB, NREG, MA>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return -(int)e;
-  if (wide) hipLaunchKernelGGL((mat_decode_wave_kernel<NB, NREG, true>), dim3(p->B), dim3(64), lds, st, *p);
-  else hipLaunchKernelGGL((mat_decode_wave_kernel<NB, NREG, false>), dim3(p->B), dim3(64), lds, st, *p);
+  hipLaunchKernelGGL((mat_decode_wave_kernel<NB, NREG, MA>), dim3(p->B), dim3(64), lds, st, *p);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : -(int)e;
+}
+template <int NB, int NREG>
+int wv_launch(const DecParams* p, bool wide, size_t lds, hipStream_t st) {
+  if (!wide) return wv_launch_ma<NB, NREG, 1>(p, lds, st);
+  return p->act_dim <= 48 ? wv_launch_ma<NB, NREG, 3>(p, lds, st) : wv_launch_ma<NB, NREG, 4>(p, lds, st);
 }
 
 }  // namespace

@@ -258,6 +258,9 @@ __global__ __launch_bounds__(256) void obs_embed_bwd_m_kernel(OEArgs a) {
 __global__ __launch_bounds__(256) void obs_embed_bwd_u_kernel(OEArgs a) {
   const int f = threadIdx.x & 63, tl = threadIdx.x >> 6;
   float u = 0.f, d = 0.f;
+  // unrolled: 8 tokens' loads in flight per thread (the rolled loop was one dependent load latency per token:
+  // 33 us for SMAC's 86,400-token minibatch)
+#pragma unroll 8
   for (int t = blockIdx.x * 4 + tl; t < a.N; t += gridDim.x * 4) {
     const float dp = a.dpre[(size_t)t * 64 + f];
     u += dp * a.stat[2 * (size_t)t + 1] * a.stat[2 * (size_t)t];
@@ -280,6 +283,7 @@ __global__ __launch_bounds__(256) void obs_embed_bwd_fin_kernel(OEArgs a) {
   if (k >= a.od) return;
   const float gk = a.g[k], bk = a.b[k];
   float dg = 0.f, dbo = 0.f;
+#pragma unroll 16   // 16 features' loads in flight (rolled: 64 dependent load latencies, 38 us)
   for (int f = 0; f < 64; ++f) {
     const float m = a.M[(size_t)f * a.od + k] - a.ud[f], db = a.ud[64 + f], w = a.we[(size_t)f * a.od + k];
     if (a.d_we) atomicAdd(a.d_we + (size_t)f * a.od + k, gk * m + bk * db);

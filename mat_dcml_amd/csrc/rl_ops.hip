@@ -477,8 +477,10 @@ __global__ __launch_bounds__(256) void smac_insert_kernel(SmacInsArgs a) {
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   for (int e = tid; e < a.E; e += 256) {
     const float r = a.reward[e];
-    bool d = true;
-    for (int ag = 0; ag < a.A; ++ag) d = d && a.dones[(size_t)e * a.A + ag] != 0;
+    int nd = 0;   // every agent's flag loaded (a short-circuit && chain was one dependent byte load per agent)
+#pragma unroll 8
+    for (int ag = 0; ag < a.A; ++ag) nd += a.dones[(size_t)e * a.A + ag] != 0;
+    const bool d = nd == a.A;
     for (int ag = 0; ag < a.A; ++ag) {
       const size_t o = (size_t)e * a.A + ag;
       a.d_rew[o] = r;
