@@ -403,3 +403,28 @@ def test_training_kernels_time_bound(gpu):
     ms = sorted(ts)[len(ts) // 2]
     print(f"four training kernels, 3200 x 33: {ms:.3f} ms per minibatch")
     assert ms < 1.85, ms
+
+
+@pytest.mark.parametrize("N", [864, 70_000])
+def test_obs_embed_forward_matches_torch(gpu, N):
+    """Wide-observation embedding forward (csrc/obs_embed.hip) at the rollout size (one 16-token tile per workgroup)
+    and at a training-minibatch size (four tiles per workgroup sharing the weight fragments): pre = W_e LN_obs(x) + b_e
+    against the fp32 torch modules, and the saved (mu, rstd)."""
+    torch.manual_seed(0)
+    od = 1288
+    m = MultiAgentTransformer(od, od, 36, 27, 2, 64, 2).to(gpu)
+    with torch.no_grad():
+        ln, lin = m.encoder.obs_encoder[0], m.encoder.obs_encoder[1]
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.2, 0.2)
+    oe = mat_train.ObsEmbed(m)
+    x = torch.randn(N, od, device=gpu) * 2.0 + 0.3
+    pre, stat = oe.forward(x)
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        ref = lin(ln(x))
+        mu, var = x.mean(-1), x.var(-1, unbiased=False)
+    err = (pre - ref).abs().max().item()
+    assert err < 1e-2 * ref.abs().max().item(), err   # W_e diag(g) enters the MFMA as bf16
+    assert torch.allclose(stat[:, 0], mu, atol=1e-4, rtol=1e-4)
+    assert torch.allclose(stat[:, 1], torch.rsqrt(var + 1e-5), atol=1e-4, rtol=1e-3)
