@@ -26,6 +26,9 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=
 # its time 676 -> 635 us per minibatch, but slow the decode kernel (323 -> 333 us), so only that unit uses them.
 PER_FILE_FLAGS = {
     "mat_dec_ct_bwd.hip": ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"],
+    # ... and the encoder forward (its saved-activation stores spilled 88 -> 63 instructions: 191 -> 178 us per
+    # training minibatch, scripts/r4_ab7.sh); the decoder forward measured neutral with them
+    "mat_enc_ct.hip": ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"],
     # the SMAC env must round every product / sum like the torch path: hip's __fmul_rn / __fadd_rn are plain
     # operators that -ffp-contract=fast still fuses into FMAs (battle positions drifted by an ulp)
     "smac_env.hip": ["-ffp-contract=off"],
