@@ -698,7 +698,7 @@ __device__ __forceinline__ void dec_fwd_tile(const DecP& p, char* smem, int seq0
 }
 
 #ifndef MDL_CT_BWD_TU
-// MA = logit tiles of the action head: 1 (A <= 16: DCML, MPE) or 4 (A <= 64: SMAC's 36 actions)
+// MA = logit tiles of the action head: 1 (A <= 16: DCML, MPE), 3 (A <= 48: SMAC's 36 actions) or 4 (A <= 64)
 template <int NB, bool SAVE, int MA, bool CONT>
 __global__ __launch_bounds__(NTHR, FWD_WGPC) void mat_dec_fwd_ct(DecP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -862,12 +862,14 @@ static int dec_fwd_ct(const DecP* p, int NB, int save, hipStream_t st) {
   if (NB == 3) return save ? launch_ct(mat_dec_fwd_ct<3, true, MA, CONT>, p, true, st) : launch_ct(mat_dec_fwd_ct<3, false, MA, CONT>, p, true, st);
   return -3;
 }
-// MA = logit tiles of the action head (1: A <= 16, 4: A <= 64); the continuous action type is its own instantiation
-// (its Normal-head / Linear-embedding code kept out of the discrete kernels' instruction stream)
+// MA = logit tiles of the action head (1: A <= 16, 3: A <= 48 — SMAC's 36 actions, 4: A <= 64); the continuous
+// action type is its own instantiation (its Normal-head / Linear-embedding code kept out of the discrete kernels'
+// instruction stream)
 MDL_API int mdl_mat_dec_fwd_ct(const DecP* p, int NB, int save, hipStream_t st) {
   if (p->A > 64 || p->A < 1) return -1;
   if (p->cont) return p->A <= 16 ? dec_fwd_ct<1, true>(p, NB, save, st) : dec_fwd_ct<4, true>(p, NB, save, st);
-  return p->A <= 16 ? dec_fwd_ct<1, false>(p, NB, save, st) : dec_fwd_ct<4, false>(p, NB, save, st);
+  if (p->A <= 16) return dec_fwd_ct<1, false>(p, NB, save, st);
+  return p->A <= 48 ? dec_fwd_ct<3, false>(p, NB, save, st) : dec_fwd_ct<4, false>(p, NB, save, st);
 }
 #else
 template <int MA, bool CONT>
@@ -881,7 +883,8 @@ static int dec_bwd_ct(const DecP* p, int NB, hipStream_t st) {
 MDL_API int mdl_mat_dec_bwd_ct(const DecP* p, int NB, hipStream_t st) {
   if (p->A > 64 || p->A < 1 || 2 * p->NRP * 128 < (p->A + 1) * 256) return -1;
   if (p->cont) return p->A <= 16 ? dec_bwd_ct<1, true>(p, NB, st) : dec_bwd_ct<4, true>(p, NB, st);
-  return p->A <= 16 ? dec_bwd_ct<1, false>(p, NB, st) : dec_bwd_ct<4, false>(p, NB, st);
+  if (p->A <= 16) return dec_bwd_ct<1, false>(p, NB, st);
+  return p->A <= 48 ? dec_bwd_ct<3, false>(p, NB, st) : dec_bwd_ct<4, false>(p, NB, st);
 }
 #endif  // MDL_CT_BWD_TU
 

@@ -136,7 +136,7 @@ def make_discrete(L, A, od, dev, seed=0, scale=0.2):
     return m
 
 
-@pytest.mark.parametrize("L,B,A,od", [(27, 24, 36, 1288), (10, 30, 12, 40)])
+@pytest.mark.parametrize("L,B,A,od", [(27, 24, 36, 1288), (10, 30, 12, 40), (9, 20, 60, 40)])
 def test_full_mat_fused_grads_wide_obs_discrete(gpu, L, B, A, od):
     """SMAC shape (27m_vs_30m: 27 agents, obs 1288 through the obs-embedding kernels, Discrete(36) heads on the MFMA
     head path) — every parameter gradient vs fp32 autograd with the bf16-autocast yardstick."""
