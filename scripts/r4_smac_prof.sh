@@ -4,7 +4,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/smacprof -o run -- python3 bench.py --config smac --steps 3 --warmup 1 --no_eval > gpurun_out/smacprof.log 2>&1 || { tail -20 gpurun_out/smacprof.log; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/smacprof -o run -- python3 bench.py --config smac --steps 3 --warmup 1 --no_eval > gpurun_out/smacprof.log 2>&1 || { tail -20 gpurun_out/smacprof.log; exit 1; }
 tail -1 gpurun_out/smacprof.log | cut -c1-200
 f=$(find gpurun_out/smacprof -name "*kernel_stats.csv" | head -1)
 cp $f gpurun_out/smac_kernel_stats.csv
