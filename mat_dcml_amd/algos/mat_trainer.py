@@ -286,7 +286,7 @@ class MATTrainer:
             for m, idx in enumerate(idx_list):
                 src = {"obs": obs_f, "actions": act_f, "ava": ava_f, "old_logp": lp_f, "value_preds": vp_f,
                        "returns": ret_f, "active": am_f, "adv": adv_f}
-                if native and len(idx_list) == 1:
+                if native and len(idx_list) == 1 and getattr(self, "inplace_single_minibatch", True):
                     # one minibatch = the whole batch: the permutation only reorders the rows the loss averages
                     # over, so the buffer's rows are used in place (SMAC: no 2 x 445 MB gather copy per epoch);
                     # only the advantages are standardised (one gather launch over the identity rows)

@@ -428,3 +428,34 @@ def test_obs_embed_forward_matches_torch(gpu, N):
     assert err < 1e-2 * ref.abs().max().item(), err   # W_e diag(g) enters the MFMA as bf16
     assert torch.allclose(stat[:, 0], mu, atol=1e-4, rtol=1e-4)
     assert torch.allclose(stat[:, 1], torch.rsqrt(var + 1e-5), atol=1e-4, rtol=1e-3)
+
+
+def test_single_minibatch_epoch_in_place_matches_gather(gpu):
+    """A one-minibatch PPO epoch trains on the buffer's rows in place (no permuted gather copy): two identically
+    seeded runners, one forced through the gather, report the same losses up to fp32 summation order, and their
+    parameters stay within the Adam step bound (an update is ~lr per step whatever the gradient's size, so a
+    near-zero gradient whose sign the summation order flips moves a weight by up to 2 lr per step)."""
+    from mat_dcml_amd.config import get_config, parse_args
+    from mat_dcml_amd.runner.dcml_runner import DCMLRunner
+
+    def run(inplace):
+        torch.manual_seed(3)
+        args = parse_args(["--env_name", "DCML", "--algorithm_name", "mat", "--n_workers", "8", "--n_rollout_threads",
+                           "16", "--episode_length", "8", "--ppo_epoch", "2", "--num_mini_batch", "1", "--use_valuenorm",
+                           "--lr", "5e-4"], get_config(), warn=False)
+        r = DCMLRunner({"all_args": args, "device": gpu, "run_dir": None})
+        assert r.policy._fused()
+        r.trainer.inplace_single_minibatch = inplace
+        r.warmup()
+        infos = r.train_iteration()
+        torch.cuda.synchronize()
+        return ({k: float(v) for k, v in infos.items() if k in ("value_loss", "policy_loss", "dist_entropy")},
+                [p.detach().clone() for p in r.policy.transformer.parameters()])
+
+    (ia, pa), (ib, pb) = run(True), run(False)
+    assert ia.keys() == ib.keys() and ia, ia
+    for k in ia:
+        assert abs(ia[k] - ib[k]) <= 1e-3 * max(1.0, abs(ib[k])), (k, ia[k], ib[k])
+    for x, y in zip(pa, pb):
+        assert torch.isfinite(x).all()
+        assert (x - y).abs().max().item() < 2 * 2 * 5e-4 * 1.5
