@@ -47,7 +47,8 @@ def _flags(src):
     extra = os.environ.get("MAT_DCML_BWD_FLAGS", "").split() if src.endswith("_bwd.hip") else []
     if os.path.basename(src) in FWD_TUS:
         extra = os.environ.get("MAT_DCML_FWD_FLAGS", "").split()
-    return FLAGS + PER_FILE_FLAGS.get(os.path.basename(src), []) + extra
+    per_file = [] if os.environ.get("MAT_DCML_NO_PER_FILE_FLAGS") else PER_FILE_FLAGS.get(os.path.basename(src), [])
+    return FLAGS + per_file + extra
 
 
 def _sources():
