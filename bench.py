@@ -43,7 +43,8 @@ def parse():
     p.add_argument("--dtype", default="bf16")
     p.add_argument("--phases", action="store_true", help="also print the phase summary to stderr")
     p.add_argument("--no_phase_timers", action="store_true",
-                   help="no hipEvent phase breakdown in the JSON (phase_ms_per_step); for the timer-overhead A/B")
+                   help="skip the phase breakdown (extra instrumented steps after the timed loop; the timed loop "
+                        "itself never records phase events)")
     p.add_argument("--allreduce", default="rccl", choices=["rccl", "oneshot", "auto"],
                    help="data-parallel gradient all-reduce: RCCL (default), the one-shot peer-memory kernel, or auto "
                         "(one-shot only if it matches RCCL and is faster at start-up)")
@@ -129,13 +130,7 @@ def main():
     for _ in range(a.warmup):
         runner.train_iteration()
     paths = kernel_report(runner)   # after the warm-up: the decode entry names the kernel its calls ran on
-    # phase breakdown of the timed steps: hipEvent pairs recorded in the stream (no sync inside the loop), resolved
-    # once after the timed region (utils/timers.PhaseTimers)
-    runner.timers.enabled = not a.no_phase_timers
-    # sampled phases (every 10th rollout step, every 4th minibatch): a recorded hipEvent pair costs a few us of
-    # stream bubble, and 540 pairs per iteration slowed the timed loop by 2 %; the totals are scaled back up
-    runner.timers.every.update(decode=10, env=10, insert=10, train_fwd=4, train_bwd=4)
-    runner.timers.summary(reset=True)
+    runner.timers.enabled = False    # the headline loop runs uninstrumented
     sync()
     comm.barrier()
     sync()
@@ -160,14 +155,7 @@ def main():
                                  for k in ("grad_allreduce", "stats_allreduce")},
             "collectives_per_step": {k: max(r[1].get(k + "_calls", 0) for r in per_rank) // max(a.steps, 1)
                                      for k in ("grad_allreduce", "stats_allreduce")}}
-    phases = None
-    if runner.timers.enabled:
-        tot = runner.timers.totals_ms()
-        n_mb = a.steps * a.ppo_epoch * a.num_mini_batch
-        phases = {"phase_ms_per_step": {k: round(v / a.steps, 3) for k, v in tot.items()},
-                  "train_kernels_ms_per_minibatch": {k[6:]: round(tot[k] / n_mb, 4) for k in ("train_fwd", "train_bwd")
-                                                     if k in tot}}
-        runner.timers.summary(reset=True)
+    phases = None if a.no_phase_timers else phase_breakdown(a, runner, comm, sync)
     env_steps = a.steps * a.episode_length * a.envs * n
     value = env_steps / dt
     eval_info = None
@@ -203,6 +191,35 @@ def main():
             "eval": eval_info,
         }), flush=True)
     comm.destroy()
+
+
+def phase_breakdown(a, runner, comm, sync):
+    """Where a step's time goes: ``a.steps`` MORE iterations after the timed loop with a hipEvent pair around EVERY
+    phase occurrence (pack / decode / env / insert per rollout step, update; train_fwd / train_bwd per minibatch).
+    Nothing is sampled or scaled, so the phases partition the instrumented step up to the GPU idle between them;
+    the headline loop above runs without any events (each pair costs a few us of stream bubble)."""
+    runner.timers.enabled = True
+    runner.timers.every.clear()
+    runner.timers.summary(reset=True)
+    sync()
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        runner.train_iteration()
+    sync()
+    dt = time.perf_counter() - t0
+    tot = runner.timers.totals_ms()
+    runner.timers.summary(reset=True)
+    runner.timers.enabled = False
+    n_mb = a.steps * a.ppo_epoch * a.num_mini_batch
+    ph = {k: round(v / a.steps, 3) for k, v in tot.items()}
+    top = sum(ph.get(k, 0.0) for k in ("pack", "decode", "env", "insert", "update"))
+    return {"phase_ms_per_step": ph,
+            "phase_run": {"ms_per_step": round(dt / a.steps * 1e3, 3), "phases_sum_ms": round(top, 3),
+                          "note": "phases = pack + decode + env + insert + update of separate instrumented steps "
+                                  "(every occurrence timed); train_fwd / train_bwd lie inside update"},
+            "train_kernels_ms_per_minibatch": {k[6:]: round(tot[k] / n_mb, 4) for k in ("train_fwd", "train_bwd")
+                                               if k in tot}}
 
 
 def _native_build():

@@ -102,20 +102,38 @@ def flags_hash(srcs=None):
     return h.hexdigest()[:16]
 
 
+def _tmp(path):
+    """Per-process temporary name next to ``path`` (several ranks may build at once: os.replace of a shared
+    ``.tmp`` name could move another process's half-written file into place)."""
+    return f"{path}.{os.getpid()}.tmp"
+
+
+def sidecar(out=None):
+    """(source hash, flags hash) recorded next to a built library, or None."""
+    try:
+        with open((out or OUT) + ".buildinfo") as f:
+            sh, fh = f.read().split()
+        return sh, fh
+    except (OSError, ValueError):
+        return None
+
+
 def _buildinfo(srcs):
     """A one-symbol-pair translation unit carrying the build identity (source hash, flags hash)."""
     sh, fh = source_hash(), flags_hash(srcs)
     os.makedirs(os.path.join(OUT_DIR, "obj"), exist_ok=True)
     obj = os.path.join(OUT_DIR, "obj", f"buildinfo_{sh}_{fh}.o")
     if not os.path.exists(obj):
-        cpp = obj[:-2] + ".cpp"
+        cpp = f"{obj[:-2]}.{os.getpid()}.cpp"
         with open(cpp, "w") as f:
             f.write(f'extern "C" __attribute__((visibility("default"))) const char mdl_build_source_hash[] = "{sh}";\n'
                     f'extern "C" __attribute__((visibility("default"))) const char mdl_build_flags_hash[] = "{fh}";\n')
-        r = subprocess.run([HIPCC, "-O2", "-fPIC", "-c", cpp, "-o", obj + ".tmp"], capture_output=True, text=True)
+        tmp = _tmp(obj)
+        r = subprocess.run([HIPCC, "-O2", "-fPIC", "-c", cpp, "-o", tmp], capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {cpp}:\n{r.stderr}")
-        os.replace(obj + ".tmp", obj)
+        os.replace(tmp, obj)
+        os.remove(cpp)
     return obj
 
 
@@ -123,11 +141,12 @@ def _compile(src):
     os.makedirs(os.path.join(OUT_DIR, "obj"), exist_ok=True)
     obj = os.path.join(OUT_DIR, "obj", os.path.basename(src) + "." + _hash(src) + ".o")
     if not os.path.exists(obj):
-        cmd = [HIPCC, *_flags(src), "-c", src, "-o", obj + ".tmp"]
+        tmp = _tmp(obj)
+        cmd = [HIPCC, *_flags(src), "-c", src, "-o", tmp]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
-        os.replace(obj + ".tmp", obj)
+        os.replace(tmp, obj)
     return obj
 
 
@@ -137,11 +156,18 @@ def build(verbose=True, jobs=None):
     with cf.ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(_compile, srcs))
     objs.append(_buildinfo(srcs))
-    cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", OUT + ".tmp"]
+    tmp = _tmp(OUT)
+    cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr}")
-    os.replace(OUT + ".tmp", OUT)
+    os.replace(tmp, OUT)
+    # sidecar identity: lets ops/kernels.lib() decide "stale -> rebuild" BEFORE the library is ever dlopen'ed (a
+    # dlclose + dlopen of one path can hand back the old image); the embedded symbols stay the authoritative check
+    side = _tmp(OUT + ".buildinfo")
+    with open(side, "w") as f:
+        f.write(f"{source_hash()} {flags_hash(srcs)}\n")
+    os.replace(side, OUT + ".buildinfo")
     if verbose:
         print(f"[build] {OUT} <- {', '.join(os.path.basename(s) for s in srcs)}")
     return OUT

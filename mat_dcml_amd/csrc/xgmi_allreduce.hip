@@ -75,7 +75,9 @@ __global__ __launch_bounds__(AR_THREADS) void oneshot_allreduce_kernel(ArArgs a)
     while (__hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.epoch) {
       __builtin_amdgcn_s_sleep(4);
       if (clock64() - t0 > a.wait_cycles) {   // a peer never arrived: flag the error, poison the slice
-        atomicOr(reinterpret_cast<unsigned*>(a.region[a.rank] + a.err_off), 1u << (tid & 31));
+        // bits 0..15 = the peer this rank waited for (world <= 16); bit 31 is reserved for "a peer timed out"
+        __hip_atomic_fetch_or(reinterpret_cast<unsigned*>(a.region[a.rank] + a.err_off), 1u << (tid & 15),
+                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         timed_out = 1;
         break;
       }
@@ -85,7 +87,10 @@ __global__ __launch_bounds__(AR_THREADS) void oneshot_allreduce_kernel(ArArgs a)
   if (timed_out && tid < a.world && tid != a.rank) {
     // tell EVERY peer (bit 31 of its error word): a peer whose own waits succeeded has applied this step, but its
     // next poll raises too, so all ranks stop together instead of training on diverged replicas
-    atomicOr(reinterpret_cast<unsigned*>(a.region[tid] + a.err_off), 0x80000000u | (1u << a.rank));   // rank < 16
+    // system scope like every other cross-GPU access here: the peer's host poll sees it without waiting for the end
+    // of this kernel's write-back
+    __hip_atomic_fetch_or(reinterpret_cast<unsigned*>(a.region[tid] + a.err_off), 0x80000000u | (1u << (a.rank & 15)),
+                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (timed_out) {   // NaN output: FlatAdam's non-finite guard skips the step instead of applying a partial sum
     for (long long i = (a.vec ? 4 * lo : lo) + tid; i < (a.vec ? 4 * hi : hi); i += AR_THREADS) a.dst[i] = __int_as_float(0x7fc00000);

@@ -9,7 +9,8 @@ device env (``synthetic.py``) is the default backend.
 Protocol-error recovery (``StarCraft2_Env.py:422-423,468-472,507-530``): a ``ProtocolError`` / ``ConnectionError`` of
 the SC2 client during ``reset`` or ``step`` closes the game process and launches a new one (``full_restart``); a
 step that hit it ends the episode (every agent done, zero reward), and every info dict carries the running
-``restarts`` count as the reference's does (``:521,603``).  ``SC2Game`` takes the env constructor and the error
+``restarts`` count as the reference's does (``:521,603``).  The env object's episode counters (battles won / played,
+timeouts) survive a restart, and the error step's info carries the reference's keys (``:517-524``).  ``SC2Game`` takes the env constructor and the error
 types as arguments, so the recovery path is tested without the game (``tests/test_smac.py``).
 """
 from __future__ import annotations
@@ -42,14 +43,32 @@ class SC2Game:
         from .synthetic import Discrete
         self.action_space = [Discrete(info["n_actions"])] * self.n_agents
 
+    # episode counters of the env object that survive a restart: the reference relaunches only the SC2 process and
+    # keeps its env object (StarCraft2_Env.py:468-472), so the runner's incremental win rate stays monotone
+    _COUNTERS = ("battles_won", "battles_game", "timeouts")
+
     def full_restart(self):
-        """Close the game process and launch a new one (StarCraft2_Env.full_restart)."""
+        """Close the game process and launch a new one (StarCraft2_Env.full_restart).  smac's env relaunches its own
+        process in place; an env object without that method is rebuilt with its episode counters carried over."""
+        self.force_restarts += 1
+        if hasattr(self.env, "full_restart"):
+            self.env.full_restart()
+            return
+        kept = {k: getattr(self.env, k) for k in self._COUNTERS if hasattr(self.env, k)}
         try:
             self.env.close()
         except Exception:   # noqa: BLE001 — the process is already gone
             pass
         self.env = self.make_env()
-        self.force_restarts += 1
+        for k, v in kept.items():
+            setattr(self.env, k, v)
+
+    def _error_info(self):
+        """The info dict of a step that hit a protocol error (StarCraft2_Env.py:517-524)."""
+        e = self.env
+        return {"battles_won": getattr(e, "battles_won", 0), "battles_game": getattr(e, "battles_game", 0),
+                "battles_draw": getattr(e, "timeouts", 0), "bad_transition": False,
+                "won": bool(getattr(e, "win_counted", False))}
 
     def _observe(self):
         obs = np.array(self.env.get_obs())
@@ -75,8 +94,9 @@ class SC2Game:
         except self.errors:
             # the reference ends the episode on a protocol error after a full restart (StarCraft2_Env.py:507-530)
             self.full_restart()
+            info = self._error_info()
             obs, state, ava = self.reset()
-            r, done, info = 0.0, True, {}
+            r, done = 0.0, True
         info = dict(info or {})
         info["restarts"] = self.force_restarts
         dones = np.array([bool(done)] * self.n_agents)

@@ -69,30 +69,58 @@ def check_build(L, src_dir=None, default_lib=None):
 BUILD_ID = None   # the loaded library's source hash (logged by bench.py / smoke)
 
 
+class _BuildLock:
+    """Exclusive ``flock`` on ``_lib/.build.lock``: the ranks of one node (``bench.py --gpus N``, torchrun) that find
+    a stale library check and rebuild it one at a time, so the first rebuilds and the others see it fresh."""
+
+    def __init__(self, lib_dir):
+        self.path = os.path.join(lib_dir, ".build.lock")
+
+    def __enter__(self):
+        import fcntl
+        self.f = open(self.path, "a")
+        fcntl.flock(self.f, fcntl.LOCK_EX)
+        return self
+
+    def __exit__(self, *exc):
+        import fcntl
+        fcntl.flock(self.f, fcntl.LOCK_UN)
+        self.f.close()
+
+
+def _sidecar_stale(b):
+    """Why the default library must be rebuilt, judged from its sidecar identity file (no dlopen), or None."""
+    if not os.path.exists(LIB_PATH):
+        return "not built"
+    got = b.sidecar(LIB_PATH)
+    if got is None:
+        return "no build identity sidecar"
+    if got != (b.source_hash(), b.flags_hash()):
+        return f"built from {got}, the tree has {(b.source_hash(), b.flags_hash())}"
+    return None
+
+
 def lib():
-    """Load the HIP library, refusing a stale one: its embedded source / flags hash must match the tree.  A stale
-    library is rebuilt when hipcc exists (the default library only) and is an error otherwise."""
+    """Load the HIP library, refusing a stale one: its embedded source / flags hash must match the tree.  When hipcc
+    exists, the default library is checked (by its sidecar identity, before it is ever dlopen'ed) and rebuilt if
+    stale, under a file lock shared by every process of the node; anything else stale is an error."""
     global _lib, _load_error, BUILD_ID
     if _lib is None:
+        b = _build_mod()
+        if os.path.exists(b.HIPCC) and LIB_PATH == b.OUT:
+            with _BuildLock(os.path.dirname(LIB_PATH)):
+                why = _sidecar_stale(b)   # re-checked under the lock: another rank may have just rebuilt it
+                if why is not None:
+                    print(f"[kernels] {LIB_PATH} is stale ({why}): rebuilding", flush=True)
+                    b.build()
         if not os.path.exists(LIB_PATH):
             _load_error = f"{LIB_PATH} not built (run python -c 'import __graft_entry__ as g; g.build()')"
             raise RuntimeError(_load_error)
         L = ctypes.CDLL(LIB_PATH)
         why = check_build(L)
         if why is not None:
-            b = _build_mod()
-            if not (os.path.exists(b.HIPCC) and LIB_PATH == b.OUT):
-                _load_error = f"stale native library {LIB_PATH}: {why}; rebuild it (python mat_dcml_amd/csrc/build.py)"
-                raise RuntimeError(_load_error)
-            import _ctypes
-            _ctypes.dlclose(L._handle)
-            print(f"[kernels] {LIB_PATH} is stale ({why}): rebuilding", flush=True)
-            b.build()
-            L = ctypes.CDLL(LIB_PATH)
-            why = check_build(L)
-            if why is not None:
-                _load_error = f"native library still stale after a rebuild: {why}"
-                raise RuntimeError(_load_error)
+            _load_error = f"stale native library {LIB_PATH}: {why}; rebuild it (python mat_dcml_amd/csrc/build.py)"
+            raise RuntimeError(_load_error)
         BUILD_ID = (build_identity(L) or ("unidentified",))[0]   # A/B variants may predate the identity
         _lib = L
         _declare(_lib)

@@ -132,6 +132,11 @@ class DCMLRunner:
         G = self._groups()
         if G > 1:
             return self._rollout_groups(G)
+        # the weight packs of the decode / encoder kernels are rebuilt once per optimizer step: their own phase, so
+        # the first rollout step's decode does not carry them
+        with self.timers("pack"):
+            from ..ops import mat_fused
+            mat_fused.refresh_packs(self.policy.transformer)
         for step in range(self.episode_length):
             with self.timers("decode"):
                 values, actions, logp = self.collect(step)

@@ -1,4 +1,7 @@
-"""Micro-benchmark of the fused training kernels on the bench minibatch shape (3200 sequences x 33 agents)."""
+"""Micro-benchmark of the fused training kernels on the bench minibatch shape (3200 sequences x 33 agents).
+
+``python tests/bench_train_kernels.py [B] [L] [iters]`` (defaults 3200 33 10).
+"""
 import sys
 import time
 
@@ -31,8 +34,10 @@ def main(B=3200, L=33, iters=10):
         if it >= 2:
             for k, (s, e) in ev.items():
                 tot[k] += s.elapsed_time(e)
-    print(" | ".join(f"{k} {v / iters * 1e3:.0f} us" for k, v in tot.items()), flush=True)
+    print(f"B={B} L={L}: " + " | ".join(f"{k} {v / iters * 1e3:.0f} us" for k, v in tot.items())
+          + f" | sum {sum(tot.values()) / iters * 1e3:.0f} us", flush=True)
 
 
 if __name__ == "__main__":
-    main()
+    a = [int(x) for x in sys.argv[1:]]
+    main(*a)

@@ -43,13 +43,16 @@ def test_bench_self_launches_two_ranks():
     assert cm["grad_allreduce"] + cm["stats_allreduce"] < out["ms_per_step"]
     # SMALL = 1 epoch x 1 minibatch: one gradient average and one epoch-statistics all-reduce per step
     assert out["collectives_per_step"] == {"grad_allreduce": 1, "stats_allreduce": 1}
-    # phase breakdown: per-step time of the rollout phases and the update, and the training
-    # forward / backward per minibatch
+    # phase breakdown: separate instrumented steps after the uninstrumented timed
+    # loop, every phase occurrence timed (nothing sampled / scaled): the rollout phases + update partition the step
     ph = out["phase_ms_per_step"]
-    assert {"decode", "env", "insert", "update", "train_fwd", "train_bwd"} <= set(ph) and all(v > 0 for v in ph.values())
+    assert {"pack", "decode", "env", "insert", "update", "train_fwd", "train_bwd"} <= set(ph)
+    assert all(v > 0 for v in ph.values())
     assert ph["train_fwd"] + ph["train_bwd"] <= ph["update"]
-    # decode / env / insert are sampled (every 10th step) and scaled: an estimate, not a partition of the step
-    assert sum(ph[k] for k in ("decode", "env", "insert", "update")) <= out["ms_per_step"] * 1.25
+    run = out["phase_run"]
+    top = sum(ph[k] for k in ("pack", "decode", "env", "insert", "update"))
+    assert abs(run["phases_sum_ms"] - top) < 0.01
+    assert top <= 1.02 * run["ms_per_step"]
     tk = out["train_kernels_ms_per_minibatch"]
     assert set(tk) == {"fwd", "bwd"} and abs(tk["fwd"] - ph["train_fwd"]) < 1e-2   # 1 epoch x 1 minibatch
 
@@ -73,3 +76,22 @@ def test_rank_without_own_gpu_fails_loudly(monkeypatch, backend, share):
     monkeypatch.setenv("MAT_DCML_SHARE_DEVICES", share)
     with pytest.raises(RuntimeError, match="needs one GPU per rank"):
         C.init_from_env(prefer_gpu=True)
+
+
+def test_bench_four_ranks_full_update_schedule():
+    """``bench.py --gpus 4`` end to end through launch_ranks (gloo), with the reference's PPO
+    schedule (15 epochs x 4 minibatches): 60 gradient averages and 15 epoch-statistics all-reduces per step, every
+    rank timed."""
+    args = ["--steps", "1", "--warmup", "0", "--envs", "8", "--episode_length", "2", "--n_workers", "4",
+            "--ppo_epoch", "15", "--num_mini_batch", "4", "--no_eval", "--no_phase_timers"]
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", *args], cwd=ROOT, env=_env(), capture_output=True,
+                       text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["ranks"] == 4 and out["n_gpus"] == 4 and out["config"]["parallelism"] == "dp4"
+    assert out["collectives_per_step"] == {"grad_allreduce": 60, "stats_allreduce": 15}
+    assert len(out["rank_ms_per_step"]) == 4 and all(0 < t <= out["ms_per_step"] * 1.001 for t in out["rank_ms_per_step"])
+    assert out["config"]["global_batch"] == 32
+    assert "phase_ms_per_step" not in out

@@ -133,3 +133,37 @@ def test_sc2_protocol_error_full_restart():
     assert (o == 0).all()                             # a fresh episode of the relaunched game
     o, s, r, d, info, a = g.step([0, 1, 2])
     assert not d.any() and info[0]["restarts"] == 1
+
+
+def test_sc2_restart_keeps_episode_counters():
+    """a restart must not reset battles_won / battles_game / timeouts (the reference keeps its env object,
+    StarCraft2_Env.py:468-472), and the error step's info carries the reference's keys (:517-524)."""
+    from mat_dcml_amd.envs.smac.adapter import SC2Game
+    made = []
+
+    def make_env():
+        e = _FlakySC2(fail_on=(2,) if not made else ())
+        e.battles_won, e.battles_game, e.timeouts, e.win_counted = 0, 0, 0, False
+        made.append(e)
+        return e
+    g = SC2Game(make_env, errors=(ConnectionError,))
+    g.reset()
+    made[0].battles_won, made[0].battles_game, made[0].timeouts = 3, 5, 1
+    g.step([0, 1, 2])
+    o, s, r, d, info, a = g.step([0, 1, 2])          # protocol error -> restart
+    assert d.all() and len(made) == 2
+    for i in info:
+        assert (i["battles_won"], i["battles_game"], i["battles_draw"], i["restarts"]) == (3, 5, 1, 1)
+        assert i["bad_transition"] is False and i["won"] is False
+    assert (g.env.battles_won, g.env.battles_game, g.env.timeouts) == (3, 5, 1)
+
+    class InPlace(_FlakySC2):   # smac's env: relaunches its own process, same object
+        def full_restart(self):
+            self.relaunched = True
+            self.fail_on = ()
+    e = InPlace(fail_on=(1,))
+    e.battles_won, e.battles_game, e.timeouts, e.win_counted = 7, 9, 2, False
+    g = SC2Game(lambda: e, errors=(ConnectionError,))
+    g.reset()
+    o, s, r, d, info, a = g.step([0, 1, 2])
+    assert g.env is e and e.relaunched and info[0]["battles_won"] == 7 and info[0]["restarts"] == 1
