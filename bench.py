@@ -240,7 +240,7 @@ def eval_block(a, args, runner, dev):
     ``--steps``: the benchmarked runner's weights are never used here."""
     from mat_dcml_amd.algos.policy import TransformerPolicy
     from mat_dcml_amd.envs.dcml.spaces import dcml_action_spaces
-    from mat_dcml_amd.runner.benchmark import run_sweep
+    from mat_dcml_amd.runner.benchmark import eval_report, run_sweep
 
     def fresh_policy():
         torch.manual_seed(1)
@@ -267,6 +267,18 @@ def eval_block(a, args, runner, dev):
         pol.restore(ckpt)
         info["trained"] = summary(run_sweep(pol, runner.dcml, dev, latency_b1=20, **kw))
         info["trained"]["checkpoint"] = ckpt
+        # held-out preset sets (Sample_2..10, which the reference benchmark never reads) and, on Sample_1, where each
+        # point lies against the heuristic's own ct-payment trade-off (K = floor(rho N), rho = 0.3 .. 1.0)
+        rep = eval_report(pol, runner.dcml, dev, **{k: v for k, v in kw.items() if k != "verbose"})
+        info["trained"]["wins_vs_fixed_sample1"] = {k: rep["per_sample"][1][k]
+                                                    for k in ("ct_wins", "payment_wins", "both_wins")}
+        info["trained"]["heldout"] = rep.get("heldout")
+        fr = rep.get("frontier") or []
+        info["trained"]["frontier"] = {"ratios": rep.get("frontier_ratios"),
+                                       "beyond_per_point": [f["beyond"] for f in fr],
+                                       "dominated_by_per_point": [f["dominated_by"] for f in fr],
+                                       "payment_margin_per_point": [f["margin"] for f in fr],
+                                       "beyond_count": sum(f["beyond"] for f in fr)}
     info["fixed_heuristic"] = summary(run_sweep(None, runner.dcml, dev, fixed=True, latency_b1=0, **kw))
     return info
 

@@ -166,6 +166,9 @@ _FOOTBALL_FLAGS = [
 _FRAMEWORK_FLAGS = [
     ("n_workers", int, 100, "DCML worker count W (agents = W + 1); 4 / 32 / 100 / 128 in the BASELINE configs"),
     ("shannon", "true", F, "Shannon-capacity links in the DCML env (shannon_enable, Shannon.py)"),
+    ("reward_alpha", float, 99.0, "DCML reward = -(alpha * completion time + beta * payment); 99 / 1 = the reference "
+     "(DCML_ENV_Functions.py:15-17)"),
+    ("reward_beta", float, 1.0, "payment weight of the DCML reward (see reward_alpha)"),
     ("central_execution", int, 1, "1: one Semi_Discrete space for all agents; 0: per-agent spaces (Env(central_execution=False))"),
     ("kernels", str, "auto", "auto|hip|torch — fused HIP kernels on GPU (auto) or the PyTorch reference path"),
     ("dtype", str, "bf16", "bf16|fp32 compute dtype (master weights and optimizer state are fp32)"),

@@ -133,3 +133,98 @@ def save_npy(path: str, result: dict):
 def load_npy(path: str):
     with open(path, "rb") as f:
         return np.load(f), np.load(f)
+
+
+# ---------------------------------------------------------------------------------------------------- eval analysis
+HELDOUT_SAMPLES = tuple(range(2, 11))   # the reference ships Sample_1..10; its benchmark reads only Sample_1
+FRONTIER_RATIOS = (0.3, 0.4, 0.5, 0.6, 0.7, 0.8, 0.9, 1.0)
+
+
+def run_sweep_sample(policy, cfg: DCMLConfig, device, sample: int, **kw):
+    """``run_sweep`` on preset set ``Sample_{sample}`` instead of the protocol's Sample_1."""
+    import dataclasses
+    return run_sweep(policy, dataclasses.replace(cfg, preset_sample=sample), device, **kw)
+
+
+def heuristic_frontier(cfg: DCMLConfig, device, ratios=FRONTIER_RATIOS, sample: int = 1, **kw):
+    """The fixed heuristic's (ct, payment) trade-off at every sweep point: all available workers with
+    K = floor(rho N) (``DCML_BID_FIRST_MA_ENV_SingleProcess.py:58-62`` has rho = 0.7) for each rho.
+    Returns {rho: run_sweep result}."""
+    import dataclasses
+    out = {}
+    for rho in ratios:
+        c = dataclasses.replace(cfg, fixed_k_ratio=float(rho), preset_sample=sample)
+        out[float(rho)] = run_sweep(None, c, device, fixed=True, latency_b1=0, **kw)
+    return out
+
+
+def frontier_verdict(ct: float, pay: float, pts) -> dict:
+    """Where a policy's (ct, payment) point lies against the heuristic's frontier ``pts`` = [(ct_rho, pay_rho)]:
+    * ``dominated_by``: the ratios whose heuristic point is at least as good on both objectives (empty = not
+      dominated by any heuristic setting);
+    * ``beyond``: the point lies strictly below the lower-left convex hull of the heuristic points in the
+      (ct, payment) plane, i.e. no mixture of heuristic settings reaches it — a policy that merely moves along the
+      heuristic's trade-off lies ON the curve, not beyond it;
+    * ``margin``: payment of the frontier at this ct minus the policy's payment (> 0 = beyond), None outside the
+      frontier's ct range."""
+    import numpy as np
+    P = sorted((float(c), float(p), r) for r, (c, p) in pts.items())
+    dominated = [r for c, p, r in P if c <= ct and p <= pay]
+    # lower convex hull (monotone chain), ct ascending
+    hull = []
+    for c, p, _ in P:
+        while len(hull) >= 2 and (hull[-1][0] - hull[-2][0]) * (p - hull[-2][1]) - (hull[-1][1] - hull[-2][1]) * (c - hull[-2][0]) <= 0:
+            hull.pop()
+        hull.append((c, p))
+    xs, ys = np.array([h[0] for h in hull]), np.array([h[1] for h in hull])
+    margin = None
+    if xs[0] <= ct <= xs[-1]:
+        margin = float(np.interp(ct, xs, ys) - pay)
+    elif ct > xs[-1]:
+        margin = float(ys[-1] - pay)   # slower than every heuristic point: beyond only if cheaper than the cheapest
+    beyond = (not dominated) and (margin is None or margin > 0)
+    return {"dominated_by": dominated, "beyond": bool(beyond), "margin": None if margin is None else round(margin, 4)}
+
+
+def eval_report(policy, cfg: DCMLConfig, device, samples=(1,) + HELDOUT_SAMPLES, frontier: bool = True, **kw):
+    """The protocol sweep (AW, 11 points x ``steps`` decisions, stride 10) of ``policy`` and of the fixed heuristic
+    on every preset set in ``samples``, with per-point wins (policy strictly better on ct / payment / both) and,
+    on Sample_1, the heuristic's frontier verdict per point.  ``policy`` None = heuristic only."""
+    import numpy as np
+    kw = {**dict(sweep="AW", n_points=11, steps=1000, shards=50, stride=10, verbose=False), **kw}
+    per = {}
+    for s in samples:
+        fx = run_sweep_sample(None, cfg, device, s, fixed=True, latency_b1=0, **kw)
+        ent = {"fixed": {"ct": fx["ct"], "payment": fx["payment"]}}
+        if policy is not None:
+            r = run_sweep_sample(policy, cfg, device, s, latency_b1=0, **kw)
+            ent["policy"] = {"ct": r["ct"], "payment": r["payment"], "reward": r["reward"]}
+            ent["ct_wins"] = int(sum(a < b for a, b in zip(r["ct"], fx["ct"])))
+            ent["payment_wins"] = int(sum(a < b for a, b in zip(r["payment"], fx["payment"])))
+            ent["both_wins"] = int(sum(a < b and c < d for a, b, c, d in zip(r["ct"], fx["ct"], r["payment"],
+                                                                             fx["payment"])))
+        per[s] = ent
+    out = {"per_sample": per}
+    if policy is not None:
+        held = [s for s in samples if s != 1]
+        def ms(key, field):
+            v = np.array([np.mean(per[s]["policy" if field == "p" else "fixed"][key]) for s in held])
+            return [round(float(v.mean()), 4), round(float(v.std()), 4)]
+        if held:
+            out["heldout"] = {"samples": held,
+                              "policy_ct_mean_std": ms("ct", "p"), "policy_payment_mean_std": ms("payment", "p"),
+                              "fixed_ct_mean_std": ms("ct", "f"), "fixed_payment_mean_std": ms("payment", "f"),
+                              "both_wins_per_sample": [per[s]["both_wins"] for s in held],
+                              "ct_wins_per_sample": [per[s]["ct_wins"] for s in held],
+                              "payment_wins_per_sample": [per[s]["payment_wins"] for s in held]}
+    if frontier and 1 in per:
+        fr = heuristic_frontier(cfg, device, sample=1, **kw)
+        out["frontier_ratios"] = list(fr)
+        if policy is not None:
+            pol = per[1]["policy"]
+            out["frontier"] = [frontier_verdict(pol["ct"][i], pol["payment"][i],
+                                                {r: (fr[r]["ct"][i], fr[r]["payment"][i]) for r in fr})
+                               for i in range(len(pol["ct"]))]
+        out["frontier_points"] = {str(r): {"ct": [round(x, 4) for x in fr[r]["ct"]],
+                                           "payment": [round(x, 3) for x in fr[r]["payment"]]} for r in fr}
+    return out

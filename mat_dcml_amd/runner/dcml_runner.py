@@ -59,7 +59,9 @@ class DCMLRunner:
         self.use_eval, self.eval_interval = a.use_eval, a.eval_interval
         self.train_stride, self.eval_stride = getattr(a, "train_stride", 1), getattr(a, "eval_stride", 2)
         self.dcml = config.get("dcml_cfg") or DCMLConfig(n_workers=getattr(a, "n_workers", 100),
-                                                         shannon=bool(getattr(a, "shannon", False)))
+                                                         shannon=bool(getattr(a, "shannon", False)),
+                                                         alpha=float(getattr(a, "reward_alpha", 99.0)),
+                                                         beta=float(getattr(a, "reward_beta", 1.0)))
         rank = self.comm.rank
         self.faults = FaultInjector(getattr(a, "fault_inject", None), rank)
         if self.faults.disable_frac is not None:

@@ -66,3 +66,31 @@ def test_benchmark_cli(tmp_path):
     assert r.stdout.count("ct:") == 3
     ct, pay = load_npy(str(out))
     assert ct.shape == (3, 1)
+
+
+def test_frontier_verdict_geometry():
+    """a policy point ON the heuristic's ct-payment trade-off is not 'beyond' it; below the
+    lower hull of the heuristic points it is; a heuristic point better on both objectives dominates it."""
+    from mat_dcml_amd.runner.benchmark import frontier_verdict
+    pts = {0.5: (1.0, 10.0), 0.7: (2.0, 6.0), 0.9: (4.0, 5.0)}
+    on = frontier_verdict(1.5, 8.0, pts)          # the chord between 0.5 and 0.7
+    assert not on["beyond"] and abs(on["margin"]) < 1e-9 and on["dominated_by"] == []
+    below = frontier_verdict(1.5, 7.0, pts)
+    assert below["beyond"] and abs(below["margin"] - 1.0) < 1e-9
+    dom = frontier_verdict(2.5, 6.5, pts)
+    assert dom["dominated_by"] == [0.7] and not dom["beyond"]
+    fast = frontier_verdict(0.9, 12.0, pts)       # faster than every heuristic setting: nothing dominates it
+    assert fast["beyond"] and fast["margin"] is None
+
+
+def test_eval_report_heldout_and_frontier_cpu():
+    """eval_report on the CPU env path (heuristic only, 40 decisions): per-sample results for Sample_1 and a
+    held-out set, and the heuristic frontier points at every rho."""
+    from mat_dcml_amd.envs.dcml.config import DCMLConfig
+    from mat_dcml_amd.runner.benchmark import FRONTIER_RATIOS, eval_report
+    rep = eval_report(None, DCMLConfig(n_workers=8), "cpu", samples=(1, 4), steps=40, shards=10, n_points=3)
+    assert set(rep["per_sample"]) == {1, 4}
+    assert len(rep["per_sample"][4]["fixed"]["ct"]) == 3
+    assert [float(r) for r in rep["frontier_points"]] == list(FRONTIER_RATIOS)
+    # rho = 0.7 on Sample_1 reproduces the protocol's fixed-heuristic sweep
+    assert rep["frontier_points"]["0.7"]["ct"] == [round(x, 4) for x in rep["per_sample"][1]["fixed"]["ct"]]
