@@ -384,6 +384,13 @@ __device__ __forceinline__ void flush_vec(const CT& acc, float* dst, int lane) {
 }
 
 // ------------------------------------------------------------------------------------------ weight gradients
+// A/B ablation (-DMDL_ABLATE_WATOM): the weight-gradient GEMMs run, but their fp32 atomics are skipped (a runtime-false
+// predicate the compiler cannot fold) — measures what the atomic traffic costs.  Never in a shipped build.
+#ifdef MDL_ABLATE_WATOM
+#define WATOM(ptr, v) do { const float v_ = (v); if (v_ == 1.17549435e-38f) atomicAdd((ptr), v_); } while (0)
+#else
+#define WATOM(ptr, v) atomicAdd((ptr), (v))
+#endif
 // dW[n][k] (row stride ld) += Σ_t Y[t][n] X[t][k] for n < nrows, k < ncols, and db[n] += Σ_t Y[t][n], from
 // token-major swizzled LDS tiles of KP rows (KP % 32 == 0, padded rows zero).  The 16 output blocks (row block
 // j & 3, column tile j >> 2) are dealt round robin, j = wave + NW i: a wave's blocks share one row block (NW % 4 == 0)
@@ -423,7 +430,7 @@ __device__ __forceinline__ void wgrad_g(const bf16_t* Y, const bf16_t* X, int KP
       for (int r = 0; r < 4; ++r) {
         const int n = 16 * rb + 4 * g + r, k = 16 * ct + c16;
         const bool ok = bj < 16 && ct < nct && n < nrows && k < ncols;
-        if (ok) atomicAdd(dW + n * ld + k, acc[j][r]);
+        if (ok) WATOM(dW + n * ld + k, acc[j][r]);
       }
     }
   }
@@ -483,7 +490,7 @@ __device__ __forceinline__ void wgrad64_shared_x(const bf16_t* const (&Y)[NM], c
         const int bj = wave + NW * j, ct = bj >> 2;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          if (bj < 16) atomicAdd(dW + (16 * rb + 4 * g + r) * 64 + 16 * ct + c16, acc[i][j][r]);
+          if (bj < 16) WATOM(dW + (16 * rb + 4 * g + r) * 64 + 16 * ct + c16, acc[i][j][r]);
       }
     }
     if (bias && db && c16 < 4) {

@@ -107,7 +107,9 @@ def lib():
     global _lib, _load_error, BUILD_ID
     if _lib is None:
         b = _build_mod()
-        if os.path.exists(b.HIPCC) and LIB_PATH == b.OUT:
+        # only the default library is rebuilt: a named variant (A/B timing builds, MAT_DCML_LIBNAME) was built with
+        # flags the environment of this process need not carry, so "stale" there means "leave it alone"
+        if os.path.exists(b.HIPCC) and LIB_PATH == b.OUT and os.path.basename(LIB_PATH) == "libmatdcml.so":
             with _BuildLock(os.path.dirname(LIB_PATH)):
                 why = _sidecar_stale(b)   # re-checked under the lock: another rank may have just rebuilt it
                 if why is not None:

@@ -5,7 +5,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for lib in libmatdcml.so libmatdcml_ab_nw12.so libmatdcml_ab_nw16.so; do
+for lib in libmatdcml.so libmatdcml_ab_nw12.so libmatdcml_ab_nw16.so libmatdcml_ab_watom.so libmatdcml_ab_nw12watom.so; do
   for L in 33 101; do
     echo -n "$lib " >> gpurun_out/train_micro.txt
     MAT_DCML_LIBNAME=$lib timeout -k 10 200 python3 tests/bench_train_kernels.py 3200 $L 10 >> gpurun_out/train_micro.txt 2>&1 || { tail gpurun_out/train_micro.txt; exit 1; }
