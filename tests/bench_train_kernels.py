@@ -2,6 +2,7 @@
 
 ``python tests/bench_train_kernels.py [B] [L] [iters]`` (defaults 3200 33 10).
 """
+import os
 import sys
 import time
 
@@ -19,8 +20,16 @@ def main(B=3200, L=33, iters=10):
     obs = torch.rand(B, L, 7, device=dev)
     ava = torch.ones(B, L, 2, device=dev)
     actions = (torch.rand(B, L, 1, device=dev) < 0.5).float()
-    for p in m.parameters():
-        p.grad = torch.zeros_like(p)
+    # the trainer's gradient layout: one flat fp32 buffer, the backward's weight-gradient atomics spread over a
+    # 32-copy workspace (algos/mat_trainer.py; without it every workgroup adds into one copy)
+    from mat_dcml_amd.ops import ppo_fused
+    fp = ppo_fused.flatten_params(m)
+    fg = torch.zeros_like(fp)
+    for p, off in ppo_fused.param_offsets(m):
+        p.grad = fg[off:off + p.numel()].view_as(p)
+    copies = int(os.environ.get("MAT_DCML_GRAD_COPIES", "32"))
+    if copies > 0:
+        mat_train.attach_grad_workspace(m, fg, copies=copies)
     enc, dec = mat_train.EncoderFused(m), mat_train.DecoderFused(m)
     ev = {k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for k in
           ("enc_fwd", "dec_fwd", "dec_bwd", "enc_bwd")}
@@ -30,6 +39,8 @@ def main(B=3200, L=33, iters=10):
         ev["dec_fwd"][0].record(); lp, ent = dec.forward(rep, actions, ava); ev["dec_fwd"][1].record()
         ev["dec_bwd"][0].record(); drep = dec.backward(torch.ones_like(lp), torch.ones_like(ent)); ev["dec_bwd"][1].record()
         ev["enc_bwd"][0].record(); enc.backward(drep, torch.ones_like(v)); ev["enc_bwd"][1].record()
+        if copies > 0:
+            mat_train.reduce_grad_workspace(m)
         torch.cuda.synchronize()
         if it >= 2:
             for k, (s, e) in ev.items():
