@@ -205,7 +205,15 @@ __device__ __forceinline__ CTr ld_lds(const bf16_t* buf, int rt, int lane) {
 // token-on-lane order — feature 16mt + 4g + r at element 16g + 4mt + r — so lane (g, c) owns 32 contiguous bytes of
 // token c (two 16-byte accesses; a [tok][64] row-major record took four scattered 8-byte pieces per lane, and the
 // forward's saves were store-issue bound).  Rows >= NR read as zero / are not written.
+// A/B ablation (-DMDL_ABLATE_LDG): every chunk reads the saved rows of chunk 0 (L2-resident) instead of its own —
+// wrong values, but it prices the HBM latency / bandwidth of the saved-activation loads.  Never in a shipped build.
+#ifdef MDL_ABLATE_LDG
+#define LDG_TOK0(t) 0
+#else
+#define LDG_TOK0(t) (t)
+#endif
 __device__ __forceinline__ CTr ld_g(const bf16_t* src, int tok0, int rt, int NR, int lane) {
+  tok0 = LDG_TOK0(tok0);
   const int g = lane >> 4, row = rt * 16 + (lane & 15);
   const bool ok = row < NR;
   const uint4* base = (const uint4*)(src + (size_t)(tok0 + (ok ? row : 0)) * 64 + 16 * g);
@@ -227,6 +235,7 @@ __device__ __forceinline__ void st_g(bf16_t* dst, int tok0, int rt, int NR, cons
 }
 // plain global [tok][64] f32
 __device__ __forceinline__ CT ld_gf(const float* src, int tok0, int rt, int NR, int lane) {
+  tok0 = LDG_TOK0(tok0);
   const int g = lane >> 4, row = rt * 16 + (lane & 15);
   const bool ok = row < NR;
   const float* base = src + (size_t)(tok0 + (ok ? row : 0)) * 64 + 4 * g;
@@ -255,7 +264,7 @@ __device__ __forceinline__ void st_tokf(float* dst, int rt, float v, const Ctx& 
 }
 __device__ __forceinline__ float ld_tokf(const float* src, int rt, const Ctx& c) {
   const int row = rt * 16 + (c.lane & 15);
-  return row < c.NR ? src[(size_t)(c.tok0 + row)] : 0.f;   // padded rows: rstd 0 -> zero gradient
+  return row < c.NR ? src[(size_t)(LDG_TOK0(c.tok0) + row)] : 0.f;   // padded rows: rstd 0 -> zero gradient
 }
 
 // ------------------------------------------------------------------------------------------ LayerNorm (per token)
@@ -391,6 +400,30 @@ __device__ __forceinline__ void flush_vec(const CT& acc, float* dst, int lane) {
 #else
 #define WATOM(ptr, v) atomicAdd((ptr), (v))
 #endif
+// Weight-gradient blocks per wave (8-wave backward): wave w owns row block w & 3 and the two ADJACENT column tiles
+// 2 (w >> 2), 2 (w >> 2) + 1, i.e. 16 rows x 32 contiguous columns of a 64 x 64 gradient.  The MFMA C layout puts
+// lane (g, c) on rows 4g + r of one column tile — a per-register atomic would cover 4 rows x 64 B; one
+// v_permlane16_swap + one v_permlane32_swap per register pair regroup the two tiles so that every fp32 atomic
+// wave-instruction covers 2 rows x 128 contiguous bytes (the rate the memory-side atomic unit is measured at).
+#ifndef MDL_WATOM_ROWS
+#define MDL_WATOM_ROWS 1
+#endif
+constexpr bool WG_ROWS2 = MDL_WATOM_ROWS && NW == 8;
+__device__ __forceinline__ int wg_ct(int wave, int j) { return WG_ROWS2 ? 2 * (wave >> 2) + j : (wave + NW * j) >> 2; }
+__device__ __forceinline__ bool wg_has(int wave, int j) { return WG_ROWS2 ? true : wave + NW * j < 16; }
+// flush a wave's 16 x 32 block (acc0 = column tile ct0, acc1 = ct0 + 1; rows 16 rb + 4g + r) of a 64-wide gradient
+__device__ __forceinline__ void flush_rows2(const f32x4& acc0, const f32x4& acc1, float* dW, int rb, int ct0, int lane) {
+  const int s = lane >> 5, col = 16 * ct0 + (lane & 31);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float x0 = acc0[r], x1 = acc1[r];   // scalars first: never bit_cast a subscripted vector element
+    const auto p = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, x0), __builtin_bit_cast(unsigned, x1),
+                                                    false, false);   // [a0 b0 a2 b2], [a1 b1 a3 b3] (16-lane rows)
+    const auto q = __builtin_amdgcn_permlane32_swap((unsigned)p[0], (unsigned)p[1], false, false);   // [a0 b0 a1 b1], [a2 b2 a3 b3]
+    WATOM(dW + (16 * rb + 4 * s + r) * 64 + col, __builtin_bit_cast(float, (unsigned)q[0]));
+    WATOM(dW + (16 * rb + 8 + 4 * s + r) * 64 + col, __builtin_bit_cast(float, (unsigned)q[1]));
+  }
+}
 // dW[n][k] (row stride ld) += Σ_t Y[t][n] X[t][k] for n < nrows, k < ncols, and db[n] += Σ_t Y[t][n], from
 // token-major swizzled LDS tiles of KP rows (KP % 32 == 0, padded rows zero).  The 16 output blocks (row block
 // j & 3, column tile j >> 2) are dealt round robin, j = wave + NW i: a wave's blocks share one row block (NW % 4 == 0)
@@ -403,7 +436,7 @@ __device__ __forceinline__ void wgrad_g(const bf16_t* Y, const bf16_t* X, int KP
   const int rb = wave & 3;
   if (wave >= 4) db = nullptr;
   const int nct = dW ? (ncols + 15) >> 4 : 0;
-  if ((!db && (wave >> 2) >= nct) || 16 * rb >= nrows) return;
+  if ((!db && wg_ct(wave, 0) >= nct) || 16 * rb >= nrows) return;
   const int g = lane >> 4, c16 = lane & 15;
   f32x4 acc[NCT];
 #pragma unroll
@@ -414,22 +447,24 @@ __device__ __forceinline__ void wgrad_g(const bf16_t* Y, const bf16_t* X, int KP
     const bf16x8 a = ld_frag_T(Y, k0, 16 * rb, lane);
 #pragma unroll
     for (int j = 0; j < NCT; ++j) {
-      const int bj = wave + NW * j, ct = bj >> 2;
-      if (bj < 16 && ct < nct) {
+      const int ct = wg_ct(wave, j);
+      if (wg_has(wave, j) && ct < nct) {
         const bf16x8 b = ld_frag_T(X, k0, 16 * ct, lane);
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[j], 0, 0, 0);
       }
     }
     if (db) accb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ones, accb, 0, 0, 0);
   }
-  if (dW) {
+  if (dW && WG_ROWS2 && ld == 64 && nrows == 64 && ncols == 64) {
+    if constexpr (WG_ROWS2) flush_rows2(acc[0], acc[1], dW, rb, wg_ct(wave, 0), lane);
+  } else if (dW) {
 #pragma unroll
     for (int j = 0; j < NCT; ++j) {
-      const int bj = wave + NW * j, ct = bj >> 2;
+      const int ct = wg_ct(wave, j);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int n = 16 * rb + 4 * g + r, k = 16 * ct + c16;
-        const bool ok = bj < 16 && ct < nct && n < nrows && k < ncols;
+        const bool ok = wg_has(wave, j) && ct < nct && n < nrows && k < ncols;
         if (ok) WATOM(dW + n * ld + k, acc[j][r]);
       }
     }
@@ -467,16 +502,14 @@ __device__ __forceinline__ void wgrad64_shared_x(const bf16_t* const (&Y)[NM], c
   for (int k0 = 0; k0 < KP; k0 += 32) {
     bf16x8 xb[NCT];
 #pragma unroll
-    for (int j = 0; j < NCT; ++j) {
-      const int bj = wave + NW * j;
-      if (bj < 16) xb[j] = ld_frag_T(X, k0, 16 * (bj >> 2), lane);
-    }
+    for (int j = 0; j < NCT; ++j)
+      if (wg_has(wave, j)) xb[j] = ld_frag_T(X, k0, 16 * wg_ct(wave, j), lane);
 #pragma unroll
     for (int i = 0; i < NM; ++i) {
       const bf16x8 a = ld_frag_T(Y[i], k0, 16 * rb, lane);
 #pragma unroll
       for (int j = 0; j < NCT; ++j)
-        if (wave + NW * j < 16) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, xb[j], acc[i][j], 0, 0, 0);
+        if (wg_has(wave, j)) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, xb[j], acc[i][j], 0, 0, 0);
       if (bias) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ones, accb[i], 0, 0, 0);
     }
   }
@@ -485,12 +518,14 @@ __device__ __forceinline__ void wgrad64_shared_x(const bf16_t* const (&Y)[NM], c
     float* dW = c.g(m[i]->dW);
     float* db = c.g(m[i]->db);
     if (dW) {
+      if constexpr (WG_ROWS2) {
+        flush_rows2(acc[i][0], acc[i][1], dW, rb, wg_ct(wave, 0), lane);
+      } else {
 #pragma unroll
-      for (int j = 0; j < NCT; ++j) {
-        const int bj = wave + NW * j, ct = bj >> 2;
+        for (int j = 0; j < NCT; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (bj < 16) WATOM(dW + (16 * rb + 4 * g + r) * 64 + 16 * ct + c16, acc[i][j][r]);
+          for (int r = 0; r < 4; ++r)
+            if (wg_has(wave, j)) WATOM(dW + (16 * rb + 4 * g + r) * 64 + 16 * wg_ct(wave, j) + c16, acc[i][j][r]);
       }
     }
     if (bias && db && c16 < 4) {
