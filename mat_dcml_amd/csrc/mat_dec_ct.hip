@@ -89,8 +89,7 @@ __device__ __forceinline__ bool emb_tab_bwd_ok(const DecP& p) { return (p.A + 1)
 // array's address into a pointer select, which kept all of xr in scratch memory in the forward kernel)
 template <bool REG>
 __device__ __forceinline__ void cross_proj(const Mat* m, const CT* xr, const bf16_t* sv_x1_in, const float* rep,
-                                           bf16_t* sv_x1_out, const Ctx& c, bool store_xb = true,
-                                           const CTr* x1pre = nullptr) {
+                                           bf16_t* sv_x1_out, const Ctx& c, bool store_xb = true) {
   const int lane = c.lane;
   CTr xp[MAXRT], rp[MAXRT];
 #pragma unroll
@@ -99,7 +98,7 @@ __device__ __forceinline__ void cross_proj(const Mat* m, const CT* xr, const bf1
     if (rt < c.NT) {
       rp[k] = ct_pack(ld_gf(rep, c.tok0, rt, c.NR, lane));
       if constexpr (REG) xp[k] = ct_pack(xr[k]);
-      else xp[k] = x1pre ? x1pre[k] : ld_g(sv_x1_in, c.tok0, rt, c.NR, lane);
+      else xp[k] = ld_g(sv_x1_in, c.tok0, rt, c.NR, lane);
       if (sv_x1_out) st_g(sv_x1_out, c.tok0, rt, c.NR, xp[k], lane);
       if constexpr (!REG) { if (store_xb) st_lds(c.XB, rt, xp[k], tok_ok(rt, c), lane); }
     }
@@ -164,13 +163,11 @@ __device__ __forceinline__ void cross_attn_fwd_ct(const Mat* m, const LNp& ln, C
   }  CP_MARK(26);
 }
 
-// backward: dx (w.r.t. the sublayer output) -> d x1 (returned in dx); d rep accumulated into global drep.
-// in = a2, x1, x-hat, a2_lo, rstd (load_attn_in, issued by the previous sublayer); next = the self attention's
-// loads, issued between the closing weight-gradient MFMAs and their atomics (deferred flush, mat_train_ct.h)
-template <typename Next>
+// backward: dx (w.r.t. the sublayer output) -> d x1 (returned in dx); d rep accumulated into global drep
 __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, CT* dx, const float* rep, float* drep,
-                                                  const bf16_t* sv_x1, const AttnIn& in, const float* sv_lse,
-                                                  bool first, const Ctx& c, int vslot, Next&& next) {
+                                                  const bf16_t* sv_x1, const bf16_t* sv_a, const bf16_t* sv_alo,
+                                                  const float* sv_lse, const bf16_t* sv_xh, const float* sv_rs,
+                                                  bool first, const Ctx& c, int vslot) {
   const int lane = c.lane;
   const LseR lse = lse_fetch(sv_lse, c);   // consumed after the recompute phase (latency hidden by passes 1-2)
   CT dres[MAXRT];
@@ -180,15 +177,26 @@ __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, C
     ct_zero(dlb);
     {   // pass 1: LN backward from the saved x-hat / rstd -> ds ; DQ = dY of Wp, XB = X of Wp
       const CT gam = ld_vec(ln.g, lane);
+      CTr as[MAXRT], xhs[MAXRT];
+      float rsv[MAXRT];
+#pragma unroll
+      for (int k = 0; k < MAXRT; ++k) {
+        const int rt = c.wave + NW * k;
+        if (rt < c.NT) {
+          as[k] = ld_g(sv_a, c.tok0, rt, c.NR, lane);
+          xhs[k] = ld_g(sv_xh, c.tok0, rt, c.NR, lane);
+          rsv[k] = ld_tokf(sv_rs, rt, c);
+        }
+      }
 #pragma unroll
       for (int k = 0; k < MAXRT; ++k) {
         const int rt = c.wave + NW * k;
         if (rt < c.NT) {
           const bool ok = tok_ok(rt, c);
           CT ds;
-          ln_bwd_ct(dx[k], ct_unpack(in.xhs[k]), in.rsv[k], gam, ok, ds, dlg, dlb);
+          ln_bwd_ct(dx[k], ct_unpack(xhs[k]), rsv[k], gam, ok, ds, dlg, dlb);
           st_lds(c.DQ, rt, ct_pack(ds), ok, lane);   // dY of Wp
-          st_lds(c.XB, rt, in.as[k], ok, lane);      // X of Wp
+          st_lds(c.XB, rt, as[k], ok, lane);         // X of Wp
           dres[k] = ds;                              // residual path -> d rep
         }
       }
@@ -202,13 +210,14 @@ __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, C
       for (int k = 0; k < MAXRT; ++k) {
         const int rt = c.wave + NW * k;
         if (rt < c.NT) {
+          const CTr alo = ld_g(sv_alo, c.tok0, rt, c.NR, lane);
           CT da;
           ct_zero(da);
           mm(da, Wpb, ld_lds(c.DQ, rt, lane));
           const bool ok = tok_ok(rt, c);
           const CTr dap = ct_pack(da);
           st_lds(c.DA, rt, dap, ok, lane);
-          attn_delta_ct(ld_lds(c.XB, rt, lane), in.alo[k], dap, rt, ok, c);
+          attn_delta_ct(ld_lds(c.XB, rt, lane), alo, dap, rt, ok, c);
         }
       }
     }
@@ -217,7 +226,7 @@ __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, C
   CP_MARK(4);
   // q / k / v recompute (writes QB / KB / VB only; x1 goes to XB later) before the Wp weight gradient (reads DQ / XB):
   // its atomics drain under the attention, one barrier fewer
-  cross_proj<false>(m, nullptr, sv_x1, rep, nullptr, c, false, in.xin);
+  cross_proj<false>(m, nullptr, sv_x1, rep, nullptr, c, false);
   wgrad64(c.DQ, c.XB, m[7], c);
   lse_store(lse, c);
   __syncthreads();
@@ -271,14 +280,11 @@ __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, C
   }
   __syncthreads();
   CP_MARK(9);
+  wgrad64(c.DQ, c.QB, m[4], c);
   {
-    const WgAcc<1> aq = wgrad64_acc(c.DQ, c.QB, m[4], c);
     const bf16_t* const ys[2] = {c.KB, c.VB};
     const Mat* const ms[2] = {&m[5], &m[6]};
-    const WgAcc<2> akv = wgrad64x_acc<2>(ys, c.XB, c);
-    next();   // the self attention's inputs: older than the atomics below
-    wgrad64_flush(aq, m[4], c);
-    wgrad64x_flush<2>(akv, ms, c);
+    wgrad64_shared_x<2>(ys, c.XB, ms, c);
   }
   __syncthreads();
   CP_MARK(10);
@@ -464,8 +470,8 @@ __device__ __forceinline__ void head_fwd_ct(const DecP& p, const CT* xr, bool sa
   }
 }
 
-template <int MA, bool CONT, typename Next>
-__device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c, Next&& next) {
+template <int MA, bool CONT>
+__device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c) {
   const int lane = c.lane, g = lane >> 4;
   constexpr int SB = (MA + 1) / 2;   // k-steps over the logit axis in dn = W_h2ᵀ dz
   CT dlg, dlb;
@@ -634,16 +640,8 @@ __device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c,
   }
   __syncthreads();
   CP_MARK(1);
-  {
-    const bf16_t* const y2[1] = {c.DA};
-    const WgAcc<1> a2 = wgrad_acc<1>(y2, c.XB, 4, p.d_bh2 != nullptr, p.A, c);   // W_h2 (A x 64) and b_h2
-    const WgAcc<1> a1 = wgrad64_acc(c.DQ, c.KB, p.h1, c);
-    next();   // the last block's MLP inputs: older than the atomics below
-    float* const w2[1] = {c.g(p.d_wh2)};
-    float* const b2[1] = {c.g(p.d_bh2)};
-    wgrad_flush<1>(a2, w2, b2, 64, p.A, 64, c);
-    wgrad64_flush(a1, p.h1, c);
-  }
+  wgrad_g(c.DA, c.XB, c.KP, c.g(p.d_wh2), 64, p.A, 64, c.g(p.d_bh2), c.wave, lane);
+  wgrad64(c.DQ, c.KB, p.h1, c);
   __syncthreads();
   CP_MARK(19);
 }
@@ -721,31 +719,20 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
   CP_MARK(0);
   const int lane = c.lane;
   CT dx[MAXRT];
-  const size_t BL = (size_t)p.Bs * p.L;
-  MlpIn mi;
-  AttnIn ai;
-  head_bwd_ct<MA, CONT>(p, dx, c, [&] {
-    const Sv& t = p.sv[NB - 1];
-    load_mlp_in(mi, t.x2, t.g, t.gp, t.xh[2], t.rs + 2 * BL, c);
-  });
-  // parameter-vector slots (vacc): 0-1 head LayerNorm, 2-3 embedding LayerNorm, 4 log_std, 5 + 6 bb + 2 k the
-  // block's k-th LayerNorm (gamma, beta)
+  head_bwd_ct<MA, CONT>(p, dx, c);
 #pragma unroll 1
   for (int bb = NB - 1; bb >= 0; --bb) {
     const Blk& B = p.blk[bb];
-    const Sv& t = p.sv[bb];
     Ctx cc = c;
     asm volatile("" : "+v"(cc.lane), "+v"(cc.tid));
-    mlp_bwd_ct(B.m[8], B.m[9], B.ln[2], dx, mi, cc, 9 + 6 * bb,
-               [&] { load_attn_in(ai, t.a2, t.x1, t.a2lo, t.xh[1], t.rs + 1 * BL, cc); });
-    cross_attn_bwd_ct(B.m, B.ln[1], dx, p.rep, p.drep, t.x1, ai, t.lse2, bb == NB - 1, cc, 7 + 6 * bb,
-                      [&] { load_attn_in(ai, t.a1, t.xin, t.a1lo, t.xh[0], t.rs, cc); });
-    self_attn_bwd_ct(B.m, B.ln[0], dx, ai, t.lse1, true, cc, 5 + 6 * bb, [&] {
-      // unconditional (block 0 reloads its own, unused): a skipped load would merge with the previous contents
-      // and keep the whole struct live around the block loop
-      const Sv& u = p.sv[bb > 0 ? bb - 1 : 0];
-      load_mlp_in(mi, u.x2, u.g, u.gp, u.xh[2], u.rs + 2 * BL, cc);
-    });
+    // parameter-vector slots (vacc): 0-1 head LayerNorm, 2-3 embedding LayerNorm, 4 log_std, 5 + 6 bb + 2 k the
+    // block's k-th LayerNorm (gamma, beta)
+    mlp_bwd_ct(B.m[8], B.m[9], B.ln[2], dx, p.sv[bb].x2, p.sv[bb].g, p.sv[bb].gp, p.sv[bb].xh[2], p.sv[bb].rs + 2 * (size_t)p.Bs * p.L, cc,
+               9 + 6 * bb);
+    cross_attn_bwd_ct(B.m, B.ln[1], dx, p.rep, p.drep, p.sv[bb].x1, p.sv[bb].a2, p.sv[bb].a2lo, p.sv[bb].lse2,
+                      p.sv[bb].xh[1], p.sv[bb].rs + 1 * (size_t)p.Bs * p.L, bb == NB - 1, cc, 7 + 6 * bb);
+    self_attn_bwd_ct(B.m, B.ln[0], dx, p.sv[bb].xin, p.sv[bb].a1, p.sv[bb].a1lo, p.sv[bb].lse1, p.sv[bb].xh[0],
+                     p.sv[bb].rs + 0 * (size_t)p.Bs * p.L, true, cc, 5 + 6 * bb);
   }
   // ---------------- embedding backward: dW_a[:, token] += d pre ; LN_dec params
   if (!CONT) {
@@ -806,8 +793,8 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
     flush_vec(dlb, c.g(p.d_lnd_b), 3, c);
     __syncthreads();
     if (p.d_wa) {
-      wgrad_g(c.DA, c.XB, c, c.g(p.d_wa), p.A + 1, 64, p.A + 1, nullptr);
-      wgrad_g(c.DQ, c.XB, c, c.g(p.d_wa), p.A + 1, 64, p.A + 1, nullptr);
+      wgrad_g(c.DA, c.XB, c.KP, c.g(p.d_wa), p.A + 1, 64, p.A + 1, nullptr, c.wave, lane);
+      wgrad_g(c.DQ, c.XB, c.KP, c.g(p.d_wa), p.A + 1, 64, p.A + 1, nullptr, c.wave, lane);
     }
   } else {
     float* EMB = (float*)c.QB;   // [(A+1)][64] f32 accumulators (QB + KB: 2 NRP x 128 B >= 65 x 256 B)

@@ -205,9 +205,6 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
   CP_MARK(0);
   const int lane = c.lane;
   CT dx[MAXRT];
-  const size_t BL = (size_t)p.Bs * p.L;
-  MlpIn mi;
-  AttnIn ai;
   // ---------------- value head backward (+ incoming d rep from the decoder)
   {
     CT dlg, dlb, dw0, dw1;
@@ -296,12 +293,7 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
       }
     }
     __syncthreads();
-    {
-      const WgAcc<1> a1 = wgrad64_acc(c.DQ, c.XB, p.h1, c);
-      const Sv& t = p.sv[NB - 1];   // the last block's MLP inputs: older than the atomics below (deferred flush)
-      load_mlp_in(mi, t.x1, t.g, t.gp, t.xh[1], t.rs + 1 * BL, c);
-      wgrad64_flush(a1, p.h1, c);
-    }
+    wgrad64(c.DQ, c.XB, p.h1, c);
     __syncthreads();
     CP_MARK(1);
   }
@@ -311,17 +303,10 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
     const Blk& B = p.blk[bb];
     Ctx cc = c;
     asm volatile("" : "+v"(cc.lane), "+v"(cc.tid));
-    const Sv& t = p.sv[bb];
-    mlp_bwd_ct(B.m[8], B.m[9], B.ln[1], dx, mi, cc, 12 + 4 * bb,
-               [&] { load_attn_in(ai, t.a1, t.xin, t.a1lo, t.xh[0], t.rs, cc); });
-    self_attn_bwd_ct(B.m, B.ln[0], dx, ai, t.lse1, false, cc, 10 + 4 * bb, [&] {
-      // the next block's MLP inputs, or (block 0) the embedding's saved x-hat / GELU' / rstd in the same slots —
-      // one unconditional load of selected sources (a skipped load would keep the struct live around the loop)
-      const bool emb = bb == 0;
-      const Sv& u = p.sv[emb ? 0 : bb - 1];
-      load_mlp_in(mi, emb ? p.es.xh : u.x1, emb ? p.es.gp : u.g, emb ? p.es.gp : u.gp, emb ? p.es.xh : u.xh[1],
-                  emb ? p.es.rs : u.rs + 1 * BL, cc);
-    });
+    mlp_bwd_ct(B.m[8], B.m[9], B.ln[1], dx, p.sv[bb].x1, p.sv[bb].g, p.sv[bb].gp, p.sv[bb].xh[1], p.sv[bb].rs + 1 * (size_t)p.Bs * p.L, cc,
+               12 + 4 * bb);
+    self_attn_bwd_ct(B.m, B.ln[0], dx, p.sv[bb].xin, p.sv[bb].a1, p.sv[bb].a1lo, p.sv[bb].lse1, p.sv[bb].xh[0],
+                     p.sv[bb].rs + 0 * (size_t)p.Bs * p.L, false, cc, 10 + 4 * bb);
   }
   // ---------------- embedding backward: x0 = LN0(GELU(pre)), pre = W_e · LN_obs(obs) + b_e
   {
@@ -341,9 +326,9 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
         float oh[4] = {0.f, 0.f, 0.f, 0.f}, hat[4] = {0.f, 0.f, 0.f, 0.f};
         if (!ex.pre_in) obs_ln(p, rt, c, oh, hat);   // X of W_e and the LN_obs backward (od <= 16 dims in-lane)
         // the forward's x-hat, GELU'(pre) and rstd (no embedding product, GELU or LayerNorm forward here)
-        const CT xh = ct_unpack(mi.xhs[k]), egp = ct_unpack(mi.gps[k]);   // loaded in the last block's hook
+        const CT xh = ct_unpack(ld_g(p.es.xh, c.tok0, rt, c.NR, lane)), egp = ct_unpack(ld_g(p.es.gp, c.tok0, rt, c.NR, lane));
         CT de;
-        ln_bwd_ct(dx[k], xh, mi.rsv[k], gam, ok, de, dlg, dlb);
+        ln_bwd_ct(dx[k], xh, ld_tokf(p.es.rs, rt, c), gam, ok, de, dlg, dlb);
 #pragma unroll
         for (int i = 0; i < 4; ++i) de.v[i] *= egp.v[i];   // padded rows: zero
         if (ex.pre_in) {
@@ -390,7 +375,7 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
         if (p.d_lno_b) vacc_add(c.g(p.d_lno_b), 9, dim, ob, c);
       }
       __syncthreads();
-      wgrad_g(c.DA, c.XB, c, c.g(p.d_we), p.od, 64, p.od, nullptr);
+      wgrad_g(c.DA, c.XB, c.KP, c.g(p.d_we), p.od, 64, p.od, nullptr, c.wave, lane);
     }
   }
   CP_MARK(30);

@@ -18,8 +18,7 @@ __host__ __device__ inline size_t mat_train_lds_main_bytes(int NRP) {
   const size_t aux = (size_t)NRP * 2 * 4 * 2;   // LSE / delta [2][NRP] f32 (also the decoder's embedding-grad scratch)
   return (size_t)NRP * 64 * 2 * 6 + (aux < 9 * 64 * 4 ? 9 * 64 * 4 : aux);
 }
-// Behind the token buffers (NRP <= 192: 150.5 KB + 7.3 KB < 160 KB):
-//  * 1 KB landing area of the saved-activation L2 prefetches (contents never read; every wave's DMA lands there);
+// Behind the token buffers (NRP <= 192: 150.5 KB + 6.2 KB < 160 KB):
 //  * the per-workgroup parameter-vector accumulators (VSLOTS x 64 f32) and their global destinations (VSLOTS
 //    pointers): LayerNorm / bias / log-std gradient partials are summed here with LDS atomics across ALL of the
 //    workgroup's chunks and leave by global fp32 atomics once, at the end of the launch.  A global atomic sits in
@@ -27,7 +26,7 @@ __host__ __device__ inline size_t mat_train_lds_main_bytes(int NRP) {
 //    next phase's saved-activation loads wait for it (~16 such stalls per chunk).
 constexpr int VSLOTS = 24;
 __host__ __device__ inline size_t mat_train_lds_bytes(int NRP, int SQ, int L) {
-  return mat_train_lds_main_bytes(NRP) + 1024 + (size_t)VSLOTS * (64 * 4 + 8);
+  return mat_train_lds_main_bytes(NRP) + (size_t)VSLOTS * (64 * 4 + 8);
 }
 
 namespace {
@@ -126,7 +125,6 @@ struct Ctx {
   __device__ __forceinline__ float* g(float* p) const { return p ? p + gofs : p; }
   bf16_t *QB, *KB, *VB, *DA, *DQ, *XB;
   float *LSE, *DEL;
-  char* PF;     // the 1 KB LDS landing area of the L2 prefetches (contents never read)
   float* VACC;  // [VSLOTS][64] parameter-vector gradient accumulators (LDS, per workgroup, all chunks)
   float** VPT;  // [VSLOTS] their global destinations (null = unused slot)
 };
@@ -255,8 +253,7 @@ __device__ __forceinline__ Ctx make_ctx(const PT& p, char* smem, int seq0, int n
   c.QB = base; c.KB = base + bs; c.VB = base + 2 * bs; c.DA = base + 3 * bs; c.DQ = base + 4 * bs; c.XB = base + 5 * bs;
   c.LSE = (float*)(base + 6 * bs);
   c.DEL = c.LSE + 2 * p.NRP;
-  c.PF = smem + mat_train_lds_main_bytes(p.NRP);
-  c.VACC = (float*)(c.PF + 1024);
+  c.VACC = (float*)(smem + mat_train_lds_main_bytes(p.NRP));
   c.VPT = (float**)(c.VACC + VSLOTS * 64);
   return c;
 }
@@ -264,7 +261,7 @@ __device__ __forceinline__ Ctx make_ctx(const PT& p, char* smem, int seq0, int n
 // parameter-vector accumulators: zeroed before a workgroup's first chunk, flushed after its last (backward kernels)
 template <typename PT>
 __device__ __forceinline__ void vacc_begin(const PT& p, char* smem) {
-  float* V = (float*)(smem + mat_train_lds_main_bytes(p.NRP) + 1024);
+  float* V = (float*)(smem + mat_train_lds_main_bytes(p.NRP));
   float** P = (float**)(V + VSLOTS * 64);
   for (int i = threadIdx.x; i < VSLOTS * 64; i += NTHR) V[i] = 0.f;
   for (int i = threadIdx.x; i < VSLOTS; i += NTHR) P[i] = nullptr;
@@ -273,7 +270,7 @@ __device__ __forceinline__ void vacc_begin(const PT& p, char* smem) {
 template <typename PT>
 __device__ __forceinline__ void vacc_end(const PT& p, char* smem) {
   __syncthreads();
-  const float* V = (const float*)(smem + mat_train_lds_main_bytes(p.NRP) + 1024);
+  const float* V = (const float*)(smem + mat_train_lds_main_bytes(p.NRP));
   float* const* P = (float* const*)(V + VSLOTS * 64);
   for (int i = threadIdx.x; i < VSLOTS * 64; i += NTHR) {
     float* d = P[i >> 6];

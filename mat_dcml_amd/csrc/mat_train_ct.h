@@ -225,9 +225,16 @@ __device__ __forceinline__ CTr ld_g(const bf16_t* src, int tok0, int rt, int NR,
   x.q[3] = ok ? make_uint2(b.z, b.w) : make_uint2(0u, 0u);
   return x;
 }
+// A/B ablation (-DMDL_ABLATE_SAVES, forward TUs): the saved-activation stores are skipped (a runtime-false predicate)
+// — prices the forward's store traffic and the vmcnt waits of the loads queued behind it.  Never shipped.
+#ifdef MDL_ABLATE_SAVES
+#define SAVE_ON(row, NR) ((row) < (NR) && (NR) < 0)
+#else
+#define SAVE_ON(row, NR) ((row) < (NR))
+#endif
 __device__ __forceinline__ void st_g(bf16_t* dst, int tok0, int rt, int NR, const CTr& x, int lane) {
   const int g = lane >> 4, row = rt * 16 + (lane & 15);
-  if (row < NR) {
+  if (SAVE_ON(row, NR)) {
     uint4* base = (uint4*)(dst + (size_t)(tok0 + row) * 64 + 16 * g);
     base[0] = make_uint4(x.q[0].x, x.q[0].y, x.q[1].x, x.q[1].y);
     base[1] = make_uint4(x.q[2].x, x.q[2].y, x.q[3].x, x.q[3].y);
@@ -260,7 +267,7 @@ __device__ __forceinline__ void st_gf(float* dst, int tok0, int rt, int NR, cons
 // consecutive tokens)
 __device__ __forceinline__ void st_tokf(float* dst, int rt, float v, const Ctx& c) {
   const int row = rt * 16 + (c.lane & 15);
-  if ((c.lane >> 4) == 0 && row < c.NR) dst[(size_t)(c.tok0 + row)] = v;
+  if ((c.lane >> 4) == 0 && SAVE_ON(row, c.NR)) dst[(size_t)(c.tok0 + row)] = v;
 }
 __device__ __forceinline__ float ld_tokf(const float* src, int rt, const Ctx& c) {
   const int row = rt * 16 + (c.lane & 15);
@@ -426,125 +433,120 @@ __device__ __forceinline__ void flush_rows2(const f32x4& acc0, const f32x4& acc1
   }
 }
 // dW[n][k] (row stride ld) += Σ_t Y[t][n] X[t][k] for n < nrows, k < ncols, and db[n] += Σ_t Y[t][n], from
-// token-major swizzled LDS tiles of KP rows (KP % 32 == 0, padded rows zero).  Wave w owns row block w & 3 and the
-// column tiles wg_ct(w, j) (8 waves: two adjacent ones), so its blocks share one Y fragment per k-step.  The bias
-// gradient is one extra MFMA per k-step against a ones fragment (waves 0-3).  Split in two: wgrad_acc runs the
-// MFMAs, wgrad_flush issues the fp32 atomics — a sublayer issues the NEXT sublayer's saved-activation loads in
-// between (deferred flush), so those loads are older than the atomics in the wave's in-order vmcnt queue and their
-// waits never include an atomic's ~3,000-cycle round trip.
-constexpr int WG_NCT = (16 + NW - 1) / NW;   // column tiles per wave (at most)
-template <int NM>
-struct WgAcc { f32x4 acc[NM][WG_NCT]; f32x4 accb[NM]; };
-
-template <int NM>
-__device__ __forceinline__ WgAcc<NM> wgrad_acc(const bf16_t* const (&Y)[NM], const bf16_t* X, int nct, bool bias,
-                                               int nrows, const Ctx& c) {
+// token-major swizzled LDS tiles of KP rows (KP % 32 == 0, padded rows zero).  The 16 output blocks (row block
+// j & 3, column tile j >> 2) are dealt round robin, j = wave + NW i: a wave's blocks share one row block (NW % 4 == 0)
+// and so one Y fragment per k-step.  The bias gradient is one extra MFMA per k-step against a ones fragment (the
+// waves holding column tile 0).  fp32 atomics.
+__device__ __forceinline__ void wgrad_g(const bf16_t* Y, const bf16_t* X, int KP, float* dW, int ld, int nrows, int ncols,
+                                        float* db, int wave, int lane) {
   static_assert(NW % 4 == 0, "row block per wave");
-  const int wave = c.wave, lane = c.lane, KP = c.KP;
+  constexpr int NCT = (16 + NW - 1) / NW;           // column tiles per wave (at most)
   const int rb = wave & 3;
-  bias = bias && wave < 4;
-  WgAcc<NM> a;
+  if (wave >= 4) db = nullptr;
+  const int nct = dW ? (ncols + 15) >> 4 : 0;
+  if ((!db && wg_ct(wave, 0) >= nct) || 16 * rb >= nrows) return;
+  const int g = lane >> 4, c16 = lane & 15;
+  f32x4 acc[NCT];
 #pragma unroll
-  for (int i = 0; i < NM; ++i) {
-    a.accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < WG_NCT; ++j) a.acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  if ((!bias && wg_ct(wave, 0) >= nct) || 16 * rb >= nrows) return a;
+  for (int j = 0; j < NCT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 accb = {0.f, 0.f, 0.f, 0.f};
   const bf16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
   for (int k0 = 0; k0 < KP; k0 += 32) {
-    bf16x8 xb[WG_NCT];
+    const bf16x8 a = ld_frag_T(Y, k0, 16 * rb, lane);
 #pragma unroll
-    for (int j = 0; j < WG_NCT; ++j)
-      if (wg_has(wave, j) && wg_ct(wave, j) < nct) xb[j] = ld_frag_T(X, k0, 16 * wg_ct(wave, j), lane);
-#pragma unroll
-    for (int i = 0; i < NM; ++i) {
-      const bf16x8 y = ld_frag_T(Y[i], k0, 16 * rb, lane);
-#pragma unroll
-      for (int j = 0; j < WG_NCT; ++j)
-        if (wg_has(wave, j) && wg_ct(wave, j) < nct)
-          a.acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(y, xb[j], a.acc[i][j], 0, 0, 0);
-      if (bias) a.accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(y, ones, a.accb[i], 0, 0, 0);
-    }
-  }
-  return a;
-}
-
-// dW_i (already offset to this block's gradient copy, row stride ld, nrows x ncols valid) and db_i (or null)
-template <int NM>
-__device__ __forceinline__ void wgrad_flush(const WgAcc<NM>& a, float* const (&dW)[NM], float* const (&db)[NM], int ld,
-                                            int nrows, int ncols, const Ctx& c) {
-  const int wave = c.wave, lane = c.lane, rb = wave & 3, g = lane >> 4, c16 = lane & 15;
-  const int nct = (ncols + 15) >> 4;
-#pragma unroll
-  for (int i = 0; i < NM; ++i) {
-    if (dW[i] && 16 * rb < nrows) {
-      if (WG_ROWS2 && ld == 64 && nrows == 64 && ncols == 64) {
-        if constexpr (WG_ROWS2) flush_rows2(a.acc[i][0], a.acc[i][1], dW[i], rb, wg_ct(wave, 0), lane);
-      } else {
-#pragma unroll
-        for (int j = 0; j < WG_NCT; ++j) {
-          const int ct = wg_ct(wave, j);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int n = 16 * rb + 4 * g + r, k = 16 * ct + c16;
-            if (wg_has(wave, j) && ct < nct && n < nrows && k < ncols) WATOM(dW[i] + n * ld + k, a.acc[i][j][r]);
-          }
-        }
+    for (int j = 0; j < NCT; ++j) {
+      const int ct = wg_ct(wave, j);
+      if (wg_has(wave, j) && ct < nct) {
+        const bf16x8 b = ld_frag_T(X, k0, 16 * ct, lane);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[j], 0, 0, 0);
       }
     }
-    if (db[i] && wave < 4 && c16 < 4) {
-      const float v = c16 == 0 ? a.accb[i][0] : c16 == 1 ? a.accb[i][1] : c16 == 2 ? a.accb[i][2] : a.accb[i][3];
-      const int n = 16 * rb + 4 * g + c16;
-      if (n < nrows) atomicAdd(db[i] + n, v);
+    if (db) accb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ones, accb, 0, 0, 0);
+  }
+  if (dW && WG_ROWS2 && ld == 64 && nrows == 64 && ncols == 64) {
+    if constexpr (WG_ROWS2) flush_rows2(acc[0], acc[1], dW, rb, wg_ct(wave, 0), lane);
+  } else if (dW) {
+#pragma unroll
+    for (int j = 0; j < NCT; ++j) {
+      const int ct = wg_ct(wave, j);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = 16 * rb + 4 * g + r, k = 16 * ct + c16;
+        const bool ok = wg_has(wave, j) && ct < nct && n < nrows && k < ncols;
+        if (ok) WATOM(dW + n * ld + k, acc[j][r]);
+      }
     }
   }
-}
-
-__device__ __forceinline__ void wgrad_g(const bf16_t* Y, const bf16_t* X, const Ctx& c, float* dW, int ld, int nrows,
-                                        int ncols, float* db) {
-  const bf16_t* const ys[1] = {Y};
-  const WgAcc<1> a = wgrad_acc<1>(ys, X, dW ? (ncols + 15) >> 4 : 0, db != nullptr, nrows, c);
-  float* const w[1] = {dW};
-  float* const b[1] = {db};
-  wgrad_flush<1>(a, w, b, ld, nrows, ncols, c);
-}
-__device__ __forceinline__ WgAcc<1> wgrad64_acc(const bf16_t* Y, const bf16_t* X, const Mat& m, const Ctx& c) {
-  const bf16_t* const ys[1] = {Y};
-  return wgrad_acc<1>(ys, X, 4, m.db != nullptr, 64, c);
-}
-__device__ __forceinline__ void wgrad64_flush(const WgAcc<1>& a, const Mat& m, const Ctx& c) {
-  float* const w[1] = {c.g(m.dW)};
-  float* const b[1] = {c.g(m.db)};
-  wgrad_flush<1>(a, w, b, 64, 64, 64, c);
+  if (db && c16 < 4) {
+    const float v = c16 == 0 ? accb[0] : c16 == 1 ? accb[1] : c16 == 2 ? accb[2] : accb[3];
+    const int n = 16 * rb + 4 * g + c16;
+    if (n < nrows) atomicAdd(db + n, v);
+  }
 }
 __device__ __forceinline__ void wgrad64(const bf16_t* Y, const bf16_t* X, const Mat& m, const Ctx& c) {
-  wgrad64_flush(wgrad64_acc(Y, X, m, c), m, c);
+  wgrad_g(Y, X, c.KP, c.g(m.dW), 64, 64, 64, c.g(m.db), c.wave, c.lane);
 }
 
 // The weight gradients of TWO or THREE 64x64 matrices that share their input X (dW_q / dW_k / dW_v of an attention,
-// dW_k / dW_v of the cross attention): one pass over the token axis reads each X fragment once for all of them.
-template <int NM>
-__device__ __forceinline__ WgAcc<NM> wgrad64x_acc(const bf16_t* const (&Y)[NM], const bf16_t* X, const Ctx& c) {
-  return wgrad_acc<NM>(Y, X, 4, true, 64, c);
-}
-template <int NM>
-__device__ __forceinline__ void wgrad64x_flush(const WgAcc<NM>& a, const Mat* const (&m)[NM], const Ctx& c) {
-  float* w[NM];
-  float* b[NM];
-#pragma unroll
-  for (int i = 0; i < NM; ++i) {
-    w[i] = c.g(m[i]->dW);
-    b[i] = c.g(m[i]->db);
-  }
-  float* const (&wc)[NM] = w;
-  float* const (&bc)[NM] = b;
-  wgrad_flush<NM>(a, wc, bc, 64, 64, 64, c);
-}
+// dW_k / dW_v of the cross attention): one pass over the token axis reads each X fragment once for all of them
+// (wgrad64 per matrix re-read X: 6 transposed LDS reads per 2 MFMAs; here 2 + 2 NM per 2 NM).
 template <int NM>
 __device__ __forceinline__ void wgrad64_shared_x(const bf16_t* const (&Y)[NM], const bf16_t* X, const Mat* const (&m)[NM],
                                                  const Ctx& c) {
-  wgrad64x_flush<NM>(wgrad64x_acc<NM>(Y, X, c), m, c);
+#ifdef MDL_WG_SEQ
+  // A/B: one matrix at a time (its atomics issued before the next matrix's MFMAs: bursts of 8, not 8 NM)
+#pragma unroll
+  for (int i = 0; i < NM; ++i) wgrad64(Y[i], X, *m[i], c);
+  return;
+#endif
+  static_assert(NW % 4 == 0, "row block per wave");
+  constexpr int NCT = (16 + NW - 1) / NW;
+  const int wave = c.wave, lane = c.lane, KP = c.KP;
+  const int rb = wave & 3;
+  const bool bias = wave < 4;
+  const int g = lane >> 4, c16 = lane & 15;
+  f32x4 acc[NM][NCT], accb[NM];
+#pragma unroll
+  for (int i = 0; i < NM; ++i) {
+    accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < NCT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const bf16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
+  for (int k0 = 0; k0 < KP; k0 += 32) {
+    bf16x8 xb[NCT];
+#pragma unroll
+    for (int j = 0; j < NCT; ++j)
+      if (wg_has(wave, j)) xb[j] = ld_frag_T(X, k0, 16 * wg_ct(wave, j), lane);
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+      const bf16x8 a = ld_frag_T(Y[i], k0, 16 * rb, lane);
+#pragma unroll
+      for (int j = 0; j < NCT; ++j)
+        if (wg_has(wave, j)) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, xb[j], acc[i][j], 0, 0, 0);
+      if (bias) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ones, accb[i], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NM; ++i) {
+    float* dW = c.g(m[i]->dW);
+    float* db = c.g(m[i]->db);
+    if (dW) {
+      if constexpr (WG_ROWS2) {
+        flush_rows2(acc[i][0], acc[i][1], dW, rb, wg_ct(wave, 0), lane);
+      } else {
+#pragma unroll
+        for (int j = 0; j < NCT; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (wg_has(wave, j)) WATOM(dW + (16 * rb + 4 * g + r) * 64 + 16 * wg_ct(wave, j) + c16, acc[i][j][r]);
+      }
+    }
+    if (bias && db && c16 < 4) {
+      const float v = c16 == 0 ? accb[i][0] : c16 == 1 ? accb[i][1] : c16 == 2 ? accb[i][2] : accb[i][3];
+      atomicAdd(db + 16 * rb + 4 * g + c16, v);
+    }
+  }
 }
 
 // q / k / v projections of the packed tiles xp (one weight matrix live at a time) -> QB / KB / VB; m0 = index of
@@ -900,62 +902,38 @@ __device__ __forceinline__ void mlp_fwd_ct(const Mat& m1, const Mat& m2, const L
 // Backward sublayers run in passes with ONE weight matrix live at a time (the 8-wave backward keeps every wave
 // under 256 registers): each pass leaves its per-tile products in this wave's own LDS rows (read back by the same
 // lanes, so no barrier between passes) or in dx.
-//
-// Deferred flush: a sublayer's saved-activation inputs (the *In structs) are loaded by the PREVIOUS sublayer, inside
-// its closing weight-gradient phase, after the MFMAs and BEFORE its fp32 atomics (the `next` hook).  A wave's vmcnt
-// queue completes in issue order, so loads issued after the atomics had to wait for them (~3,000 cycles under
-// load) — every sublayer started with that stall.  Issued before, they also overlap the previous phase's barrier.
-struct MlpIn { CTr xs[MAXRT], hs[MAXRT], xhs[MAXRT], gps[MAXRT]; float rsv[MAXRT]; };   // x, GELU(h), x-hat, GELU'(h), rstd
-struct AttnIn { CTr as[MAXRT], xin[MAXRT], xhs[MAXRT], alo[MAXRT]; float rsv[MAXRT]; };  // a, x (self only), x-hat, a_lo, rstd
-
-// Every field is written, tiles past NT included (ld_g / ld_tokf read rows >= NR as zero): a conditional write would
-// merge with the struct's previous contents and keep all of it live across every phase (hipcc spilled 500 B / lane).
-__device__ __forceinline__ void load_mlp_in(MlpIn& in, const bf16_t* sv_x, const bf16_t* sv_g, const bf16_t* sv_gp,
-                                            const bf16_t* sv_xh, const float* sv_rs, const Ctx& c) {
-#pragma unroll
-  for (int k = 0; k < MAXRT; ++k) {
-    const int rt = c.wave + NW * k;
-    in.xs[k] = ld_g(sv_x, c.tok0, rt, c.NR, c.lane);
-    in.hs[k] = ld_g(sv_g, c.tok0, rt, c.NR, c.lane);
-    in.xhs[k] = ld_g(sv_xh, c.tok0, rt, c.NR, c.lane);
-    in.gps[k] = ld_g(sv_gp, c.tok0, rt, c.NR, c.lane);
-    in.rsv[k] = ld_tokf(sv_rs, rt, c);
-  }
-}
-// cross attention: sv_xin = x1 (its k / v input; its q input is rep)
-__device__ __forceinline__ void load_attn_in(AttnIn& in, const bf16_t* sv_a, const bf16_t* sv_xin, const bf16_t* sv_alo,
-                                             const bf16_t* sv_xh, const float* sv_rs, const Ctx& c) {
-#pragma unroll
-  for (int k = 0; k < MAXRT; ++k) {
-    const int rt = c.wave + NW * k;
-    in.as[k] = ld_g(sv_a, c.tok0, rt, c.NR, c.lane);
-    in.xin[k] = ld_g(sv_xin, c.tok0, rt, c.NR, c.lane);
-    in.xhs[k] = ld_g(sv_xh, c.tok0, rt, c.NR, c.lane);
-    in.alo[k] = ld_g(sv_alo, c.tok0, rt, c.NR, c.lane);
-    in.rsv[k] = ld_tokf(sv_rs, rt, c);
-  }
-}
-struct NoNext { __device__ __forceinline__ void operator()() const {} };
-
-template <typename Next>
-__device__ __forceinline__ void mlp_bwd_ct(const Mat& m1, const Mat& m2, const LNp& ln, CT* dx, const MlpIn& in,
-                                           const Ctx& c, int vslot, Next&& next) {
+__device__ __forceinline__ void mlp_bwd_ct(const Mat& m1, const Mat& m2, const LNp& ln, CT* dx, const bf16_t* sv_x,
+                                           const bf16_t* sv_g, const bf16_t* sv_gp, const bf16_t* sv_xh,
+                                           const float* sv_rs, const Ctx& c, int vslot) {
   const int lane = c.lane;
   {   // pass 1: LN backward from the saved x-hat / rstd -> ds (dx) ; DA = dY of W2, XB = X of W2 (GELU(h))
     CT dlg, dlb;
     ct_zero(dlg);
     ct_zero(dlb);
     const CT gam = ld_vec(ln.g, lane);
+    CTr xs[MAXRT], hs[MAXRT], xhs[MAXRT];
+    float rsv[MAXRT];
+#pragma unroll
+    for (int k = 0; k < MAXRT; ++k) {   // every saved-activation load of the wave issued up front
+      const int rt = c.wave + NW * k;
+      if (rt < c.NT) {
+        xs[k] = ld_g(sv_x, c.tok0, rt, c.NR, lane);
+        hs[k] = ld_g(sv_g, c.tok0, rt, c.NR, lane);
+        xhs[k] = ld_g(sv_xh, c.tok0, rt, c.NR, lane);
+        rsv[k] = ld_tokf(sv_rs, rt, c);
+      }
+    }
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
       const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         const bool ok = tok_ok(rt, c);
+        const CTr glr = hs[k];   // GELU(h): the forward's own W2 operand
         CT ds;
-        ln_bwd_ct(dx[k], ct_unpack(in.xhs[k]), in.rsv[k], gam, ok, ds, dlg, dlb);
+        ln_bwd_ct(dx[k], ct_unpack(xhs[k]), rsv[k], gam, ok, ds, dlg, dlb);
         st_lds(c.DA, rt, ct_pack(ds), ok, lane);   // dY of W2
-        st_lds(c.XB, rt, in.hs[k], ok, lane);      // X of W2 (GELU(h): the forward's own W2 operand)
-        st_lds(c.QB, rt, in.xs[k], ok, lane);      // X of W1
+        st_lds(c.XB, rt, glr, ok, lane);           // X of W2
+        st_lds(c.QB, rt, xs[k], ok, lane);         // X of W1
         dx[k] = ds;                                // residual path
       }
     }
@@ -970,7 +948,7 @@ __device__ __forceinline__ void mlp_bwd_ct(const Mat& m1, const Mat& m2, const L
       const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         const bool ok = tok_ok(rt, c);
-        const CT gp = ct_unpack(in.gps[k]);   // GELU'(h), saved by the forward
+        const CT gp = ct_unpack(ld_g(sv_gp, c.tok0, rt, c.NR, lane));   // GELU'(h), saved by the forward
         CT dg;
         ct_zero(dg);
         mm(dg, W2b, ld_lds(c.DA, rt, lane));
@@ -991,38 +969,49 @@ __device__ __forceinline__ void mlp_bwd_ct(const Mat& m1, const Mat& m2, const L
   }
   __syncthreads();
   CP_MARK(2);
-  const WgAcc<1> a2 = wgrad64_acc(c.DA, c.XB, m2, c);
-  const WgAcc<1> a1 = wgrad64_acc(c.KB, c.QB, m1, c);
-  next();   // the next sublayer's inputs: older than the atomics below
-  wgrad64_flush(a2, m2, c);
-  wgrad64_flush(a1, m1, c);
+  wgrad64(c.DA, c.XB, m2, c);
+  wgrad64(c.KB, c.QB, m1, c);
   __syncthreads();
   CP_MARK(3);
 }
 
 // recompute + store q / k / v of the saved input, attention backward, weight gradients; returns through dx (+=) the
-// input gradient of the q / k / v projections.  Self: q-input = kv-input = x (in.xin).  The attention output
+// input gradient of the q / k / v projections.  Self: q-input = kv-input = x (sv_xin).  The attention output
 // gradient dO must already be in DA.
-template <typename Next>
-__device__ __forceinline__ void self_attn_bwd_ct(const Mat* m, const LNp& ln, CT* dx, const AttnIn& in,
-                                                 const float* sv_lse, bool causal, const Ctx& c, int vslot, Next&& next) {
+__device__ __forceinline__ void self_attn_bwd_ct(const Mat* m, const LNp& ln, CT* dx, const bf16_t* sv_xin,
+                                                 const bf16_t* sv_a, const bf16_t* sv_alo, const float* sv_lse,
+                                                 const bf16_t* sv_xh, const float* sv_rs, bool causal,
+                                                 const Ctx& c, int vslot) {
   const int lane = c.lane;
   const LseR lse = lse_fetch(sv_lse, c);   // consumed after the recompute phase (latency hidden by passes 1-2)
+  CTr xin[MAXRT];
   {
     CT dlg, dlb;
     ct_zero(dlg);
     ct_zero(dlb);
     {   // pass 1: LN backward from the saved x-hat / rstd -> ds (dx) ; DQ = dY of Wp, XB = X of Wp
       const CT gam = ld_vec(ln.g, lane);
+      CTr as[MAXRT], xhs[MAXRT];
+      float rsv[MAXRT];
+#pragma unroll
+      for (int k = 0; k < MAXRT; ++k) {
+        const int rt = c.wave + NW * k;
+        if (rt < c.NT) {
+          as[k] = ld_g(sv_a, c.tok0, rt, c.NR, lane);
+          xin[k] = ld_g(sv_xin, c.tok0, rt, c.NR, lane);
+          xhs[k] = ld_g(sv_xh, c.tok0, rt, c.NR, lane);
+          rsv[k] = ld_tokf(sv_rs, rt, c);
+        }
+      }
 #pragma unroll
       for (int k = 0; k < MAXRT; ++k) {
         const int rt = c.wave + NW * k;
         if (rt < c.NT) {
           const bool ok = tok_ok(rt, c);
           CT ds;
-          ln_bwd_ct(dx[k], ct_unpack(in.xhs[k]), in.rsv[k], gam, ok, ds, dlg, dlb);
+          ln_bwd_ct(dx[k], ct_unpack(xhs[k]), rsv[k], gam, ok, ds, dlg, dlb);
           st_lds(c.DQ, rt, ct_pack(ds), ok, lane);   // dY of Wp
-          st_lds(c.XB, rt, in.as[k], ok, lane);      // X of Wp
+          st_lds(c.XB, rt, as[k], ok, lane);         // X of Wp
           dx[k] = ds;                                // residual path
         }
       }
@@ -1036,13 +1025,14 @@ __device__ __forceinline__ void self_attn_bwd_ct(const Mat* m, const LNp& ln, CT
       for (int k = 0; k < MAXRT; ++k) {
         const int rt = c.wave + NW * k;
         if (rt < c.NT) {
+          const CTr alo = ld_g(sv_alo, c.tok0, rt, c.NR, lane);
           CT da;
           ct_zero(da);
           mm(da, Wpb, ld_lds(c.DQ, rt, lane));
           const bool ok = tok_ok(rt, c);
           const CTr dap = ct_pack(da);
           st_lds(c.DA, rt, dap, ok, lane);
-          attn_delta_ct(ld_lds(c.XB, rt, lane), in.alo[k], dap, rt, ok, c);
+          attn_delta_ct(ld_lds(c.XB, rt, lane), alo, dap, rt, ok, c);
         }
       }
     }
@@ -1053,7 +1043,7 @@ __device__ __forceinline__ void self_attn_bwd_ct(const Mat* m, const LNp& ln, CT
   // (reads DQ / XB): its fp32 atomics drain under the attention instead of stalling the next global loads behind
   // them (vmcnt counts them in order), and one barrier fewer.  XB takes x (the X of dWq/k/v) once every wave is past
   // dWp (after the query-pass barrier).
-  proj3(m, 0, in.xin, c);
+  proj3(m, 0, xin, c);
   wgrad64(c.DQ, c.XB, m[3], c);
   lse_store(lse, c);
   __syncthreads();
@@ -1062,7 +1052,7 @@ __device__ __forceinline__ void self_attn_bwd_ct(const Mat* m, const LNp& ln, CT
 #pragma unroll
   for (int k = 0; k < MAXRT; ++k) {
     const int rt = c.wave + NW * k;
-    if (rt < c.NT) st_lds(c.XB, rt, in.xin[k], tok_ok(rt, c), lane);   // X of dWq / dWk / dWv
+    if (rt < c.NT) st_lds(c.XB, rt, xin[k], tok_ok(rt, c), lane);   // X of dWq / dWk / dWv
   }
   __syncthreads();
   CP_MARK(14);
@@ -1074,9 +1064,7 @@ __device__ __forceinline__ void self_attn_bwd_ct(const Mat* m, const LNp& ln, CT
   {
     const bf16_t* const ys[3] = {c.DQ, c.KB, c.VB};
     const Mat* const ms[3] = {&m[0], &m[1], &m[2]};
-    const WgAcc<3> a = wgrad64x_acc<3>(ys, c.XB, c);
-    next();   // the next sublayer's inputs: older than the atomics below
-    wgrad64x_flush<3>(a, ms, c);
+    wgrad64_shared_x<3>(ys, c.XB, ms, c);
   }
   __syncthreads();
   CP_MARK(17);
