@@ -232,12 +232,27 @@ __device__ __forceinline__ CTr ld_g(const bf16_t* src, int tok0, int rt, int NR,
 #else
 #define SAVE_ON(row, NR) ((row) < (NR))
 #endif
+// The saved-activation records leave as NONTEMPORAL stores (global_store ... nt): measured in the bench (rocprofv3),
+// dec_fwd 189.8 -> 171.3 us and dec_bwd 483 -> 460 us per minibatch — the ~580 MB of records per minibatch no longer
+// churn the L2 the forward's weight / rep loads and the backward's streams run through.  -DMDL_NT_SAVES=0: plain.
+#ifndef MDL_NT_SAVES
+#define MDL_NT_SAVES 1
+#endif
+#ifndef MDL_NT_SCALARS
+#define MDL_NT_SCALARS 0   // A/B: the per-token f32 records (rstd, log-sum-exp) as nontemporal stores too
+#endif
 __device__ __forceinline__ void st_g(bf16_t* dst, int tok0, int rt, int NR, const CTr& x, int lane) {
   const int g = lane >> 4, row = rt * 16 + (lane & 15);
   if (SAVE_ON(row, NR)) {
-    uint4* base = (uint4*)(dst + (size_t)(tok0 + row) * 64 + 16 * g);
-    base[0] = make_uint4(x.q[0].x, x.q[0].y, x.q[1].x, x.q[1].y);
-    base[1] = make_uint4(x.q[2].x, x.q[2].y, x.q[3].x, x.q[3].y);
+    u32x4v* base = (u32x4v*)(dst + (size_t)(tok0 + row) * 64 + 16 * g);
+    const u32x4v a = {x.q[0].x, x.q[0].y, x.q[1].x, x.q[1].y}, b = {x.q[2].x, x.q[2].y, x.q[3].x, x.q[3].y};
+#if MDL_NT_SAVES
+    __builtin_nontemporal_store(a, base);
+    __builtin_nontemporal_store(b, base + 1);
+#else
+    base[0] = a;
+    base[1] = b;
+#endif
   }
 }
 // plain global [tok][64] f32
@@ -267,7 +282,13 @@ __device__ __forceinline__ void st_gf(float* dst, int tok0, int rt, int NR, cons
 // consecutive tokens)
 __device__ __forceinline__ void st_tokf(float* dst, int rt, float v, const Ctx& c) {
   const int row = rt * 16 + (c.lane & 15);
-  if ((c.lane >> 4) == 0 && SAVE_ON(row, c.NR)) dst[(size_t)(c.tok0 + row)] = v;
+  if ((c.lane >> 4) == 0 && SAVE_ON(row, c.NR)) {
+#if MDL_NT_SCALARS
+    __builtin_nontemporal_store(v, dst + (size_t)(c.tok0 + row));
+#else
+    dst[(size_t)(c.tok0 + row)] = v;
+#endif
+  }
 }
 __device__ __forceinline__ float ld_tokf(const float* src, int rt, const Ctx& c) {
   const int row = rt * 16 + (c.lane & 15);
@@ -683,7 +704,14 @@ __device__ __forceinline__ void attn_fwd_ct(const bf16_t* Q, const bf16_t* K, co
         const float il = l > 0.f ? 1.f / l : 0.f;
         O[k].v[2 * h] = o0 * il;
         O[k].v[2 * h + 1] = o1 * il;
-        if (lse_g && g == 0 && q < c.NR) lse_g[(size_t)(c.tok0 + q) * 2 + h] = l > 0.f ? m + __log2f(l) : 0.f;
+        if (lse_g && g == 0 && q < c.NR) {
+          const float lv = l > 0.f ? m + __log2f(l) : 0.f;
+#if MDL_NT_SCALARS
+          __builtin_nontemporal_store(lv, lse_g + (size_t)(c.tok0 + q) * 2 + h);
+#else
+          lse_g[(size_t)(c.tok0 + q) * 2 + h] = lv;
+#endif
+        }
       }
     }
   }
