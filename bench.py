@@ -228,8 +228,8 @@ def _native_build():
     return kernels.BUILD_ID
 
 
-# 32 workers: trained by the round-4 code (linear LR decay, 44.8 M env steps; profiles/r4_train32/README.md)
-DEFAULT_CKPT = {32: "profiles/r4_train32/transformer_3500_lrdecay.pt"}
+# 32 workers: round-5 run with payment weight 3, selected on the held-out preset sets (profiles/r5_train32/README.md)
+DEFAULT_CKPT = {32: "profiles/r5_train32/transformer_500_beta3.pt"}
 
 
 def eval_block(a, args, runner, dev):

@@ -47,6 +47,8 @@ def _flags(src):
     extra = os.environ.get("MAT_DCML_BWD_FLAGS", "").split() if src.endswith("_bwd.hip") else []
     if os.path.basename(src) in FWD_TUS:
         extra = os.environ.get("MAT_DCML_FWD_FLAGS", "").split()
+    if os.path.basename(src) == "mat_enc_ct.hip":   # A/B: the encoder forward alone
+        extra = extra + os.environ.get("MAT_DCML_ENCF_FLAGS", "").split()
     per_file = [] if os.environ.get("MAT_DCML_NO_PER_FILE_FLAGS") else PER_FILE_FLAGS.get(os.path.basename(src), [])
     return FLAGS + per_file + extra
 
