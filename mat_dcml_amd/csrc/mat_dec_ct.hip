@@ -99,7 +99,6 @@ __device__ __forceinline__ void cross_proj(const Mat* m, const CT* xr, const bf1
       rp[k] = ct_pack(ld_gf(rep, c.tok0, rt, c.NR, lane));
       if constexpr (REG) xp[k] = ct_pack(xr[k]);
       else xp[k] = ld_g(sv_x1_in, c.tok0, rt, c.NR, lane);
-      if (sv_x1_out) st_g(sv_x1_out, c.tok0, rt, c.NR, xp[k], lane);
       if constexpr (!REG) { if (store_xb) st_lds(c.XB, rt, xp[k], tok_ok(rt, c), lane); }
     }
   }
@@ -108,6 +107,13 @@ __device__ __forceinline__ void cross_proj(const Mat* m, const CT* xr, const bf1
     AFr W;
     loadA(W, m[4 + mi].fa, lane);
     const CT b = ld_vec(m[4 + mi].b, lane);
+    if (mi == 0 && sv_x1_out) {   // saved x1 behind the first weight load (in-order vmcnt), not ahead of it
+#pragma unroll
+      for (int k = 0; k < MAXRT; ++k) {
+        const int rt = c.wave + NW * k;
+        if (rt < c.NT) st_g(sv_x1_out, c.tok0, rt, c.NR, xp[k], lane);
+      }
+    }
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
       const int rt = c.wave + NW * k;
@@ -131,7 +137,8 @@ __device__ __forceinline__ void cross_attn_fwd_ct(const Mat* m, const LNp& ln, C
   __syncthreads();
   CP_MARK(24);
   CT O[MAXRT];
-  attn_fwd_ct(c.QB, c.KB, c.VB, true, SAVE ? sv_lse : nullptr, O, c);
+  float lse[MAXRT][2];
+  attn_fwd_ct(c.QB, c.KB, c.VB, true, nullptr, O, c, lse);
   CP_MARK(25);
   AFr Wp;
   loadA(Wp, m[7].fa, lane);
@@ -142,6 +149,7 @@ __device__ __forceinline__ void cross_attn_fwd_ct(const Mat* m, const LNp& ln, C
     const int rt = c.wave + NW * k;
     if (rt < c.NT) rp[k] = ld_gf(rep, c.tok0, rt, c.NR, lane);
   }
+  if (SAVE) lse_store_fwd(sv_lse, lse, c);   // behind the proj weight / rep loads
 #pragma unroll
   for (int k = 0; k < MAXRT; ++k) {
     const int rt = c.wave + NW * k;

@@ -572,13 +572,22 @@ __device__ __forceinline__ void wgrad64_shared_x(const bf16_t* const (&Y)[NM], c
 
 // q / k / v projections of the packed tiles xp (one weight matrix live at a time) -> QB / KB / VB; m0 = index of
 // the query matrix (0: self attention; the cross attention has its own q input)
-__device__ __forceinline__ void proj3(const Mat* m, int m0, const CTr* xp, const Ctx& c) {
+// sv_save (forward): the input tiles are saved right after the FIRST weight load is issued (not before the phase's
+// barrier: a store ahead of the weight loads would make them wait for it in the wave's in-order vmcnt)
+__device__ __forceinline__ void proj3(const Mat* m, int m0, const CTr* xp, const Ctx& c, bf16_t* sv_save = nullptr) {
   bf16_t* outs[3] = {c.QB, c.KB, c.VB};
 #pragma unroll
   for (int mi = 0; mi < 3; ++mi) {
     AFr W;
     loadA(W, m[m0 + mi].fa, c.lane);
     const CT b = ld_vec(m[m0 + mi].b, c.lane);
+    if (mi == 0 && sv_save) {
+#pragma unroll
+      for (int k = 0; k < MAXRT; ++k) {
+        const int rt = c.wave + NW * k;
+        if (rt < c.NT) st_g(sv_save, c.tok0, rt, c.NR, xp[k], c.lane);
+      }
+    }
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
       const int rt = c.wave + NW * k;
@@ -658,8 +667,10 @@ __device__ __forceinline__ void split8v(const float* x, bf16x8& hi, bf16x8& lo) 
 }
 
 // forward: O (CT, the wave's query tiles rt = wave + NW k, both heads) = softmax(scale Q Kᵀ) V
+// lse (optional): this lane's log-sum-exp per (tile, head), stored by the CALLER (lse_store_fwd) once it has issued
+// the next phase's weight loads — a store issued before them would sit ahead of them in the wave's in-order vmcnt
 __device__ __forceinline__ void attn_fwd_ct(const bf16_t* Q, const bf16_t* K, const bf16_t* V, bool causal, float* lse_g,
-                                            CT* O, const Ctx& c) {
+                                            CT* O, const Ctx& c, float (*lse)[2] = nullptr) {
   const int lane = c.lane, g = lane >> 4, c16 = lane & 15;
 #pragma unroll
   for (int k = 0; k < MAXRT; ++k) {
@@ -704,7 +715,9 @@ __device__ __forceinline__ void attn_fwd_ct(const bf16_t* Q, const bf16_t* K, co
         const float il = l > 0.f ? 1.f / l : 0.f;
         O[k].v[2 * h] = o0 * il;
         O[k].v[2 * h + 1] = o1 * il;
-        if (lse_g && g == 0 && q < c.NR) {
+        if (lse) {
+          lse[k][h] = l > 0.f ? m + __log2f(l) : 0.f;
+        } else if (lse_g && g == 0 && q < c.NR) {
           const float lv = l > 0.f ? m + __log2f(l) : 0.f;
 #if MDL_NT_SCALARS
           __builtin_nontemporal_store(lv, lse_g + (size_t)(c.tok0 + q) * 2 + h);
@@ -713,6 +726,18 @@ __device__ __forceinline__ void attn_fwd_ct(const bf16_t* Q, const bf16_t* K, co
 #endif
         }
       }
+    }
+  }
+}
+
+__device__ __forceinline__ void lse_store_fwd(float* lse_g, const float (*lse)[2], const Ctx& c) {
+  const int g = c.lane >> 4;
+#pragma unroll
+  for (int k = 0; k < MAXRT; ++k) {
+    const int rt = c.wave + NW * k, q = rt * 16 + (c.lane & 15);
+    if (rt < c.NT && g == 0 && q < c.NR) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) lse_g[(size_t)(c.tok0 + q) * 2 + h] = lse[k][h];
     }
   }
 }
@@ -849,22 +874,21 @@ __device__ __forceinline__ void self_attn_fwd_ct(const Mat* m, const LNp& ln, CT
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {
       const int rt = c.wave + NW * k;
-      if (rt < c.NT) {
-        xp[k] = ct_pack(xr[k]);
-        if (SAVE) st_g(sv_xin, c.tok0, rt, c.NR, xp[k], lane);
-      }
+      if (rt < c.NT) xp[k] = ct_pack(xr[k]);
     }
     __syncthreads();   // every wave done reading the previous attention's K / V (no barrier after an attention)
-    proj3(m, 0, xp, c);
+    proj3(m, 0, xp, c, SAVE ? sv_xin : nullptr);
   }
   __syncthreads();
   CP_MARK(20);
   CT O[MAXRT];
-  attn_fwd_ct(c.QB, c.KB, c.VB, causal, SAVE ? sv_lse : nullptr, O, c);
+  float lse[MAXRT][2];
+  attn_fwd_ct(c.QB, c.KB, c.VB, causal, nullptr, O, c, lse);
   CP_MARK(21);
   AFr Wp;
   loadA(Wp, m[3].fa, lane);
   const CT bp = ld_vec(m[3].b, lane), gam = ld_vec(ln.g, lane), bet = ld_vec(ln.b, lane);
+  if (SAVE) lse_store_fwd(sv_lse, lse, c);   // behind the proj weight loads
 #pragma unroll
   for (int k = 0; k < MAXRT; ++k) {
     const int rt = c.wave + NW * k;

@@ -127,6 +127,10 @@ def test_decode_discrete_smac_shape(gpu, det):
         print(f"mat_decode B=32 L=27 A=36: {s.elapsed_time(e) / 20 * 1e3:.1f} us per env step")
 
 
+# 1.10 x the round-5 measurements taken exactly this way (profiles/r5_final/perf_guards.jsonl)
+DECODE_BOUND_US = {33: 400.0, 101: 1500.0}
+
+
 @pytest.mark.parametrize("L", [33, 101])
 def test_decode_latency(gpu, L):
     B = 256
@@ -142,9 +146,9 @@ def test_decode_latency(gpu, L):
     e.record()
     torch.cuda.synchronize()
     us = s.elapsed_time(e) / 20 * 1e3
-    print(f"mat_decode B=256 L={L}: {us:.1f} us per env step")
-    # regression bounds (~1.4x the round-4 measurement: 282 us one-wave at L = 33, 1,072 us 4-wave at L = 101)
-    assert us < {33: 400.0, 101: 1500.0}[L], us
+    from conftest import perf_record
+    perf_record(f"decode_256x{L}_us", us, DECODE_BOUND_US[L])
+    assert us < DECODE_BOUND_US[L], us
 
 
 @pytest.mark.parametrize("L,A,B", [(6, 1, 64), (2, 6, 40), (17, 3, 16), (33, 2, 8)])
@@ -319,5 +323,7 @@ def test_wave_decode_latency(gpu, L, nb, A, B):
             res[wave] = s.elapsed_time(e) / 20 * 1e3
     finally:
         mat_fused.WAVE_DECODE = saved
-    print(f"decode B={B} L={L} n_block={nb} A={A}: one-wave {res[True]:.1f} us, 4-wave {res[False]:.1f} us per env step")
+    from conftest import perf_record
+    perf_record(f"decode_wave_{B}x{L}_nb{nb}_A{A}_us", res[True], None)
+    perf_record(f"decode_4wave_{B}x{L}_nb{nb}_A{A}_us", res[False], None)
     assert res[True] < res[False] * 1.05, res

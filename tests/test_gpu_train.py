@@ -370,6 +370,10 @@ def test_mat_dec_runner_trains_through_the_hybrid_path(gpu):
     assert r.policy.transformer._mdl_train_state[0].ctx is None   # every fused encoder forward got its backward
 
 
+# 1.10 x the round-5 measurement taken exactly this way (profiles/r5_final/perf_guards.jsonl)
+TRAIN_KERNELS_BOUND_MS = 1.85
+
+
 def test_training_kernels_time_bound(gpu):
     """The four fused training kernels at the bench minibatch (3,200 sequences x 33 agents, n_block 2): hipEvent time
     per minibatch (printed; launch gaps included: ~1.54 ms measured this way, 1.17 ms of kernel time under rocprofv3)
@@ -401,8 +405,9 @@ def test_training_kernels_time_bound(gpu):
         torch.cuda.synchronize()
         ts.append(a.elapsed_time(b))
     ms = sorted(ts)[len(ts) // 2]
-    print(f"four training kernels, 3200 x 33: {ms:.3f} ms per minibatch")
-    assert ms < 1.85, ms
+    from conftest import perf_record
+    perf_record("four_training_kernels_3200x33_ms", ms, TRAIN_KERNELS_BOUND_MS, "ms")
+    assert ms < TRAIN_KERNELS_BOUND_MS, ms
 
 
 @pytest.mark.parametrize("N", [864, 70_000])
