@@ -319,13 +319,35 @@ __device__ __forceinline__ int chunk_plan(int n, int SQ, int L) {
   if (n0 + 1 <= n && bal(n0 + 1) < cost) best = n0 + 1;
   return best;
 }
+// Every other group of 8 workgroups (one per XCD) walks its chunks in reverse order (MDL_STAGGER=1): with unequal chunks (L = 33: 5, 5, 3
+// sequences) half the workgroups of every XCD are then out of phase with the other half, so their weight-gradient atomic bursts
+// (the memory-side atomic unit's 1.3 TB/s is chip-wide) interleave instead of coinciding.
+// Measured in the bench (profiles/r5_ab): dec_bwd 457.6 -> 428.5 us, enc_bwd 305.1 -> 274.3 us per minibatch; the
+// forwards (no atomics) measured +2 us with it, so only the backward translation units default to it.
+// MDL_STAGGER=2 (A/B): three groups — the third walks (0, 2, 1) — measured the same as 1.
+#ifndef MDL_STAGGER
+#ifdef MDL_CT_BWD_TU
+#define MDL_STAGGER 1
+#else
+#define MDL_STAGGER 0
+#endif
+#endif
+__device__ __forceinline__ int stagger_chunk(int it, int nch, int grp) {
+  if (MDL_STAGGER == 0 || nch < 2) return it;
+  if (MDL_STAGGER == 1) return (grp & 1) ? nch - 1 - it : it;
+  const int k = grp % 3;
+  if (k == 0) return it;
+  if (k == 1) return nch - 1 - it;
+  return it == 0 ? 0 : nch - it;   // (0, nch - 1, ..., 1)
+}
 #define FOR_TILES(p, CALL)                                                                         \
   {                                                                                                \
     const long long G_ = gridDim.x, w_ = blockIdx.x;                                               \
     const int lo_ = (int)((long long)(p).Bs * w_ / G_), hi_ = (int)((long long)(p).Bs * (w_ + 1) / G_); \
     const int n_ = hi_ - lo_, plan_ = chunk_plan(n_, (p).SQ, (p).L);                               \
     const int nch_ = plan_ < 0 ? -plan_ : plan_;                                                   \
-    for (int ch_ = 0; ch_ < nch_; ++ch_) {                                                         \
+    for (int it_ = 0; it_ < nch_; ++it_) {                                                         \
+      const int ch_ = stagger_chunk(it_, nch_, (int)(w_ >> 3));                                       \
       int s0, ns;                                                                                  \
       if (plan_ < 0) {                                                                             \
         s0 = lo_ + ch_ * (p).SQ;                                                                   \
@@ -334,7 +356,7 @@ __device__ __forceinline__ int chunk_plan(int n, int SQ, int L) {
         s0 = lo_ + (int)((long long)n_ * ch_ / nch_);                                              \
         ns = lo_ + (int)((long long)n_ * (ch_ + 1) / nch_) - s0;                                   \
       }                                                                                            \
-      if (ch_) __syncthreads();                                                                    \
+      if (it_) __syncthreads();                                                                    \
       CALL;                                                                                        \
     }                                                                                              \
   }
