@@ -357,6 +357,181 @@ __device__ __forceinline__ float rdlane(float x, int l) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
 }
 
+// folded head: W' = W_h2 diag(gamma_h) as hi / lo A fragments (rows = actions 16 ma + c, k in the CT order), and
+// G_a = Σ W'[a], C_a = W_h2 beta_h + b_h2 for this lane's logit slots a = 16 ma + 4 g + r
+template <int MA>
+struct WvHeadW { bf16x8 HH[MA][2], HL[MA][2]; f32x4 HG[MA], HC[MA]; };
+template <int MA>
+__device__ __forceinline__ void wv_head_load(WvHeadW<MA>& hw, const DecParams& p, int lane) {
+  const int g = lane >> 4, c = lane & 15, A = p.act_dim;
+#pragma unroll
+  for (int ma = 0; ma < MA; ++ma) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int a = 16 * ma + c, kk = 32 * s + 16 * (j >> 2) + 4 * g + (j & 3);
+        const float wv = a < A ? p.hfold[(a < A ? a : 0) * 64 + kk] : 0.f;
+        const bf16_t h = f2bf(wv);
+        hw.HH[ma][s][j] = (short)h;
+        hw.HL[ma][s][j] = (short)f2bf(wv - bf2f(h));
+      }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int a = 16 * ma + 4 * g + r;
+      hw.HG[ma][r] = a < A ? p.hfold[A * 64 + a] : 0.f;
+      hw.HC[ma][r] = a < A ? p.hfold[A * 65 + a] : 0.f;
+    }
+  }
+}
+
+// sampling noise of every row: lane j holds row j (+ 64, + 128); the Normal draw of the semi-discrete last row
+struct WvNoise { float U[3]; float zlast; };
+__device__ __forceinline__ WvNoise wv_noise_load(const DecParams& p, int env, int lane) {
+  WvNoise nz{{0.f, 0.f, 0.f}, 0.f};
+  const int L = p.L, A = p.act_dim, n_disc = p.n_disc;
+  if (!p.deterministic) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int row = lane + 64 * q;
+      if (row < n_disc) nz.U[q] = p.gen ? draw_u(p, env, row) : p.rnd_u[(size_t)env * L + row];
+    }
+    if (n_disc < L) nz.zlast = p.gen ? draw_n(p, env, L - 1, A - 1) : p.rnd_n[((size_t)env * L + L - 1) * A + A - 1];
+  }
+  // opaque: otherwise hipcc re-materialises the Philox rounds inside the agent loop (~80 VALU per agent step)
+  asm volatile("" : "+v"(nz.U[0]), "+v"(nz.U[1]), "+v"(nz.U[2]), "+v"(nz.zlast));
+  return nz;
+}
+
+// the head of row i (transformer_act.py:86-97): GELU(W_h1 x + b) -> folded LayerNorm -> logits (hi / lo MFMA
+// products: fp32-like) -> masked categorical / the ratio agent's Normal, every lane alike; writes the row's action
+// and log-prob and returns the next row's input token (unchanged after the continuous last row)
+template <int NM, int NLDS, int NREG, int MA>
+__device__ __forceinline__ int wv_head_sample(const CT& x, const WvHeadW<MA>& hw, const WvNoise& nz, const RegW<NREG>& rw,
+                                              const bf16_t* W, const float* BI, float* SC, const DecParams& p, int env,
+                                              int i, float avl, int tok, int lane) {
+  constexpr bool WIDE = MA > 1;
+  const int g = lane >> 4, c = lane & 15, A = p.act_dim, L = p.L, n_disc = p.n_disc;
+  const bool det = p.deterministic != 0;
+  constexpr int NB = (NM - 7) / 9 + 1;
+  CT h = ld_vec(BI + 64 * (10 * NB), lane);
+  {
+    AFr w;
+    wv_getw<NM - 1, NLDS, NREG>(w, rw, W, lane);
+    mm(h, w, ct_pack(x));
+  }
+  h = gelu_dist(h, lane);
+  WDBG(12, h);
+  f32x4 s4 = (h.v[0] + h.v[1]) + (h.v[2] + h.v[3]);
+  f32x4 q4 = h.v[0] * h.v[0];
+#pragma unroll
+  for (int mt = 1; mt < 4; ++mt) q4 = h.v[mt] * h.v[mt] + q4;
+  const float mean = cross_row_sum((s4[0] + s4[1]) + (s4[2] + s4[3])) * (1.f / 64.f);
+  const float rstd = rsqrtf(fmaxf(cross_row_sum((q4[0] + q4[1]) + (q4[2] + q4[3])) * (1.f / 64.f) - mean * mean, 0.f) + 1e-5f);
+  CTr nh, nl;
+  ct_split(h, nh, nl);
+  f32x4 lg[MA];
+#pragma unroll
+  for (int ma = 0; ma < MA; ++ma) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hw.HH[ma][s], rb(nh, s), acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hw.HH[ma][s], rb(nl, s), acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hw.HL[ma][s], rb(nh, s), acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) lg[ma][r] = rstd * (acc[r] - mean * hw.HG[ma][r]) + hw.HC[ma][r];
+  }
+#ifdef MDL_WAVE_DEBUG
+  {
+    CT lgc;
+#pragma unroll
+    for (int ma = 0; ma < 4; ++ma) lgc.v[ma] = ma < MA ? lg[ma < MA ? ma : 0] : f32x4{0.f, 0.f, 0.f, 0.f};
+    WDBG(13, lgc);
+  }
+#endif
+  const size_t oi = (size_t)env * L + i;
+  float a_out, lp_out;
+  if constexpr (!WIDE) {   // A <= 4: the logits are registers r < A of lanes g = 0
+    float l[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) l[a] = rdlane(lg[0][a], 0);
+    if (i < n_disc) {
+      float mx = -INFINITY;
+      int amax = 0;
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        l[a] = a < A ? (rdlane(avl, a) == 0.f ? -1e10f : l[a]) : -INFINITY;
+        if (l[a] > mx) { mx = l[a]; amax = a; }
+      }
+      float e[4], se = 0.f;
+#pragma unroll
+      for (int a = 0; a < 4; ++a) { e[a] = a < A ? __expf(l[a] - mx) : 0.f; se += e[a]; }
+      const float lse = mx + __logf(se);
+      int act = amax;
+      if (!det) {
+        const float uu = rdlane(i < 64 ? nz.U[0] : i < 128 ? nz.U[1] : nz.U[2], i & 63);
+        const float inv = 1.f / se;
+        float cdf = 0.f;
+        int cnt = 0;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          cdf += e[a] * inv;
+          cnt += (a < A) & (cdf < uu);
+        }
+        act = min(cnt, A - 1);
+      }
+      float la = l[0];
+#pragma unroll
+      for (int a = 1; a < 4; ++a) la = act == a ? l[a] : la;
+      a_out = (float)act;
+      lp_out = la - lse;
+      tok = 1 + act;
+    } else {
+      const float mu = A == 1 ? l[0] : A == 2 ? l[1] : A == 3 ? l[2] : l[3];
+      const float sd = p.stdv[A - 1];
+      a_out = det ? mu : mu + sd * nz.zlast;
+      const float z = (a_out - mu) / sd;
+      lp_out = -0.5f * z * z - __logf(sd) - 0.91893853320467274f;
+    }
+  } else {   // 4 < A <= 64: logits through LDS, lane a = action a
+    if (c == 0) {
+#pragma unroll
+      for (int ma = 0; ma < MA; ++ma) *(f32x4*)(SC + 16 * ma + 4 * g) = lg[ma];
+    }
+    asm volatile("" ::: "memory");
+    const bool aok = lane < A;
+    const float raw = SC[lane];
+    asm volatile("" ::: "memory");   // the next row's writes stay behind these reads
+    if (i < n_disc) {
+      const float l = aok ? (avl == 0.f ? -1e10f : raw) : -INFINITY;
+      const float mx = wave_max(l);
+      int act = __ffsll((unsigned long long)__ballot(l == mx)) - 1;   // first maximum (argmax)
+      const float lse = mx + __logf(wave_sum(aok ? __expf(l - mx) : 0.f));
+      if (!det) {   // inverse CDF: the number of actions whose running probability is below u
+        const float cdf = wv_incl_scan(aok ? __expf(l - lse) : 0.f, lane);
+        const float uu = rdlane(i < 64 ? nz.U[0] : i < 128 ? nz.U[1] : nz.U[2], i & 63);
+        act = min((int)__popcll((unsigned long long)__ballot(aok && cdf < uu)), A - 1);
+      }
+      act = __builtin_amdgcn_readfirstlane(act);
+      a_out = (float)act;
+      lp_out = rdlane(l, act) - lse;
+      tok = 1 + act;
+    } else {
+      const float mu = rdlane(raw, A - 1), sd = p.stdv[A - 1];
+      a_out = det ? mu : mu + sd * nz.zlast;
+      const float z = (a_out - mu) / sd;
+      lp_out = -0.5f * z * z - __logf(sd) - 0.91893853320467274f;
+    }
+  }
+  if (lane == 0) {
+    p.out_a[oi] = a_out;
+    p.out_lp[oi] = lp_out;
+  }
+  return tok;
+}
+
 // MA = logit tiles of the head: 1 (A <= 4: the logits sit in registers r < A of lanes g = 0), 3 (A <= 48: SMAC's
 // 36 actions — a 4th tile was 6 dead MFMAs and 24 registers of folded weights per agent step), 4 (A <= 64)
 template <int NB, int NREG, int MA>
@@ -396,29 +571,8 @@ __global__ __launch_bounds__(64, 1) void mat_decode_wave_kernel(DecParams p) {
   for (int i = lane; i < (10 * NB + 1) * 64; i += 64) BI[i] = p.bias[i];
   for (int i = lane; i < (3 * NB + 1) * 128; i += 64) LP[i] = p.lnp[i];
   for (int i = lane * 8; i < (NB * 4 * L + 32) * 64; i += 512) *(uint4*)(KV + i) = make_uint4(0, 0, 0, 0);
-  // folded head: W' = W_h2 diag(gamma_h) as hi / lo A fragments (rows = actions 16 ma + c, k in the CT order), and
-  // G_a = Σ W'[a], C_a = W_h2 beta_h + b_h2 for this lane's logit slots a = 16 ma + 4 g + r
-  bf16x8 HH[MA][2], HL[MA][2];
-  f32x4 HG[MA], HC[MA];
-#pragma unroll
-  for (int ma = 0; ma < MA; ++ma) {
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int a = 16 * ma + c, kk = 32 * s + 16 * (j >> 2) + 4 * g + (j & 3);
-        const float wv = a < A ? p.hfold[(a < A ? a : 0) * 64 + kk] : 0.f;
-        const bf16_t h = f2bf(wv);
-        HH[ma][s][j] = (short)h;
-        HL[ma][s][j] = (short)f2bf(wv - bf2f(h));
-      }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int a = 16 * ma + 4 * g + r;
-      HG[ma][r] = a < A ? p.hfold[A * 64 + a] : 0.f;
-      HC[ma][r] = a < A ? p.hfold[A * 65 + a] : 0.f;
-    }
-  }
+  WvHeadW<MA> hw;
+  wv_head_load<MA>(hw, p, lane);
   // cross-attention queries of every row and block: q2 = W_q2 rep + b (bf16, as the 4-wave kernel rounds them)
   const float* rep = p.rep + (size_t)env * L * 64;
 #pragma unroll
@@ -439,21 +593,7 @@ __global__ __launch_bounds__(64, 1) void mat_decode_wave_kernel(DecParams p) {
       }
     }
   }
-  // sampling noise of every row: lane j holds row j (+ 64, + 128); the Normal draw of the semi-discrete last row
-  const int n_disc = p.n_disc;
-  const bool det = p.deterministic != 0;
-  float U[3] = {0.f, 0.f, 0.f};
-  float zlast = 0.f;
-  if (!det) {
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const int row = lane + 64 * q;
-      if (row < n_disc) U[q] = p.gen ? draw_u(p, env, row) : p.rnd_u[(size_t)env * L + row];
-    }
-    if (n_disc < L) zlast = p.gen ? draw_n(p, env, L - 1, A - 1) : p.rnd_n[((size_t)env * L + L - 1) * A + A - 1];
-  }
-  // opaque: otherwise hipcc re-materialises the Philox rounds inside the agent loop (~80 VALU per agent step)
-  asm volatile("" : "+v"(U[0]), "+v"(U[1]), "+v"(U[2]), "+v"(zlast));
+  const WvNoise nz = wv_noise_load(p, env, lane);
   __syncthreads();
 
   // ---------------------------------------------------------------- agent loop
@@ -469,123 +609,322 @@ __global__ __launch_bounds__(64, 1) void mat_decode_wave_kernel(DecParams p) {
     CT x;
     wv_block<0, NB, NLDS, NREG>(x, k, rw, i, tok, repi);
     if constexpr (NB > 1) wv_block<1, NB, NLDS, NREG>(x, k, rw, i, tok, repi);
-    // ---- head: GELU(W_h1 x + b) -> folded LayerNorm -> logits (hi / lo MFMA products: fp32-like)
-    CT h = ld_vec(BI + 64 * (10 * NB), lane);
-    {
-      AFr w;
-      wv_getw<NM - 1, NLDS, NREG>(w, rw, W, lane);
-      mm(h, w, ct_pack(x));
+    tok = wv_head_sample<NM, NLDS, NREG, MA>(x, hw, nz, rw, W, BI, SC, p, env, i, avl, tok, lane);
+  }
+}
+
+// ================================================================================================ speculative block 0
+// mat_decode_spec_kernel: the one-wave kernel's agent chain split over 1 + NS waves of one workgroup.  Block 0 of
+// row i + 1 depends on the previous agents only through its input token (the action of agent i) and the committed
+// cache rows 0..i; every candidate token is known in advance (1 + a, a < act_dim).  So while the MAIN wave (wave 0)
+// runs blocks 1.. and the head of row i (the one-wave kernel's code: replicated live row, folded head, sampling),
+// the SPECULATIVE waves (1..NS) run block 0 of row i + 1 for ALL candidate tokens at once — one candidate per MFMA
+// token column, 16 per wave (the one-wave kernel replicates its live row over those 16 columns, so the candidates
+// cost about what the replicated row did).  One workgroup barrier per agent step hands over:
+//   main -> spec : the sampled token (TOK[parity]);
+//   spec -> main : block 0's output row of every candidate (SLOT[parity][cand], fp32) — main reads its token's row;
+//   spec -> spec : the staged cross-attention K / V rows of every candidate (STG[parity][cand]); after the barrier
+//                  every spec wave commits the chosen candidate's rows (and the token's self-attention K / V table
+//                  rows) to the block-0 caches itself (identical values, so the waves' writes never conflict).
+// The critical path per agent step drops from blocks 0 + 1 + head to max(blocks 1 + head, block 0) + one barrier.
+// Block-0 weights live in the speculative waves' registers (6 matrices, 192 VGPRs each), the main wave's matrices
+// in LDS (the last NREG in its registers).  Rows of the candidate attention: keys 0..i-1 from the committed cache
+// (MFMA, as the one-wave kernel), the candidate's own key i from its registers (a per-column dot product), both
+// heads in separate score MFMAs (columns are no longer replicated).  Reference: transformer_act.py:76-99.
+struct SpLds { int w, kv, q2, qt, bi, lp, sc, slot, stg, tok, total; };
+__host__ __device__ inline SpLds sp_lds(int NB, int L, int n_tok, int nlds_main, int A) {
+  SpLds o;
+  int off = 0;
+  auto take = [&](int bytes) { const int r = off; off += (bytes + 15) & ~15; return r; };
+  o.w = take(nlds_main * 8192);              // the main wave's LDS-resident matrices (blocks 1.., head)
+  o.kv = take((NB * 4 * L + 32) * 128);      // K / V caches (+ 32 zero rows)
+  o.q2 = take(NB * L * 128);                 // cross-attention queries
+  o.qt = take(n_tok * 3 * 128);              // block-0 q / k / v of every token
+  o.bi = take((10 * NB + 1) * 256);
+  o.lp = take((3 * NB + 1) * 512);
+  o.sc = take(64 * 4);
+  o.slot = take(2 * A * 256);                // [parity][candidate][64] f32 block-0 outputs
+  o.stg = take(2 * A * 256);                 // [parity][candidate][K, V][64] bf16 cross-attention cache rows
+  o.tok = take(16);                          // [parity] token of the next row
+  o.total = off;
+  return o;
+}
+
+// Causal attention of row i for the wave's 16 candidates (column c): keys 0..i-1 from the committed caches, key i the
+// candidate's own (ks, vs).  Online softmax per head in log2 units, seeded with the own key (score m, weight 1,
+// value vs), so every row has a finite running max and no chunk needs a FIRST special case.
+__device__ __forceinline__ CT sp_attn(const bf16_t* Kc, const bf16_t* Vc, const CTr& q, const CTr& ks, const CTr& vs,
+                                      int i, int lane) {
+  const int g = lane >> 4, c = lane & 15;
+  float m[2], l[2];
+  f32x4 o[4];
+  {
+    const CT qf = ct_unpack(q), kf = ct_unpack(ks), vf = ct_unpack(vs);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x4 d = qf.v[2 * h] * kf.v[2 * h] + qf.v[2 * h + 1] * kf.v[2 * h + 1];
+      m[h] = cross_row_sum((d[0] + d[1]) + (d[2] + d[3])) * ATT_L2;
+      l[h] = g == 0 ? 1.f : 0.f;   // the own key's weight, counted once per column
+      o[2 * h] = vf.v[2 * h];
+      o[2 * h + 1] = vf.v[2 * h + 1];
     }
-    h = gelu_dist(h, lane);
-    WDBG(12, h);
-    f32x4 s4 = (h.v[0] + h.v[1]) + (h.v[2] + h.v[3]);
-    f32x4 q4 = h.v[0] * h.v[0];
+  }
+  const bf16x8 qb0 = rb(q, 0), qb1 = rb(q, 1);
+  for (int kb = 0; kb < i; kb += 32) {
+    const bf16_t* Kk = Kc + kb * 64;
+    float sc[2][8];
 #pragma unroll
-    for (int mt = 1; mt < 4; ++mt) q4 = h.v[mt] * h.v[mt] + q4;
-    const float mean = cross_row_sum((s4[0] + s4[1]) + (s4[2] + s4[3])) * (1.f / 64.f);
-    const float rstd = rsqrtf(fmaxf(cross_row_sum((q4[0] + q4[1]) + (q4[2] + q4[3])) * (1.f / 64.f) - mean * mean, 0.f) + 1e-5f);
-    CTr nh, nl;
-    ct_split(h, nh, nl);
-    f32x4 lg[MA];
+    for (int t = 0; t < 2; ++t) {
+      const int key = pi_row(t, c);
+      const uint2 p0 = kv_ld2(Kk, key, 4 * g), p1 = kv_ld2(Kk, key, 16 + 4 * g);
+      const uint2 p2 = kv_ld2(Kk, key, 32 + 4 * g), p3 = kv_ld2(Kk, key, 48 + 4 * g);
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      const f32x4 r0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(mk8(p0.x, p0.y, p1.x, p1.y), qb0, z, 0, 0, 0);
+      const f32x4 r1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(mk8(p2.x, p2.y, p3.x, p3.y), qb1, z, 0, 0, 0);
 #pragma unroll
-    for (int ma = 0; ma < MA; ++ma) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(HH[ma][s], rb(nh, s), acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(HH[ma][s], rb(nl, s), acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(HL[ma][s], rb(nh, s), acc, 0, 0, 0);
+      for (int rr = 0; rr < 4; ++rr) {
+        sc[0][4 * t + rr] = r0[rr];
+        sc[1][4 * t + rr] = r1[rr];
       }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) lg[ma][r] = rstd * (acc[r] - mean * HG[ma][r]) + HC[ma][r];
     }
-#ifdef MDL_WAVE_DEBUG
-    {
-      CT lgc;
+    const int d0 = i - 1 - kb - 8 * g;   // key kb + 8g + j is committed (< i) iff j <= d0
 #pragma unroll
-      for (int ma = 0; ma < 4; ++ma) lgc.v[ma] = ma < MA ? lg[ma < MA ? ma : 0] : f32x4{0.f, 0.f, 0.f, 0.f};
-      WDBG(13, lgc);
+    for (int h = 0; h < 2; ++h) {
+      float cm = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sc[h][j] = j <= d0 ? sc[h][j] : -INFINITY;
+        cm = fmaxf(cm, sc[h][j]);
+      }
+      const float nm = fmaxf(m[h], cross_row_max(cm) * ATT_L2);
+      const float alpha = fast_exp2(m[h] - nm);
+      float ps = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sc[h][j] = fast_exp2(fmaf(sc[h][j], ATT_L2, -nm));
+        ps += sc[h][j];
+      }
+      l[h] = l[h] * alpha + ps;
+      bf16x8 ph, pl;
+      split8v(sc[h], ph, pl);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int mt = 2 * h + u;
+        const bf16x8 va = ld_frag_T(Vc + kb * 64, 0, 16 * mt, lane);
+        o[mt] *= alpha;
+        o[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, ph, o[mt], 0, 0, 0);
+        o[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pl, o[mt], 0, 0, 0);
+      }
+      m[h] = nm;
     }
-#endif
-    // ---- sample (transformer_act.py:86-97: masked categorical / the ratio agent's Normal), every lane alike
-    const size_t oi = (size_t)env * L + i;
-    float a_out, lp_out;
-    if constexpr (!WIDE) {   // A <= 4: the logits are registers r < A of lanes g = 0
-      float l[4];
+  }
+  CT O;
 #pragma unroll
-      for (int a = 0; a < 4; ++a) l[a] = rdlane(lg[0][a], 0);
-      if (i < n_disc) {
-        float mx = -INFINITY;
-        int amax = 0;
+  for (int h = 0; h < 2; ++h) {
+    const float il = 1.f / cross_row_sum(l[h]);
+    O.v[2 * h] = o[2 * h] * il;
+    O.v[2 * h + 1] = o[2 * h + 1] * il;
+  }
+  return O;
+}
+
+// block 0 (ma_transformer.py:95-98) of row i for the wave's 16 candidates: x = the candidates' embedded input rows in,
+// block 0's output out; kp / vp = their cross-attention K / V rows (staged for the commit)
+__device__ __forceinline__ void sp_block0(CT& x, const CTr& cq, const CTr& ck, const CTr& cv, const RegW<6>& w0,
+                                          const WvCtx& k, int i, const CT& repi, CTr& kp, CTr& vp) {
+  const int lane = k.lane, g = lane >> 4, L = k.L;
+  CT xh;
+  {
+    const CT O = sp_attn(wv_cache(k.KV, 0, 0, L), wv_cache(k.KV, 0, 1, L), cq, ck, cv, i, lane);
+    CT t = ct_add(ld_vec(k.BI + 64 * 3, lane), x);
+    mm(t, w0.w[0], ct_pack(O));
+    ln_fwd_ct(t, xh, x, ld_vec(k.LP, lane), ld_vec(k.LP + 64, lane));
+  }
+  {
+    const CTr xp = ct_pack(x);
+    CT kk = ld_vec(k.BI + 64 * 5, lane), vv = ld_vec(k.BI + 64 * 6, lane);
+    mm(kk, w0.w[1], xp);
+    mm(vv, w0.w[2], xp);
+    kp = ct_pack(kk);
+    vp = ct_pack(vv);
+  }
+  {
+    CTr q2;
 #pragma unroll
-        for (int a = 0; a < 4; ++a) {
-          l[a] = a < A ? (rdlane(avl, a) == 0.f ? -1e10f : l[a]) : -INFINITY;
-          if (l[a] > mx) { mx = l[a]; amax = a; }
+    for (int mt = 0; mt < 4; ++mt) q2.q[mt] = *(const uint2*)(k.Q2 + (size_t)i * 64 + 16 * mt + 4 * g);
+    const CT O = sp_attn(wv_cache(k.KV, 0, 2, L), wv_cache(k.KV, 0, 3, L), q2, kp, vp, i, lane);
+    CT t = ct_add(ld_vec(k.BI + 64 * 7, lane), repi);
+    mm(t, w0.w[3], ct_pack(O));
+    ln_fwd_ct(t, xh, x, ld_vec(k.LP + 128, lane), ld_vec(k.LP + 128 + 64, lane));
+  }
+  {
+    CT h = ld_vec(k.BI + 64 * 8, lane);
+    mm(h, w0.w[4], ct_pack(x));
+    gelu_ct(h);
+    CT t = ct_add(ld_vec(k.BI + 64 * 9, lane), x);
+    mm(t, w0.w[5], ct_pack(h));
+    ln_fwd_ct(t, xh, x, ld_vec(k.LP + 256, lane), ld_vec(k.LP + 256 + 64, lane));
+  }
+}
+
+// candidate token constants of one lane: block-0 q / k / v table rows (bf16) and the embedded input row (f32)
+struct SpCand { CTr q, k, v; CT e; };
+__device__ __forceinline__ SpCand sp_cand(const bf16_t* QT, const float* emb, int tok, int lane) {
+  const int g = lane >> 4;
+  SpCand cd;
+  const bf16_t* t = QT + tok * 192;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    cd.q.q[mt] = *(const uint2*)(t + 16 * mt + 4 * g);
+    cd.k.q[mt] = *(const uint2*)(t + 64 + 16 * mt + 4 * g);
+    cd.v.q[mt] = *(const uint2*)(t + 128 + 16 * mt + 4 * g);
+  }
+  cd.e = ld_vec(emb + tok * 64, lane);
+  return cd;
+}
+
+template <int NB, int NS, int NREG, int MA>
+__global__ __launch_bounds__(64 * (1 + NS), 1) void mat_decode_spec_kernel(DecParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NM = wv_nm(NB), NMM = NM - 6, NLDS = NM - NREG;   // main: slots 6 .. NM - 1, LDS: 6 .. NLDS - 1
+  constexpr int NT = 64 * (1 + NS);
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, c = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int env = blockIdx.x, L = p.L, A = p.act_dim;
+  const SpLds lo = sp_lds(NB, L, p.n_tok, NMM - NREG, A);
+  bf16_t* Wl = (bf16_t*)(smem + lo.w);
+  bf16_t* KV = (bf16_t*)(smem + lo.kv);
+  bf16_t* Q2 = (bf16_t*)(smem + lo.q2);
+  bf16_t* QT = (bf16_t*)(smem + lo.qt);
+  float* BI = (float*)(smem + lo.bi);
+  float* LP = (float*)(smem + lo.lp);
+  float* SC = (float*)(smem + lo.sc);
+  float* SLOT = (float*)(smem + lo.slot);
+  bf16_t* STG = (bf16_t*)(smem + lo.stg);
+  int* TOK = (int*)(smem + lo.tok);
+  const float* rep = p.rep + (size_t)env * L * 64;
+
+  // ---------------------------------------------------------------- setup (all waves)
+  for (int e = tid; e < (NLDS - 6) * 512; e += NT) {
+    const int sl = 6 + e / 512, j = e % 512;
+    ((uint4*)(Wl + (size_t)(sl - 6) * 4096))[j] = ((const uint4*)(p.wfa + (size_t)wv_lin(NB, sl) * 4096))[j];
+  }
+  for (int e = tid; e < p.n_tok * 192; e += NT) QT[e] = f2bf(p.qkv0[e]);
+  for (int e = tid; e < (10 * NB + 1) * 64; e += NT) BI[e] = p.bias[e];
+  for (int e = tid; e < (3 * NB + 1) * 128; e += NT) LP[e] = p.lnp[e];
+  for (int e = tid * 8; e < (NB * 4 * L + 32) * 64; e += NT * 8) *(uint4*)(KV + e) = make_uint4(0, 0, 0, 0);
+  // cross-attention queries q2 = W_q2 rep + b of every row and block, 16-row tiles spread over the waves
+  {
+    const int ntile = (L + 15) >> 4;
+    for (int jt = wave; jt < NB * ntile; jt += 1 + NS) {
+      const int b = jt / ntile, t0 = 16 * (jt % ntile);
+      AFr wq;
+      loadA(wq, p.wfa + (size_t)(10 * b + 4) * 4096, lane);
+      const int row = t0 + c;
+      CT xr;
+      if (row < L) xr = ld_vec(rep + (size_t)row * 64, lane); else ct_zero(xr);
+      CT q = ld_vec(p.bias + (10 * b + 4) * 64, lane);
+      mm(q, wq, ct_pack(xr));
+      const CTr qp = ct_pack(q);
+      if (row < L) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) *(uint2*)(Q2 + (size_t)(b * L + row) * 64 + 16 * mt + 4 * g) = qp.q[mt];
+      }
+    }
+  }
+  __syncthreads();
+
+  const WvCtx k{Wl - 6 * 4096, KV, Q2, QT, p.emb, BI, LP, lane, L};
+  if (wave == 0) {
+    // ---------------------------------------------------------------- main wave: blocks 1.., head, sampling
+    RegW<NREG> rw;
+#pragma unroll
+    for (int r = 0; r < NREG; ++r) loadA(rw.w[r], p.wfa + (size_t)wv_lin(NB, NLDS + r) * 4096, lane);
+    WvHeadW<MA> hw;
+    wv_head_load<MA>(hw, p, lane);
+    const WvNoise nz = wv_noise_load(p, env, lane);
+    const float* ava = p.ava ? p.ava + (size_t)env * L * A : nullptr;
+    int tok = p.tok_start;
+    if (lane == 0) TOK[0] = tok;
+    __syncthreads();   // (1) row 0's block 0 is staged
+#pragma unroll 1
+    for (int i = 0; i < L; ++i) {
+      const CT repi = ld_vec(rep + (size_t)i * 64, lane);
+      const float avl = (ava && lane < A) ? ava[(size_t)i * A + lane] : 1.f;
+      CT x = ld_vec(SLOT + (size_t)((i & 1) * A + (i == 0 ? 0 : tok - 1)) * 64, lane);
+      if constexpr (NB > 1) wv_block<1, NB, NLDS, NREG>(x, k, rw, i, tok, repi);
+      tok = wv_head_sample<NM, NLDS, NREG, MA>(x, hw, nz, rw, k.W, BI, SC, p, env, i, avl, tok, lane);
+      if (lane == 0) TOK[(i + 1) & 1] = tok;
+      __syncthreads();   // (2) token of row i + 1 published; block 0 of row i + 1 staged for every candidate
+    }
+  } else {
+    // ---------------------------------------------------------------- speculative waves: block 0 of the next row
+    RegW<6> w0;
+#pragma unroll
+    for (int r = 0; r < 6; ++r) loadA(w0.w[r], p.wfa + (size_t)wv_lin(NB, r) * 4096, lane);
+    const int cand = 16 * (wave - 1) + c;   // this lane's candidate: input token 1 + cand (rows >= 1)
+    const bool own = cand < A;
+    auto stage = [&](int par, const CT& x, const CTr& kp, const CTr& vp) {
+      if (own) {
+        float* sl = SLOT + (size_t)(par * A + cand) * 64;
+        bf16_t* st = STG + (size_t)(par * A + cand) * 128;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          *(f32x4*)(sl + 16 * mt + 4 * g) = x.v[mt];
+          *(uint2*)(st + 16 * mt + 4 * g) = kp.q[mt];
+          *(uint2*)(st + 64 + 16 * mt + 4 * g) = vp.q[mt];
         }
-        float e[4], se = 0.f;
-#pragma unroll
-        for (int a = 0; a < 4; ++a) { e[a] = a < A ? __expf(l[a] - mx) : 0.f; se += e[a]; }
-        const float lse = mx + __logf(se);
-        int act = amax;
-        if (!det) {
-          const float uu = rdlane(i < 64 ? U[0] : i < 128 ? U[1] : U[2], i & 63);
-          const float inv = 1.f / se;
-          float cdf = 0.f;
-          int cnt = 0;
-#pragma unroll
-          for (int a = 0; a < 4; ++a) {
-            cdf += e[a] * inv;
-            cnt += (a < A) & (cdf < uu);
-          }
-          act = min(cnt, A - 1);
-        }
-        float la = l[0];
-#pragma unroll
-        for (int a = 1; a < 4; ++a) la = act == a ? l[a] : la;
-        a_out = (float)act;
-        lp_out = la - lse;
-        tok = 1 + act;
-      } else {
-        const float mu = A == 1 ? l[0] : A == 2 ? l[1] : A == 3 ? l[2] : l[3];
-        const float sd = p.stdv[A - 1];
-        a_out = det ? mu : mu + sd * zlast;
-        const float z = (a_out - mu) / sd;
-        lp_out = -0.5f * z * z - __logf(sd) - 0.91893853320467274f;
       }
-    } else {   // 4 < A <= 64: logits through LDS, lane a = action a
-      if (c == 0) {
-#pragma unroll
-        for (int ma = 0; ma < MA; ++ma) *(f32x4*)(SC + 16 * ma + 4 * g) = lg[ma];
-      }
-      asm volatile("" ::: "memory");
-      const bool aok = lane < A;
-      const float raw = SC[lane];
-      asm volatile("" ::: "memory");   // the next row's writes stay behind these reads
-      if (i < n_disc) {
-        const float l = aok ? (avl == 0.f ? -1e10f : raw) : -INFINITY;
-        const float mx = wave_max(l);
-        int act = __ffsll((unsigned long long)__ballot(l == mx)) - 1;   // first maximum (argmax)
-        const float lse = mx + __logf(wave_sum(aok ? __expf(l - mx) : 0.f));
-        if (!det) {   // inverse CDF: the number of actions whose running probability is below u
-          const float cdf = wv_incl_scan(aok ? __expf(l - lse) : 0.f, lane);
-          const float uu = rdlane(i < 64 ? U[0] : i < 128 ? U[1] : U[2], i & 63);
-          act = min((int)__popcll((unsigned long long)__ballot(aok && cdf < uu)), A - 1);
-        }
-        act = __builtin_amdgcn_readfirstlane(act);
-        a_out = (float)act;
-        lp_out = rdlane(l, act) - lse;
-        tok = 1 + act;
-      } else {
-        const float mu = rdlane(raw, A - 1), sd = p.stdv[A - 1];
-        a_out = det ? mu : mu + sd * zlast;
-        const float z = (a_out - mu) / sd;
-        lp_out = -0.5f * z * z - __logf(sd) - 0.91893853320467274f;
-      }
+    };
+    {   // row 0: every column runs the start token
+      const SpCand c0 = sp_cand(QT, p.emb, p.tok_start, lane);
+      CT x = c0.e;
+      CTr kp, vp;
+      sp_block0(x, c0.q, c0.k, c0.v, w0, k, 0, ld_vec(rep, lane), kp, vp);
+      stage(0, x, kp, vp);
     }
-    if (lane == 0) {
-      p.out_a[oi] = a_out;
-      p.out_lp[oi] = lp_out;
+    const SpCand cd = sp_cand(QT, p.emb, min(1 + cand, p.n_tok - 1), lane);
+    __syncthreads();   // (1)
+#pragma unroll 1
+    for (int i = 0; i < L; ++i) {
+      const CT repn = ld_vec(rep + (size_t)min(i + 1, L - 1) * 64, lane);
+      // commit row i of the block-0 caches: the token's self-attention K / V table rows and the staged cross K / V
+      // rows of its candidate; lane (kind, 16-byte chunk), kinds 0..3 = self K, self V, cross K, cross V
+      const int tk = TOK[i & 1];
+      if (lane < 32) {
+        const int kind = lane >> 3, ch = lane & 7;
+        const bf16_t* src = kind < 2 ? QT + tk * 192 + 64 * (kind + 1) + 8 * ch
+                                     : STG + (size_t)((i & 1) * A + (i == 0 ? 0 : tk - 1)) * 128 + 64 * (kind - 2) + 8 * ch;
+        *(uint4*)(wv_cache(KV, 0, kind, L) + tmo(i, 8 * ch)) = *(const uint4*)src;
+      }
+      asm volatile("" ::: "memory");   // the committed row is read back by other lanes below (LDS is in order per wave)
+      if (i + 1 < L) {
+        CT x = cd.e;
+        CTr kp, vp;
+        sp_block0(x, cd.q, cd.k, cd.v, w0, k, i + 1, repn, kp, vp);
+        stage((i + 1) & 1, x, kp, vp);
+      }
+      __syncthreads();   // (2)
     }
+  }
+}
+
+template <int NB, int NS, int NREG, int MA>
+int sp_launch(const DecParams* p, size_t lds, hipStream_t st) {
+  hipError_t e = hipFuncSetAttribute((const void*)mat_decode_spec_kernel<NB, NS, NREG, MA>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return -(int)e;
+  hipLaunchKernelGGL((mat_decode_spec_kernel<NB, NS, NREG, MA>), dim3(p->B), dim3(64 * (1 + NS)), lds, st, *p);
+  e = hipGetLastError();
+  return e == hipSuccess ? 0 : -(int)e;
+}
+template <int NS, int MA>
+int sp_launch_nreg(const DecParams* p, int nreg, size_t lds, hipStream_t st) {
+  switch (nreg) {
+    case 2: return sp_launch<2, NS, 2, MA>(p, lds, st);
+    case 4: return sp_launch<2, NS, 4, MA>(p, lds, st);
+    case 6: return sp_launch<2, NS, 6, MA>(p, lds, st);
+    default: return sp_launch<2, NS, 0, MA>(p, lds, st);
   }
 }
 
@@ -627,7 +966,43 @@ MDL_API int mdl_decode_wave_plan(const DecParams* p, int NB) {
   return -1;
 }
 
+// The speculative-block-0 path (mat_decode_spec_kernel): n_block 2 one-wave-path calls with act_dim <= 48 (one to
+// three speculative waves).  MAT_DCML_DECODE_SPEC=0 or mdl_decode_spec_enable(0) keeps the one-wave kernel.
+// Returns the number of register-resident main-wave matrices, or -1 (not on this path).
+static int g_spec_enable = -1;
+MDL_API void mdl_decode_spec_enable(int on) { g_spec_enable = on; }
+static bool spec_enabled() {
+  if (g_spec_enable < 0) {
+    const char* e = getenv("MAT_DCML_DECODE_SPEC");
+    g_spec_enable = !(e && e[0] == '0');
+  }
+  return g_spec_enable != 0;
+}
+MDL_API int mdl_decode_spec_plan(const DecParams* p, int NB) {
+  if (!spec_enabled() || NB != 2 || mdl_decode_wave_plan(p, NB) < 0 || p->act_dim > 48) return -1;
+  if (p->n_tok < p->act_dim + 1) return -1;
+  const int nmm = wv_nm(NB) - 6;
+  static const int minreg = [] { const char* e = getenv("MAT_DCML_SPEC_NREG"); return e ? atoi(e) : 4; }();
+  for (int nreg = minreg; nreg <= 6; nreg += 2)
+    if (sp_lds(NB, p->L, p->n_tok, nmm - nreg, p->act_dim).total <= 160 * 1024) return nreg;
+  return -1;
+}
+static int mdl_decode_spec(const DecParams* p, int NB, hipStream_t st) {
+  const int nreg = mdl_decode_spec_plan(p, NB);
+  if (nreg < 0) return 1;
+  const int A = p->act_dim, NS = (A + 15) / 16;
+  const size_t lds = (size_t)sp_lds(NB, p->L, p->n_tok, wv_nm(NB) - 6 - nreg, A).total;
+  if (A <= 4) return sp_launch_nreg<1, 1>(p, nreg, lds, st);
+  if (NS == 1) return sp_launch_nreg<1, 3>(p, nreg, lds, st);
+  if (NS == 2) return sp_launch_nreg<2, 3>(p, nreg, lds, st);
+  return sp_launch_nreg<3, 3>(p, nreg, lds, st);
+}
+
 int mdl_decode_wave(const DecParams* p, int NB, hipStream_t st) {
+  if (p->B > 0) {
+    const int r = mdl_decode_spec(p, NB, st);
+    if (r <= 0) return r;
+  }
   const int nreg = mdl_decode_wave_plan(p, NB);
   if (nreg < 0) return 1;
   if (p->B <= 0) return 0;

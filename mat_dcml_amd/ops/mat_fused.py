@@ -35,6 +35,8 @@ class DecParams(ctypes.Structure):
 sig("mdl_mat_decode", ctypes.POINTER(DecParams), i32, vp)
 sig("mdl_mat_decode_geometry", i32, i32, i32)
 sig("mdl_decode_wave_plan", ctypes.POINTER(DecParams), i32)
+sig("mdl_decode_spec_plan", ctypes.POINTER(DecParams), i32)
+sig("mdl_decode_spec_enable", i32)
 
 
 def _is_cont(model):
@@ -83,6 +85,11 @@ def supports(model, L=None) -> bool:
 # One-wave decode (csrc/mat_decode_wave.hip) for one-row token passes; False (or MAT_DCML_DECODE_WAVE=0) keeps every
 # decode on the 4-wave kernel (csrc/mat_decode.hip) — the A/B switch and the parity tests' reference.
 WAVE_DECODE = os.environ.get("MAT_DCML_DECODE_WAVE", "1") != "0"
+# Speculative block 0 on that path (csrc/mat_decode_wave.hip:mat_decode_spec_kernel, n_block 2, act_dim <= 48): block 0
+# of the next agent runs for every candidate token on extra waves while the main wave finishes the current agent.
+# False (or MAT_DCML_DECODE_SPEC=0) keeps the one-wave kernel — the A/B switch and the parity tests' reference.
+SPEC_DECODE = os.environ.get("MAT_DCML_DECODE_SPEC", "1") != "0"
+_spec_set = [None]
 
 # envs per decode workgroup: the kernel runs one env per workgroup (its MFMA attention shares the K / V operand
 # over the tile's query rows); the geometry query still takes the cap for its signature.
@@ -262,14 +269,20 @@ def decode(model, rep, ava=None, deterministic=False, stride=1, rand=None):
                     P(pk.get("wa")).value, P(pk.get("ba")).value, P(pk.get("lnd")).value, int(gen), rk0, rk1, rctr,
                     avail, P(pk.get("qkv0")).value, 0, int(getattr(model, "_mdl_env0", 0)) & 0xFFFFFFFF,
                     P(pk.get("hfold")).value, P(pk.get("wfa") if WAVE_DECODE else None).value)
+    if _spec_set[0] != SPEC_DECODE:
+        lib().mdl_decode_spec_enable(int(SPEC_DECODE))
+        _spec_set[0] = SPEC_DECODE
     model._mdl_decode_path = wave_path(prm, model.n_block)
     check(lib().mdl_mat_decode(ctypes.byref(prm), model.n_block, kernels._stream()), "mat_decode")
     return out_a, out_lp
 
 
 def wave_path(prm, n_block):
-    """'wave(nreg=k)' when the decode call runs on the one-wave kernel (k weight matrices register-resident), else
-    '4wave'."""
+    """'spec(nreg=k)' when the decode call runs on the speculative-block-0 kernel (k main-wave matrices
+    register-resident), 'wave(nreg=k)' on the one-wave kernel, else '4wave'."""
+    k = lib().mdl_decode_spec_plan(ctypes.byref(prm), n_block)
+    if k >= 0:
+        return f"spec(nreg={k})"
     k = lib().mdl_decode_wave_plan(ctypes.byref(prm), n_block)
     return f"wave(nreg={k})" if k >= 0 else "4wave"
 

@@ -128,7 +128,7 @@ def test_decode_discrete_smac_shape(gpu, det):
 
 
 # 1.10 x the round-5 measurements taken exactly this way (profiles/r5_final/perf_guards.jsonl)
-DECODE_BOUND_US = {33: 278.0, 101: 1138.0}   # 252.5 / 1034.6 us measured
+DECODE_BOUND_US = {33: 175.0, 101: 1138.0}   # 159.2 (speculative kernel) / 1034.6 us measured
 
 
 @pytest.mark.parametrize("L", [33, 101])
@@ -228,17 +228,18 @@ def test_decode_available_continuous_matches_torch(gpu, L, A, B, det):
     assert err.mean().item() < 2e-2 and err.max().item() < 0.2, (err.mean().item(), err.max().item())
 
 
-def _both_kernels(m, rep, ava, det, rand):
-    """The same decode call on the one-wave kernel (csrc/mat_decode_wave.hip) and on the 4-wave kernel."""
-    saved = mat_fused.WAVE_DECODE
+def _both_kernels(m, rep, ava, det, rand, spec=False):
+    """The same decode call on the one-wave kernel (csrc/mat_decode_wave.hip; spec: its speculative-block-0 variant
+    where the configuration allows it) and on the 4-wave kernel."""
+    saved = mat_fused.WAVE_DECODE, mat_fused.SPEC_DECODE
     try:
-        mat_fused.WAVE_DECODE = True
+        mat_fused.WAVE_DECODE, mat_fused.SPEC_DECODE = True, spec
         a_w, lp_w = mat_fused.decode(m, rep, ava, det, 1, rand)
         path = m._mdl_decode_path
         mat_fused.WAVE_DECODE = False
         a_4, lp_4 = mat_fused.decode(m, rep, ava, det, 1, rand)
     finally:
-        mat_fused.WAVE_DECODE = saved
+        mat_fused.WAVE_DECODE, mat_fused.SPEC_DECODE = saved
     torch.cuda.synchronize()
     return path, a_w, lp_w, a_4, lp_4
 
@@ -247,18 +248,20 @@ def _both_kernels(m, rep, ava, det, rand):
                                             (5, 64, 2, "Semi_Discrete", 2), (101, 16, 1, "Semi_Discrete", 2),
                                             (27, 32, 2, "Discrete", 36), (9, 48, 1, "Discrete", 3)])
 @pytest.mark.parametrize("det", [False, True])
-def test_wave_decode_matches_4wave_and_torch(gpu, L, B, nb, atype, A, det):
-    """One-wave decode vs the 4-wave kernel and the fp32 torch decode on the same draws: decisions taken from the same
-    prefix agree (bf16 near-ties aside), the kernel's log-probs are the teacher-forced log-probs of its own actions,
-    masked actions are never taken, and the launch really is the one-wave kernel."""
+@pytest.mark.parametrize("spec", [False, True])
+def test_wave_decode_matches_4wave_and_torch(gpu, L, B, nb, atype, A, det, spec):
+    """One-wave decode (and, n_block 2, its speculative-block-0 variant) vs the 4-wave kernel and the fp32 torch decode
+    on the same draws: decisions taken from the same prefix agree (bf16 near-ties aside), the kernel's log-probs are
+    the teacher-forced log-probs of its own actions, masked actions are never taken, and the launch really is the
+    kernel under test."""
     m = make(L, gpu, atype=atype, A=A, seed=11, nb=nb)
     obs, ava, rep, rand = inputs(m, B, L, gpu, A=A)
     if A > 2:
         g = torch.Generator(device=gpu).manual_seed(3)
         ava = (torch.rand(B, L, A, device=gpu, generator=g) < 0.6).float()
         ava[..., 0] = 1.0
-    path, a_w, lp_w, a_4, lp_4 = _both_kernels(m, rep, ava, det, rand)
-    assert path.startswith("wave"), path
+    path, a_w, lp_w, a_4, lp_4 = _both_kernels(m, rep, ava, det, rand, spec)
+    assert path.startswith("spec" if spec and nb == 2 else "wave"), path
     a_ref, _ = act.autoregressive_act(m, rep, obs, ava, det, 1, rand)
     n_disc = L if atype == "Discrete" else L - 1
     for other in (a_4, a_ref):
@@ -302,6 +305,8 @@ def test_wave_decode_inkernel_draws_match_4wave(gpu):
 
 # one-wave kernel bounds: 1.10 x the round-5 measurements (251.8 / 448.1 / 215.1 us, profiles/r5_final/perf_guards.jsonl)
 WAVE_BOUND_US = {(33, 2, 2, 256): 277.0, (101, 1, 2, 256): 493.0, (27, 2, 36, 32): 237.0}
+# speculative-block-0 kernel (the default rollout path at these shapes): 1.10 x 157.1 / 139.8 us measured
+SPEC_BOUND_US = {(33, 2, 2, 256): 173.0, (27, 2, 36, 32): 154.0}
 
 
 @pytest.mark.parametrize("L,nb,A,B", [(33, 2, 2, 256), (101, 1, 2, 256), (27, 2, 36, 32)])
@@ -310,11 +315,11 @@ def test_wave_decode_latency(gpu, L, nb, A, B):
     slower than the 4-wave one)."""
     m = make(L, gpu, nb=nb, A=A, atype="Discrete" if A > 2 else "Semi_Discrete")
     obs, ava, rep, rand = inputs(m, B, L, gpu, A=A)
-    saved = mat_fused.WAVE_DECODE
-    res = {}
+    saved = mat_fused.WAVE_DECODE, mat_fused.SPEC_DECODE
+    res, paths = {}, {}
     try:
-        for wave in (True, False):
-            mat_fused.WAVE_DECODE = wave
+        for kind, wave, spec in (("spec", True, True), ("wave", True, False), ("4wave", False, False)):
+            mat_fused.WAVE_DECODE, mat_fused.SPEC_DECODE = wave, spec
             for _ in range(3):
                 mat_fused.decode(m, rep, ava, False, 1, None)
             torch.cuda.synchronize()
@@ -324,11 +329,16 @@ def test_wave_decode_latency(gpu, L, nb, A, B):
                 mat_fused.decode(m, rep, ava, False, 1, None)
             e.record()
             torch.cuda.synchronize()
-            res[wave] = s.elapsed_time(e) / 20 * 1e3
+            res[kind] = s.elapsed_time(e) / 20 * 1e3
+            paths[kind] = m._mdl_decode_path
     finally:
-        mat_fused.WAVE_DECODE = saved
+        mat_fused.WAVE_DECODE, mat_fused.SPEC_DECODE = saved
     from conftest import perf_record
-    perf_record(f"decode_wave_{B}x{L}_nb{nb}_A{A}_us", res[True], WAVE_BOUND_US[(L, nb, A, B)])
-    perf_record(f"decode_4wave_{B}x{L}_nb{nb}_A{A}_us", res[False], None)
-    assert res[True] < res[False] * 1.05, res
-    assert res[True] < WAVE_BOUND_US[(L, nb, A, B)], res
+    perf_record(f"decode_wave_{B}x{L}_nb{nb}_A{A}_us", res["wave"], WAVE_BOUND_US[(L, nb, A, B)])
+    perf_record(f"decode_4wave_{B}x{L}_nb{nb}_A{A}_us", res["4wave"], None)
+    assert res["wave"] < res["4wave"] * 1.05, res
+    assert res["wave"] < WAVE_BOUND_US[(L, nb, A, B)], res
+    if paths["spec"].startswith("spec"):
+        perf_record(f"decode_spec_{B}x{L}_nb{nb}_A{A}_us", res["spec"], SPEC_BOUND_US.get((L, nb, A, B)))
+        assert res["spec"] < res["wave"], res
+        assert res["spec"] < SPEC_BOUND_US.get((L, nb, A, B), 1e9), res
