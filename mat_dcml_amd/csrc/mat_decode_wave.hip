@@ -263,7 +263,8 @@ struct WvCtx {
 // one decoder block for the live row i (ma_transformer.py:95-98): x <- LN1(x + attn1(x)); x <- LN2(rep_i + attn2(q =
 // rep_i, k = v = x)); x <- LN3(x + mlp(x)).  Block 0's q / K / V of x come from the token table (x = ET[tok]).
 template <int B, int NB, int NLDS, int NREG>
-__device__ __forceinline__ void wv_block(CT& x, const WvCtx& k, const RegW<NREG>& rw, int i, int tok, const CT& repi) {
+__device__ __forceinline__ void wv_block(CT& x, const WvCtx& k, const RegW<NREG>& rw, int i, int tok, const CT& repi,
+                                         const CTr* q2in = nullptr) {
   const int lane = k.lane, g = lane >> 4, L = k.L;
   CT xh;
   AFr w;
@@ -318,7 +319,8 @@ __device__ __forceinline__ void wv_block(CT& x, const WvCtx& k, const RegW<NREG>
   {
     CTr q2;
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) q2.q[mt] = *(const uint2*)(k.Q2 + (size_t)(B * L + i) * 64 + 16 * mt + 4 * g);
+    for (int mt = 0; mt < 4; ++mt)
+      q2.q[mt] = q2in ? q2in->q[mt] : *(const uint2*)(k.Q2 + (size_t)(B * L + i) * 64 + 16 * mt + 4 * g);
     WDBG(6 * B + 2, x);
     const CT O = wv_attn(wv_cache(k.KV, B, 2, L), wv_cache(k.KV, B, 3, L), q2, i, lane);
     WDBG(6 * B + 3, O);
@@ -631,14 +633,18 @@ __global__ __launch_bounds__(64, 1) void mat_decode_wave_kernel(DecParams p) {
 // in LDS (the last NREG in its registers).  Rows of the candidate attention: keys 0..i-1 from the committed cache
 // (MFMA, as the one-wave kernel), the candidate's own key i from its registers (a per-column dot product), both
 // heads in separate score MFMAs (columns are no longer replicated).  Reference: transformer_act.py:76-99.
-struct SpLds { int w, kv, q2, qt, bi, lp, sc, slot, stg, tok, total; };
-__host__ __device__ inline SpLds sp_lds(int NB, int L, int n_tok, int nlds_main, int A) {
+// IND (long rows, L = 101): block 0's self-attention K / V rows are the token table's rows, so instead of two caches of
+// L rows the kernel keeps the row -> token array ROWTOK and reads K / V through it (25 KB less LDS at L = 101)
+struct SpLds { int w, kv, q2, qt, bi, lp, sc, slot, stg, tok, rowtok, total; };
+// Q2F (L = 129): no cross-attention query table either — the main wave computes block 1's query of its row from
+// W_q2 (one more LDS matrix), the speculative waves block 0's from a register copy of W_q2
+__host__ __device__ inline SpLds sp_lds(int NB, int L, int n_tok, int nlds_main, int A, bool ind, bool q2f = false) {
   SpLds o;
   int off = 0;
   auto take = [&](int bytes) { const int r = off; off += (bytes + 15) & ~15; return r; };
-  o.w = take(nlds_main * 8192);              // the main wave's LDS-resident matrices (blocks 1.., head)
-  o.kv = take((NB * 4 * L + 32) * 128);      // K / V caches (+ 32 zero rows)
-  o.q2 = take(NB * L * 128);                 // cross-attention queries
+  o.w = take((nlds_main + (q2f ? 1 : 0)) * 8192);   // the main wave's LDS-resident matrices (blocks 1.., head)
+  o.kv = take(((NB * 4 - (ind ? 2 : 0)) * L + 32) * 128);   // K / V caches (+ 32 zero rows)
+  o.q2 = take(q2f ? 0 : NB * L * 128);       // cross-attention queries
   o.qt = take(n_tok * 3 * 128);              // block-0 q / k / v of every token
   o.bi = take((10 * NB + 1) * 256);
   o.lp = take((3 * NB + 1) * 512);
@@ -646,6 +652,7 @@ __host__ __device__ inline SpLds sp_lds(int NB, int L, int n_tok, int nlds_main,
   o.slot = take(2 * A * 256);                // [parity][candidate][64] f32 block-0 outputs
   o.stg = take(2 * A * 256);                 // [parity][candidate][K, V][64] bf16 cross-attention cache rows
   o.tok = take(16);                          // [parity] token of the next row
+  o.rowtok = take(ind ? ((L + 31) & ~31) * 4 : 0);   // IND: input token of every committed row (0 beyond)
   o.total = off;
   return o;
 }
@@ -653,8 +660,31 @@ __host__ __device__ inline SpLds sp_lds(int NB, int L, int n_tok, int nlds_main,
 // Causal attention of row i for the wave's 16 candidates (column c): keys 0..i-1 from the committed caches, key i the
 // candidate's own (ks, vs).  Online softmax per head in log2 units, seeded with the own key (score m, weight 1,
 // value vs), so every row has a finite running max and no chunk needs a FIRST special case.
-__device__ __forceinline__ CT sp_attn(const bf16_t* Kc, const bf16_t* Vc, const CTr& q, const CTr& ks, const CTr& vs,
-                                      int i, int lane) {
+// K / V row sources of the committed keys: a swizzled cache (SpCache) or, IND, the token table through ROWTOK
+struct SpCache {
+  const bf16_t *K, *V;
+  __device__ __forceinline__ uint2 k4(int row, int col) const { return kv_ld2(K, row, col); }
+  __device__ __forceinline__ bf16x8 vT(int kb, int n0, int lane) const { return ld_frag_T(V + kb * 64, 0, n0, lane); }
+};
+struct SpTokRows {
+  const bf16_t* QT;
+  const int* rowtok;
+  __device__ __forceinline__ uint2 k4(int row, int col) const {
+    return *(const uint2*)(QT + rowtok[row] * 192 + 64 + col);
+  }
+  // ld_frag_T over rows kb + 8g + (c >> 2) (+ 4) of the V table rows: every lane addresses its own row
+  __device__ __forceinline__ bf16x8 vT(int kb, int n0, int lane) const {
+    const int g = lane >> 4, c = lane & 15, col = n0 + 4 * (c & 3);
+    const int r0 = kb + 8 * g + (c >> 2);
+    const s16x4 lo = ld_tr(QT + rowtok[r0] * 192 + 128 + col), hi = ld_tr(QT + rowtok[r0 + 4] * 192 + 128 + col);
+    bf16x8 f;
+    f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+    f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+    return f;
+  }
+};
+template <class KVS>
+__device__ __forceinline__ CT sp_attn(const KVS& kvs, const CTr& q, const CTr& ks, const CTr& vs, int i, int lane) {
   const int g = lane >> 4, c = lane & 15;
   float m[2], l[2];
   f32x4 o[4];
@@ -671,13 +701,12 @@ __device__ __forceinline__ CT sp_attn(const bf16_t* Kc, const bf16_t* Vc, const 
   }
   const bf16x8 qb0 = rb(q, 0), qb1 = rb(q, 1);
   for (int kb = 0; kb < i; kb += 32) {
-    const bf16_t* Kk = Kc + kb * 64;
     float sc[2][8];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      const int key = pi_row(t, c);
-      const uint2 p0 = kv_ld2(Kk, key, 4 * g), p1 = kv_ld2(Kk, key, 16 + 4 * g);
-      const uint2 p2 = kv_ld2(Kk, key, 32 + 4 * g), p3 = kv_ld2(Kk, key, 48 + 4 * g);
+      const int key = kb + pi_row(t, c);
+      const uint2 p0 = kvs.k4(key, 4 * g), p1 = kvs.k4(key, 16 + 4 * g);
+      const uint2 p2 = kvs.k4(key, 32 + 4 * g), p3 = kvs.k4(key, 48 + 4 * g);
       const f32x4 z = {0.f, 0.f, 0.f, 0.f};
       const f32x4 r0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(mk8(p0.x, p0.y, p1.x, p1.y), qb0, z, 0, 0, 0);
       const f32x4 r1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(mk8(p2.x, p2.y, p3.x, p3.y), qb1, z, 0, 0, 0);
@@ -710,7 +739,7 @@ __device__ __forceinline__ CT sp_attn(const bf16_t* Kc, const bf16_t* Vc, const 
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int mt = 2 * h + u;
-        const bf16x8 va = ld_frag_T(Vc + kb * 64, 0, 16 * mt, lane);
+        const bf16x8 va = kvs.vT(kb, 16 * mt, lane);
         o[mt] *= alpha;
         o[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, ph, o[mt], 0, 0, 0);
         o[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pl, o[mt], 0, 0, 0);
@@ -730,12 +759,14 @@ __device__ __forceinline__ CT sp_attn(const bf16_t* Kc, const bf16_t* Vc, const 
 
 // block 0 (ma_transformer.py:95-98) of row i for the wave's 16 candidates: x = the candidates' embedded input rows in,
 // block 0's output out; kp / vp = their cross-attention K / V rows (staged for the commit)
+template <class KVS>
 __device__ __forceinline__ void sp_block0(CT& x, const CTr& cq, const CTr& ck, const CTr& cv, const RegW<6>& w0,
-                                          const WvCtx& k, int i, const CT& repi, CTr& kp, CTr& vp) {
+                                          const WvCtx& k, const KVS& selfkv, int i, const CT& repi, const CTr& q2,
+                                          CTr& kp, CTr& vp) {
   const int lane = k.lane, g = lane >> 4, L = k.L;
   CT xh;
   {
-    const CT O = sp_attn(wv_cache(k.KV, 0, 0, L), wv_cache(k.KV, 0, 1, L), cq, ck, cv, i, lane);
+    const CT O = sp_attn(selfkv, cq, ck, cv, i, lane);
     CT t = ct_add(ld_vec(k.BI + 64 * 3, lane), x);
     mm(t, w0.w[0], ct_pack(O));
     ln_fwd_ct(t, xh, x, ld_vec(k.LP, lane), ld_vec(k.LP + 64, lane));
@@ -749,10 +780,7 @@ __device__ __forceinline__ void sp_block0(CT& x, const CTr& cq, const CTr& ck, c
     vp = ct_pack(vv);
   }
   {
-    CTr q2;
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) q2.q[mt] = *(const uint2*)(k.Q2 + (size_t)i * 64 + 16 * mt + 4 * g);
-    const CT O = sp_attn(wv_cache(k.KV, 0, 2, L), wv_cache(k.KV, 0, 3, L), q2, kp, vp, i, lane);
+    const CT O = sp_attn(SpCache{wv_cache(k.KV, 0, 2, L), wv_cache(k.KV, 0, 3, L)}, q2, kp, vp, i, lane);
     CT t = ct_add(ld_vec(k.BI + 64 * 7, lane), repi);
     mm(t, w0.w[3], ct_pack(O));
     ln_fwd_ct(t, xh, x, ld_vec(k.LP + 128, lane), ld_vec(k.LP + 128 + 64, lane));
@@ -783,7 +811,14 @@ __device__ __forceinline__ SpCand sp_cand(const bf16_t* QT, const float* emb, in
   return cd;
 }
 
-template <int NB, int NS, int NREG, int MA>
+// q2 = W_q2 rep + b (bf16) of one row: the query table's values, computed in place (Q2F)
+__device__ __forceinline__ CTr sp_q2(const AFr& wq, const float* bias, const CT& repr, int lane) {
+  CT q = ld_vec(bias, lane);
+  mm(q, wq, ct_pack(repr));
+  return ct_pack(q);
+}
+
+template <int NB, int NS, int NREG, int MA, bool IND, bool Q2F>
 __global__ __launch_bounds__(64 * (1 + NS), 1) void mat_decode_spec_kernel(DecParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NM = wv_nm(NB), NMM = NM - 6, NLDS = NM - NREG;   // main: slots 6 .. NM - 1, LDS: 6 .. NLDS - 1
@@ -791,9 +826,11 @@ __global__ __launch_bounds__(64 * (1 + NS), 1) void mat_decode_spec_kernel(DecPa
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, c = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int env = blockIdx.x, L = p.L, A = p.act_dim;
-  const SpLds lo = sp_lds(NB, L, p.n_tok, NMM - NREG, A);
+  static_assert(!Q2F || NB == 2, "Q2F: n_block 2");
+  const SpLds lo = sp_lds(NB, L, p.n_tok, NMM - NREG, A, IND, Q2F);
   bf16_t* Wl = (bf16_t*)(smem + lo.w);
-  bf16_t* KV = (bf16_t*)(smem + lo.kv);
+  bf16_t* KV = (bf16_t*)(smem + lo.kv) - (IND ? 2 * L * 64 : 0);   // IND: no block-0 self K / V caches (kinds 0, 1)
+  int* ROWTOK = (int*)(smem + lo.rowtok);
   bf16_t* Q2 = (bf16_t*)(smem + lo.q2);
   bf16_t* QT = (bf16_t*)(smem + lo.qt);
   float* BI = (float*)(smem + lo.bi);
@@ -805,16 +842,22 @@ __global__ __launch_bounds__(64 * (1 + NS), 1) void mat_decode_spec_kernel(DecPa
   const float* rep = p.rep + (size_t)env * L * 64;
 
   // ---------------------------------------------------------------- setup (all waves)
-  for (int e = tid; e < (NLDS - 6) * 512; e += NT) {
+  for (int e = tid; e < (NLDS - 6 + (Q2F ? 1 : 0)) * 512; e += NT) {
     const int sl = 6 + e / 512, j = e % 512;
-    ((uint4*)(Wl + (size_t)(sl - 6) * 4096))[j] = ((const uint4*)(p.wfa + (size_t)wv_lin(NB, sl) * 4096))[j];
+    const int lin = sl < NLDS ? wv_lin(NB, sl) : 10 * 1 + 4;   // Q2F: block 1's W_q2 after the main wave's slots
+    ((uint4*)(Wl + (size_t)(sl - 6) * 4096))[j] = ((const uint4*)(p.wfa + (size_t)lin * 4096))[j];
   }
   for (int e = tid; e < p.n_tok * 192; e += NT) QT[e] = f2bf(p.qkv0[e]);
   for (int e = tid; e < (10 * NB + 1) * 64; e += NT) BI[e] = p.bias[e];
   for (int e = tid; e < (3 * NB + 1) * 128; e += NT) LP[e] = p.lnp[e];
-  for (int e = tid * 8; e < (NB * 4 * L + 32) * 64; e += NT * 8) *(uint4*)(KV + e) = make_uint4(0, 0, 0, 0);
-  // cross-attention queries q2 = W_q2 rep + b of every row and block, 16-row tiles spread over the waves
   {
+    bf16_t* kv0 = (bf16_t*)(smem + lo.kv);
+    for (int e = tid * 8; e < ((NB * 4 - (IND ? 2 : 0)) * L + 32) * 64; e += NT * 8) *(uint4*)(kv0 + e) = make_uint4(0, 0, 0, 0);
+    if constexpr (IND)
+      for (int e = tid; e < ((L + 31) & ~31); e += NT) ROWTOK[e] = 0;
+  }
+  // cross-attention queries q2 = W_q2 rep + b of every row and block, 16-row tiles spread over the waves
+  if constexpr (!Q2F) {
     const int ntile = (L + 15) >> 4;
     for (int jt = wave; jt < NB * ntile; jt += 1 + NS) {
       const int b = jt / ntile, t0 = 16 * (jt % ntile);
@@ -852,7 +895,14 @@ __global__ __launch_bounds__(64 * (1 + NS), 1) void mat_decode_spec_kernel(DecPa
       const CT repi = ld_vec(rep + (size_t)i * 64, lane);
       const float avl = (ava && lane < A) ? ava[(size_t)i * A + lane] : 1.f;
       CT x = ld_vec(SLOT + (size_t)((i & 1) * A + (i == 0 ? 0 : tok - 1)) * 64, lane);
-      if constexpr (NB > 1) wv_block<1, NB, NLDS, NREG>(x, k, rw, i, tok, repi);
+      if constexpr (Q2F) {
+        AFr wq;
+        wv_getw<0, 1, 0>(wq, RegW<0>{}, Wl + (size_t)(NLDS - 6) * 4096, lane);
+        const CTr q2 = sp_q2(wq, BI + 64 * (10 * 1 + 4), repi, lane);
+        wv_block<1, NB, NLDS, NREG>(x, k, rw, i, tok, repi, &q2);
+      } else if constexpr (NB > 1) {
+        wv_block<1, NB, NLDS, NREG>(x, k, rw, i, tok, repi);
+      }
       tok = wv_head_sample<NM, NLDS, NREG, MA>(x, hw, nz, rw, k.W, BI, SC, p, env, i, avl, tok, lane);
       if (lane == 0) TOK[(i + 1) & 1] = tok;
       __syncthreads();   // (2) token of row i + 1 published; block 0 of row i + 1 staged for every candidate
@@ -862,6 +912,22 @@ __global__ __launch_bounds__(64 * (1 + NS), 1) void mat_decode_spec_kernel(DecPa
     RegW<6> w0;
 #pragma unroll
     for (int r = 0; r < 6; ++r) loadA(w0.w[r], p.wfa + (size_t)wv_lin(NB, r) * 4096, lane);
+    RegW<Q2F ? 1 : 0> wq0;   // Q2F: block 0's W_q2
+    if constexpr (Q2F) loadA(wq0.w[0], p.wfa + (size_t)4 * 4096, lane);
+    auto q2row = [&](int row, const CT& repr) {
+      CTr q2;
+      if constexpr (Q2F) {
+        q2 = sp_q2(wq0.w[0], BI + 64 * 4, repr, lane);
+      } else {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) q2.q[mt] = *(const uint2*)(Q2 + (size_t)row * 64 + 16 * mt + 4 * g);
+      }
+      return q2;
+    };
+    const auto selfkv = [&] {
+      if constexpr (IND) return SpTokRows{QT, ROWTOK};
+      else return SpCache{wv_cache(KV, 0, 0, L), wv_cache(KV, 0, 1, L)};
+    }();
     const int cand = 16 * (wave - 1) + c;   // this lane's candidate: input token 1 + cand (rows >= 1)
     const bool own = cand < A;
     auto stage = [&](int par, const CT& x, const CTr& kp, const CTr& vp) {
@@ -880,7 +946,8 @@ __global__ __launch_bounds__(64 * (1 + NS), 1) void mat_decode_spec_kernel(DecPa
       const SpCand c0 = sp_cand(QT, p.emb, p.tok_start, lane);
       CT x = c0.e;
       CTr kp, vp;
-      sp_block0(x, c0.q, c0.k, c0.v, w0, k, 0, ld_vec(rep, lane), kp, vp);
+      const CT rep0 = ld_vec(rep, lane);
+      sp_block0(x, c0.q, c0.k, c0.v, w0, k, selfkv, 0, rep0, q2row(0, rep0), kp, vp);
       stage(0, x, kp, vp);
     }
     const SpCand cd = sp_cand(QT, p.emb, min(1 + cand, p.n_tok - 1), lane);
@@ -891,7 +958,8 @@ __global__ __launch_bounds__(64 * (1 + NS), 1) void mat_decode_spec_kernel(DecPa
       // commit row i of the block-0 caches: the token's self-attention K / V table rows and the staged cross K / V
       // rows of its candidate; lane (kind, 16-byte chunk), kinds 0..3 = self K, self V, cross K, cross V
       const int tk = TOK[i & 1];
-      if (lane < 32) {
+      if (IND && lane == 0) ROWTOK[i] = tk;
+      if (lane < 32 && (!IND || lane >= 16)) {
         const int kind = lane >> 3, ch = lane & 7;
         const bf16_t* src = kind < 2 ? QT + tk * 192 + 64 * (kind + 1) + 8 * ch
                                      : STG + (size_t)((i & 1) * A + (i == 0 ? 0 : tk - 1)) * 128 + 64 * (kind - 2) + 8 * ch;
@@ -901,7 +969,7 @@ __global__ __launch_bounds__(64 * (1 + NS), 1) void mat_decode_spec_kernel(DecPa
       if (i + 1 < L) {
         CT x = cd.e;
         CTr kp, vp;
-        sp_block0(x, cd.q, cd.k, cd.v, w0, k, i + 1, repn, kp, vp);
+        sp_block0(x, cd.q, cd.k, cd.v, w0, k, selfkv, i + 1, repn, q2row(i + 1, repn), kp, vp);
         stage((i + 1) & 1, x, kp, vp);
       }
       __syncthreads();   // (2)
@@ -909,12 +977,12 @@ __global__ __launch_bounds__(64 * (1 + NS), 1) void mat_decode_spec_kernel(DecPa
   }
 }
 
-template <int NB, int NS, int NREG, int MA>
+template <int NB, int NS, int NREG, int MA, bool IND = false, bool Q2F = false>
 int sp_launch(const DecParams* p, size_t lds, hipStream_t st) {
-  hipError_t e = hipFuncSetAttribute((const void*)mat_decode_spec_kernel<NB, NS, NREG, MA>,
+  hipError_t e = hipFuncSetAttribute((const void*)mat_decode_spec_kernel<NB, NS, NREG, MA, IND, Q2F>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return -(int)e;
-  hipLaunchKernelGGL((mat_decode_spec_kernel<NB, NS, NREG, MA>), dim3(p->B), dim3(64 * (1 + NS)), lds, st, *p);
+  hipLaunchKernelGGL((mat_decode_spec_kernel<NB, NS, NREG, MA, IND, Q2F>), dim3(p->B), dim3(64 * (1 + NS)), lds, st, *p);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : -(int)e;
 }
@@ -956,11 +1024,15 @@ MDL_API int mdl_wave_debug_read(float* out, int row) {
 // stride 1) of the Discrete / Semi_Discrete(-1) action types with the block-0 token table and the folded head,
 // n_block 1 or 2, L up to what the LDS carve holds (weights beyond it in registers, at most 6 matrices).
 // Returns the number of register-resident weight matrices of the launch it would make, or -1 (not on this path).
+static bool wv_eligible(const DecParams* p, int NB) {
+  if (!p->wfa || p->cont || p->avail_cont || !p->qkv0 || !p->hfold || !p->rep || p->epw != 1) return false;
+  if (NB < 1 || NB > 2 || p->act_dim < 1 || p->act_dim > 64 || p->stride != 1 || p->L < 1 || p->L > 192) return false;
+  if (p->n_disc != p->L && p->n_disc != p->L - 1) return false;
+  if (!p->deterministic && !p->gen && (!p->rnd_u || (p->n_disc < p->L && !p->rnd_n))) return false;
+  return true;
+}
 MDL_API int mdl_decode_wave_plan(const DecParams* p, int NB) {
-  if (!p->wfa || p->cont || p->avail_cont || !p->qkv0 || !p->hfold || !p->rep || p->epw != 1) return -1;
-  if (NB < 1 || NB > 2 || p->act_dim < 1 || p->act_dim > 64 || p->stride != 1 || p->L < 1 || p->L > 192) return -1;
-  if (p->n_disc != p->L && p->n_disc != p->L - 1) return -1;
-  if (!p->deterministic && !p->gen && (!p->rnd_u || (p->n_disc < p->L && !p->rnd_n))) return -1;
+  if (!wv_eligible(p, NB)) return -1;
   for (int nreg = 0; nreg <= (NB == 1 ? 4 : 6); nreg += 2)
     if (wv_lds(NB, p->L, p->n_tok, wv_nm(NB) - nreg, p->act_dim > 4).total <= 160 * 1024) return nreg;
   return -1;
@@ -979,19 +1051,30 @@ static bool spec_enabled() {
   return g_spec_enable != 0;
 }
 MDL_API int mdl_decode_spec_plan(const DecParams* p, int NB) {
-  if (!spec_enabled() || NB != 2 || mdl_decode_wave_plan(p, NB) < 0 || p->act_dim > 48) return -1;
+  if (!spec_enabled() || NB != 2 || !wv_eligible(p, NB) || p->act_dim > 48) return -1;
   if (p->n_tok < p->act_dim + 1) return -1;
   const int nmm = wv_nm(NB) - 6;
   static const int minreg = [] { const char* e = getenv("MAT_DCML_SPEC_NREG"); return e ? atoi(e) : 4; }();
   for (int nreg = minreg; nreg <= 6; nreg += 2)
-    if (sp_lds(NB, p->L, p->n_tok, nmm - nreg, p->act_dim).total <= 160 * 1024) return nreg;
+    if (sp_lds(NB, p->L, p->n_tok, nmm - nreg, p->act_dim, false).total <= 160 * 1024) return nreg;
+  // long rows (A <= 4): block 0's self K / V through the token table (+ 8 marks the IND layout), then without the
+  // query table as well (+ 16: Q2F)
+  if (p->act_dim <= 4) {
+    for (int nreg = 4; nreg <= 6; nreg += 2)
+      if (sp_lds(NB, p->L, p->n_tok, nmm - nreg, p->act_dim, true).total <= 160 * 1024) return 8 + nreg;
+    if (sp_lds(NB, p->L, p->n_tok, nmm - 6, p->act_dim, true, true).total <= 160 * 1024) return 16 + 8 + 6;
+  }
   return -1;
 }
 static int mdl_decode_spec(const DecParams* p, int NB, hipStream_t st) {
-  const int nreg = mdl_decode_spec_plan(p, NB);
+  int nreg = mdl_decode_spec_plan(p, NB);
   if (nreg < 0) return 1;
+  const bool ind = nreg & 8, q2f = nreg & 16;
+  nreg &= 7;
   const int A = p->act_dim, NS = (A + 15) / 16;
-  const size_t lds = (size_t)sp_lds(NB, p->L, p->n_tok, wv_nm(NB) - 6 - nreg, A).total;
+  const size_t lds = (size_t)sp_lds(NB, p->L, p->n_tok, wv_nm(NB) - 6 - nreg, A, ind, q2f).total;
+  if (q2f) return sp_launch<2, 1, 6, 1, true, true>(p, lds, st);
+  if (ind) return nreg == 4 ? sp_launch<2, 1, 4, 1, true>(p, lds, st) : sp_launch<2, 1, 6, 1, true>(p, lds, st);
   if (A <= 4) return sp_launch_nreg<1, 1>(p, nreg, lds, st);
   if (NS == 1) return sp_launch_nreg<1, 3>(p, nreg, lds, st);
   if (NS == 2) return sp_launch_nreg<2, 3>(p, nreg, lds, st);

@@ -282,7 +282,7 @@ def wave_path(prm, n_block):
     register-resident), 'wave(nreg=k)' on the one-wave kernel, else '4wave'."""
     k = lib().mdl_decode_spec_plan(ctypes.byref(prm), n_block)
     if k >= 0:
-        return f"spec(nreg={k})"
+        return f"spec(nreg={k & 7}{', tokrows' if k & 8 else ''}{', q2inline' if k & 16 else ''})"
     k = lib().mdl_decode_wave_plan(ctypes.byref(prm), n_block)
     return f"wave(nreg={k})" if k >= 0 else "4wave"
 

@@ -128,7 +128,7 @@ def test_decode_discrete_smac_shape(gpu, det):
 
 
 # 1.10 x the round-5 measurements taken exactly this way (profiles/r5_final/perf_guards.jsonl)
-DECODE_BOUND_US = {33: 175.0, 101: 1138.0}   # 159.2 (speculative kernel) / 1034.6 us measured
+DECODE_BOUND_US = {33: 175.0, 101: 598.0}   # 159.2 / 543.8 us measured (speculative kernel)
 
 
 @pytest.mark.parametrize("L", [33, 101])
@@ -279,6 +279,31 @@ def test_wave_decode_matches_4wave_and_torch(gpu, L, B, nb, atype, A, det, spec)
         assert (a_4[same, -1] - a_w[same, -1]).abs().max().item() < 5e-2
 
 
+@pytest.mark.parametrize("L,q2inline", [(101, False), (129, True)])
+@pytest.mark.parametrize("det", [False, True])
+def test_spec_decode_long_rows_token_table(gpu, det, L, q2inline):
+    """256 x 101 with n_block 2: both blocks' K / V caches do not fit next to the speculative kernel's other operands,
+    so block 0's self-attention K / V are read through the row -> token array from the token table ('tokrows'); at
+    L = 129 the cross-attention queries are computed in place as well ('q2inline').  Same checks as the one-wave
+    parity test."""
+    B = 64
+    m = make(L, gpu, seed=13)
+    obs, ava, rep, rand = inputs(m, B, L, gpu)
+    path, a_s, lp_s, a_4, lp_4 = _both_kernels(m, rep, ava, det, rand, spec=True)
+    assert path.startswith("spec") and "tokrows" in path and ("q2inline" in path) == q2inline, path
+    a_ref, _ = act.autoregressive_act(m, rep, obs, ava, det, 1, rand)
+    n_disc = L - 1
+    for other in (a_4, a_ref):
+        eq = (other[:, :n_disc] == a_s[:, :n_disc]).squeeze(-1).float()
+        same_prefix = torch.cat([torch.ones_like(eq[:, :1]), torch.cumprod(eq, 1)[:, :-1]], 1)
+        rate = ((1 - eq) * same_prefix).sum().item() / same_prefix.sum().item()
+        assert rate < 0.02, rate
+    with torch.no_grad():
+        lp_tf, _ = act.parallel_act(m, rep, obs, a_s, ava)
+    err = (lp_tf - lp_s).abs()
+    assert err.mean().item() < 2e-2 and err.max().item() < 0.2, (err.mean().item(), err.max().item())
+
+
 def test_wave_decode_inkernel_draws_match_4wave(gpu):
     """rand=None (in-kernel Philox keyed by env / row / call counter): both kernels draw the same noise, so with the
     same key they take the same decisions except at bf16 near-ties."""
@@ -305,11 +330,12 @@ def test_wave_decode_inkernel_draws_match_4wave(gpu):
 
 # one-wave kernel bounds: 1.10 x the round-5 measurements (251.8 / 448.1 / 215.1 us, profiles/r5_final/perf_guards.jsonl)
 WAVE_BOUND_US = {(33, 2, 2, 256): 277.0, (101, 1, 2, 256): 493.0, (27, 2, 36, 32): 237.0}
-# speculative-block-0 kernel (the default rollout path at these shapes): 1.10 x 157.1 / 139.8 us measured
-SPEC_BOUND_US = {(33, 2, 2, 256): 173.0, (27, 2, 36, 32): 154.0}
+# speculative-block-0 kernel (the default rollout path at these shapes): 1.10 x 157.1 / 139.8 / 544.5 / 749.4 us
+SPEC_BOUND_US = {(33, 2, 2, 256): 173.0, (27, 2, 36, 32): 154.0, (101, 2, 2, 256): 599.0, (129, 2, 2, 256): 824.0}
 
 
-@pytest.mark.parametrize("L,nb,A,B", [(33, 2, 2, 256), (101, 1, 2, 256), (27, 2, 36, 32)])
+@pytest.mark.parametrize("L,nb,A,B", [(33, 2, 2, 256), (101, 1, 2, 256), (27, 2, 36, 32), (101, 2, 2, 256),
+                                      (129, 2, 2, 256)])
 def test_wave_decode_latency(gpu, L, nb, A, B):
     """Per-env-step decode time of both kernels at the rollout shapes (printed; the one-wave kernel must not be
     slower than the 4-wave one)."""
@@ -334,11 +360,12 @@ def test_wave_decode_latency(gpu, L, nb, A, B):
     finally:
         mat_fused.WAVE_DECODE, mat_fused.SPEC_DECODE = saved
     from conftest import perf_record
-    perf_record(f"decode_wave_{B}x{L}_nb{nb}_A{A}_us", res["wave"], WAVE_BOUND_US[(L, nb, A, B)])
     perf_record(f"decode_4wave_{B}x{L}_nb{nb}_A{A}_us", res["4wave"], None)
-    assert res["wave"] < res["4wave"] * 1.05, res
-    assert res["wave"] < WAVE_BOUND_US[(L, nb, A, B)], res
+    if paths["wave"].startswith("wave"):
+        perf_record(f"decode_wave_{B}x{L}_nb{nb}_A{A}_us", res["wave"], WAVE_BOUND_US[(L, nb, A, B)])
+        assert res["wave"] < res["4wave"] * 1.05, res
+        assert res["wave"] < WAVE_BOUND_US[(L, nb, A, B)], res
     if paths["spec"].startswith("spec"):
         perf_record(f"decode_spec_{B}x{L}_nb{nb}_A{A}_us", res["spec"], SPEC_BOUND_US.get((L, nb, A, B)))
-        assert res["spec"] < res["wave"], res
+        assert res["spec"] < min(res["wave"], res["4wave"]), res
         assert res["spec"] < SPEC_BOUND_US.get((L, nb, A, B), 1e9), res
