@@ -992,6 +992,9 @@ int sp_launch_nreg(const DecParams* p, int nreg, size_t lds, hipStream_t st) {
     case 2: return sp_launch<2, NS, 2, MA>(p, lds, st);
     case 4: return sp_launch<2, NS, 4, MA>(p, lds, st);
     case 6: return sp_launch<2, NS, 6, MA>(p, lds, st);
+    case 8:   // the narrow head only (465 VGPRs; the wide head's folded logit fragments spill with 8)
+      if constexpr (MA == 1) return sp_launch<2, NS, 8, MA>(p, lds, st);
+      return -1;
     default: return sp_launch<2, NS, 0, MA>(p, lds, st);
   }
 }
@@ -1043,6 +1046,9 @@ MDL_API int mdl_decode_wave_plan(const DecParams* p, int NB) {
 // Returns the number of register-resident main-wave matrices, or -1 (not on this path).
 static int g_spec_enable = -1;
 MDL_API void mdl_decode_spec_enable(int on) { g_spec_enable = on; }
+// tests: 1 = the token-table layout, 2 = token table + in-place queries even where the plain carve fits; 0 = auto
+static int g_spec_layout = 0;
+MDL_API void mdl_decode_spec_layout(int v) { g_spec_layout = v; }
 static bool spec_enabled() {
   if (g_spec_enable < 0) {
     const char* e = getenv("MAT_DCML_DECODE_SPEC");
@@ -1054,23 +1060,34 @@ MDL_API int mdl_decode_spec_plan(const DecParams* p, int NB) {
   if (!spec_enabled() || NB != 2 || !wv_eligible(p, NB) || p->act_dim > 48) return -1;
   if (p->n_tok < p->act_dim + 1) return -1;
   const int nmm = wv_nm(NB) - 6;
-  static const int minreg = [] { const char* e = getenv("MAT_DCML_SPEC_NREG"); return e ? atoi(e) : 4; }();
-  for (int nreg = minreg; nreg <= 6; nreg += 2)
+  // register-resident main-wave matrices, in the order measured fastest (scripts/r5_nreg.sh, profiles/r5_spec):
+  // narrow head (DCML) 0 < 8 < 2 < 6 < 4 (148.8 / 150.1 / 153.5 / 155.6 / 157.9 us at 256 x 33; 8 also beats the
+  // token-table layout at 256 x 101, 530.6 vs 541 us); wide head (SMAC) 6 < 4 (134.1 / 139.8 us).
+  // MAT_DCML_SPEC_NREG=k forces k when it fits.
+  static const int force = [] { const char* e = getenv("MAT_DCML_SPEC_NREG"); return e ? atoi(e) : -1; }();
+  static const int narrow[] = {0, 8, 2, 6, 4}, wide[] = {6, 4, 2, 0};
+  const bool nar = p->act_dim <= 4;
+  const int* order = nar ? narrow : wide;
+  const int norder = nar ? 5 : 4;
+  for (int j = -1; j < norder && g_spec_layout == 0; ++j) {
+    const int nreg = j < 0 ? force : order[j];
+    if (nreg < 0 || nreg > (nar ? 8 : 6) || (nreg & 1)) continue;
     if (sp_lds(NB, p->L, p->n_tok, nmm - nreg, p->act_dim, false).total <= 160 * 1024) return nreg;
-  // long rows (A <= 4): block 0's self K / V through the token table (+ 8 marks the IND layout), then without the
-  // query table as well (+ 16: Q2F)
+  }
+  // long rows (A <= 4): block 0's self K / V through the token table (+ 16 marks the IND layout), then without the
+  // query table as well (+ 32: Q2F)
   if (p->act_dim <= 4) {
-    for (int nreg = 4; nreg <= 6; nreg += 2)
-      if (sp_lds(NB, p->L, p->n_tok, nmm - nreg, p->act_dim, true).total <= 160 * 1024) return 8 + nreg;
-    if (sp_lds(NB, p->L, p->n_tok, nmm - 6, p->act_dim, true, true).total <= 160 * 1024) return 16 + 8 + 6;
+    for (int nreg = 4; nreg <= 6 && g_spec_layout <= 1; nreg += 2)
+      if (sp_lds(NB, p->L, p->n_tok, nmm - nreg, p->act_dim, true).total <= 160 * 1024) return 16 + nreg;
+    if (sp_lds(NB, p->L, p->n_tok, nmm - 6, p->act_dim, true, true).total <= 160 * 1024) return 32 + 16 + 6;
   }
   return -1;
 }
 static int mdl_decode_spec(const DecParams* p, int NB, hipStream_t st) {
   int nreg = mdl_decode_spec_plan(p, NB);
   if (nreg < 0) return 1;
-  const bool ind = nreg & 8, q2f = nreg & 16;
-  nreg &= 7;
+  const bool ind = nreg & 16, q2f = nreg & 32;
+  nreg &= 15;
   const int A = p->act_dim, NS = (A + 15) / 16;
   const size_t lds = (size_t)sp_lds(NB, p->L, p->n_tok, wv_nm(NB) - 6 - nreg, A, ind, q2f).total;
   if (q2f) return sp_launch<2, 1, 6, 1, true, true>(p, lds, st);

@@ -37,6 +37,7 @@ sig("mdl_mat_decode_geometry", i32, i32, i32)
 sig("mdl_decode_wave_plan", ctypes.POINTER(DecParams), i32)
 sig("mdl_decode_spec_plan", ctypes.POINTER(DecParams), i32)
 sig("mdl_decode_spec_enable", i32)
+sig("mdl_decode_spec_layout", i32)
 
 
 def _is_cont(model):
@@ -282,7 +283,7 @@ def wave_path(prm, n_block):
     register-resident), 'wave(nreg=k)' on the one-wave kernel, else '4wave'."""
     k = lib().mdl_decode_spec_plan(ctypes.byref(prm), n_block)
     if k >= 0:
-        return f"spec(nreg={k & 7}{', tokrows' if k & 8 else ''}{', q2inline' if k & 16 else ''})"
+        return f"spec(nreg={k & 15}{', tokrows' if k & 16 else ''}{', q2inline' if k & 32 else ''})"
     k = lib().mdl_decode_wave_plan(ctypes.byref(prm), n_block)
     return f"wave(nreg={k})" if k >= 0 else "4wave"
 

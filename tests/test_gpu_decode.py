@@ -128,7 +128,7 @@ def test_decode_discrete_smac_shape(gpu, det):
 
 
 # 1.10 x the round-5 measurements taken exactly this way (profiles/r5_final/perf_guards.jsonl)
-DECODE_BOUND_US = {33: 175.0, 101: 598.0}   # 159.2 / 543.8 us measured (speculative kernel)
+DECODE_BOUND_US = {33: 166.0, 101: 584.0}   # 150.7 / 530.4 us measured (speculative kernel)
 
 
 @pytest.mark.parametrize("L", [33, 101])
@@ -279,18 +279,26 @@ def test_wave_decode_matches_4wave_and_torch(gpu, L, B, nb, atype, A, det, spec)
         assert (a_4[same, -1] - a_w[same, -1]).abs().max().item() < 5e-2
 
 
-@pytest.mark.parametrize("L,q2inline", [(101, False), (129, True)])
+@pytest.mark.parametrize("L,layout", [(101, 0), (101, 1), (101, 2), (129, 0)])
 @pytest.mark.parametrize("det", [False, True])
-def test_spec_decode_long_rows_token_table(gpu, det, L, q2inline):
+def test_spec_decode_long_rows_token_table(gpu, det, L, layout):
     """256 x 101 with n_block 2: both blocks' K / V caches do not fit next to the speculative kernel's other operands,
     so block 0's self-attention K / V are read through the row -> token array from the token table ('tokrows'); at
-    L = 129 the cross-attention queries are computed in place as well ('q2inline').  Same checks as the one-wave
-    parity test."""
+    L = 129 the cross-attention queries are computed in place as well ('q2inline').  At L = 101 the plain carve fits
+    with 8 register-resident main-wave matrices (the default there); layout 1 / 2 force the token-table variants
+    (mdl_decode_spec_layout).  Same checks as the one-wave parity test."""
     B = 64
     m = make(L, gpu, seed=13)
     obs, ava, rep, rand = inputs(m, B, L, gpu)
-    path, a_s, lp_s, a_4, lp_4 = _both_kernels(m, rep, ava, det, rand, spec=True)
-    assert path.startswith("spec") and "tokrows" in path and ("q2inline" in path) == q2inline, path
+    from mat_dcml_amd.ops.kernels import lib
+    lib().mdl_decode_spec_layout(layout)
+    try:
+        path, a_s, lp_s, a_4, lp_4 = _both_kernels(m, rep, ava, det, rand, spec=True)
+    finally:
+        lib().mdl_decode_spec_layout(0)
+    want = {0: "q2inline" if L == 129 else "", 1: "tokrows", 2: "q2inline"}[layout]
+    assert path.startswith("spec") and want in path, path
+    assert ("tokrows" in path) == (layout > 0 or L == 129), path
     a_ref, _ = act.autoregressive_act(m, rep, obs, ava, det, 1, rand)
     n_disc = L - 1
     for other in (a_4, a_ref):
@@ -330,8 +338,8 @@ def test_wave_decode_inkernel_draws_match_4wave(gpu):
 
 # one-wave kernel bounds: 1.10 x the round-5 measurements (251.8 / 448.1 / 215.1 us, profiles/r5_final/perf_guards.jsonl)
 WAVE_BOUND_US = {(33, 2, 2, 256): 277.0, (101, 1, 2, 256): 493.0, (27, 2, 36, 32): 237.0}
-# speculative-block-0 kernel (the default rollout path at these shapes): 1.10 x 157.1 / 139.8 / 544.5 / 749.4 us
-SPEC_BOUND_US = {(33, 2, 2, 256): 173.0, (27, 2, 36, 32): 154.0, (101, 2, 2, 256): 599.0, (129, 2, 2, 256): 824.0}
+# speculative-block-0 kernel (the default rollout path at these shapes): 1.10 x 148.6 / 135.3 / 531.2 / 746.8 us
+SPEC_BOUND_US = {(33, 2, 2, 256): 164.0, (27, 2, 36, 32): 149.0, (101, 2, 2, 256): 585.0, (129, 2, 2, 256): 822.0}
 
 
 @pytest.mark.parametrize("L,nb,A,B", [(33, 2, 2, 256), (101, 1, 2, 256), (27, 2, 36, 32), (101, 2, 2, 256),
