@@ -34,7 +34,10 @@ PER_FILE_FLAGS = {
     "smac_env.hip": ["-ffp-contract=off"],
     # MFMA results written straight to VGPRs: by default hipcc accumulates in AGPRs and copies every result to a VGPR
     # for the VALU work that follows (847 v_accvgpr moves per agent step in the one-wave decode, 131 with this form)
-    "mat_decode_wave.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
+    # ... and the max-ILP scheduler for the latency-bound speculative decode (scripts/r5_sched.sh: 256 x 33 150.0 ->
+    # 146.7 us, SMAC 135.2 -> 133.0 us, 256 x 129 749 -> 741 us; max-memory-clause and the register-pressure trackers
+    # were slower; the training backward / forward measured neutral / slower with max-ilp)
+    "mat_decode_wave.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-mllvm", "-amdgpu-sched-strategy=max-ilp"],
     "mat_decode.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
 }
 
@@ -49,6 +52,8 @@ def _flags(src):
         extra = os.environ.get("MAT_DCML_FWD_FLAGS", "").split()
     if os.path.basename(src) == "mat_enc_ct.hip":   # A/B: the encoder forward alone
         extra = extra + os.environ.get("MAT_DCML_ENCF_FLAGS", "").split()
+    if os.path.basename(src) == "mat_decode_wave.hip":   # A/B: the one-wave / speculative decode
+        extra = extra + os.environ.get("MAT_DCML_DECW_FLAGS", "").split()
     per_file = [] if os.environ.get("MAT_DCML_NO_PER_FILE_FLAGS") else PER_FILE_FLAGS.get(os.path.basename(src), [])
     return FLAGS + per_file + extra
 
