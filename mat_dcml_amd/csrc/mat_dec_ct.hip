@@ -155,10 +155,10 @@ __device__ __forceinline__ void cross_attn_fwd_ct(const Mat* m, const LNp& ln, C
     const int rt = c.wave + NW * k;
     if (rt < c.NT) {
       CTr a, alo;
-      ct_split(O[k], a, alo);
+      if (MDL_SAVE_OLO2) ct_split(O[k], a, alo); else a = ct_pack(O[k]);
       if (SAVE) {
         st_g(sv_a, c.tok0, rt, c.NR, a, lane);
-        st_g(sv_alo, c.tok0, rt, c.NR, alo, lane);
+        if (MDL_SAVE_OLO2) st_g(sv_alo, c.tok0, rt, c.NR, alo, lane);
       }
       CT t = ct_add(bp, rp[k]), xh;
       mm(t, Wp, a);
@@ -218,7 +218,7 @@ __device__ __forceinline__ void cross_attn_bwd_ct(const Mat* m, const LNp& ln, C
       for (int k = 0; k < MAXRT; ++k) {
         const int rt = c.wave + NW * k;
         if (rt < c.NT) {
-          const CTr alo = ld_g(sv_alo, c.tok0, rt, c.NR, lane);
+          const CTr alo = MDL_SAVE_OLO2 ? ld_g(sv_alo, c.tok0, rt, c.NR, lane) : ct_zero_r();
           CT da;
           ct_zero(da);
           mm(da, Wpb, ld_lds(c.DQ, rt, lane));

@@ -241,6 +241,14 @@ __device__ __forceinline__ CTr ld_g(const bf16_t* src, int tok0, int rt, int NR,
 #ifndef MDL_NT_SCALARS
 #define MDL_NT_SCALARS 0   // A/B: the per-token f32 records (rstd, log-sum-exp) as nontemporal stores too
 #endif
+// MDL_SAVE_OLO=0 (A/B): the attention output is saved as bf16 only (its lo half — used only by the backward's
+// delta = rowsum(dO O) — is not stored / loaded: 128 B per token and attention less in both directions)
+#ifndef MDL_SAVE_OLO
+#define MDL_SAVE_OLO 1
+#endif
+#ifndef MDL_SAVE_OLO2   // the same for the decoder's cross attention
+#define MDL_SAVE_OLO2 MDL_SAVE_OLO
+#endif
 __device__ __forceinline__ void st_g(bf16_t* dst, int tok0, int rt, int NR, const CTr& x, int lane) {
   const int g = lane >> 4, row = rt * 16 + (lane & 15);
   if (SAVE_ON(row, NR)) {
@@ -894,10 +902,10 @@ __device__ __forceinline__ void self_attn_fwd_ct(const Mat* m, const LNp& ln, CT
     const int rt = c.wave + NW * k;
     if (rt < c.NT) {
       CTr a, alo;
-      ct_split(O[k], a, alo);
+      if (MDL_SAVE_OLO) ct_split(O[k], a, alo); else a = ct_pack(O[k]);
       if (SAVE) {
         st_g(sv_a, c.tok0, rt, c.NR, a, lane);
-        st_g(sv_alo, c.tok0, rt, c.NR, alo, lane);
+        if (MDL_SAVE_OLO) st_g(sv_alo, c.tok0, rt, c.NR, alo, lane);
       }
       CT t = ct_add(bp, xr[k]), xh;
       mm(t, Wp, a);
@@ -1077,7 +1085,7 @@ __device__ __forceinline__ void self_attn_bwd_ct(const Mat* m, const LNp& ln, CT
       for (int k = 0; k < MAXRT; ++k) {
         const int rt = c.wave + NW * k;
         if (rt < c.NT) {
-          const CTr alo = ld_g(sv_alo, c.tok0, rt, c.NR, lane);
+          const CTr alo = MDL_SAVE_OLO ? ld_g(sv_alo, c.tok0, rt, c.NR, lane) : ct_zero_r();
           CT da;
           ct_zero(da);
           mm(da, Wpb, ld_lds(c.DQ, rt, lane));

@@ -106,7 +106,7 @@ def test_full_mat_fused_grads(gpu, L, B):
     assert rel(v_k, v_r) < tol(v_b, v_r) and rel(ent_k, ent_r) < tol(ent_b, ent_r)
     ((lp_k * w1).sum() + (v_k * w2).sum() + (ent_k * w3).sum()).backward()
     torch.cuda.synchronize()
-    bad = []
+    bad, margins = [], []
     params = dict(m.named_parameters())
     for n, r in ref.items():
         gg = params[n].grad
@@ -165,7 +165,7 @@ def test_full_mat_fused_grads_wide_obs_discrete(gpu, L, B, A, od):
     assert rel(v_k, v_r) < tol(v_b, v_r) and rel(ent_k, ent_r) < tol(ent_b, ent_r)
     ((lp_k * w1).sum() + (v_k * w2).sum() + (ent_k * w3).sum()).backward()
     torch.cuda.synchronize()
-    bad = []
+    bad, margins = [], []
     params = dict(m.named_parameters())
     for n, r in ref.items():
         gg = params[n].grad
@@ -175,8 +175,10 @@ def test_full_mat_fused_grads_wide_obs_discrete(gpu, L, B, A, od):
         else:
             e = rel(gg, r)
             lim = max(6e-2, 2.5 * rel(refb[n], r))
+        margins.append((e / lim, n))
         if e > lim:
             bad.append((n, round(e, 4), round(rel(refb[n], r), 4)))
+    print("[grad-margin] worst error / limit:", [(round(x, 3), n) for x, n in sorted(margins, reverse=True)[:4]])
     assert not bad, bad
 
 
@@ -220,7 +222,7 @@ def test_full_mat_fused_grads_continuous(gpu, L, B, A):
     assert rel(v_k, v_r) < tol(v_b, v_r) and rel(ent_k, ent_r) < tol(ent_b, ent_r)
     ((lp_k * w1).sum() + (v_k * w2).sum() + (ent_k * w3).sum()).backward()
     torch.cuda.synchronize()
-    bad = []
+    bad, margins = [], []
     params = dict(m.named_parameters())
     for n, r in ref.items():
         gg = params[n].grad
@@ -230,8 +232,10 @@ def test_full_mat_fused_grads_continuous(gpu, L, B, A):
         else:
             e = rel(gg, r)
             lim = max(6e-2, 2.5 * rel(refb[n], r))
+        margins.append((e / lim, n))
         if e > lim:
             bad.append((n, round(e, 4), round(rel(refb[n], r), 4)))
+    print("[grad-margin] worst error / limit:", [(round(x, 3), n) for x, n in sorted(margins, reverse=True)[:4]])
     assert not bad, bad
 
 
@@ -299,7 +303,7 @@ def test_hybrid_available_continuous_grads(gpu, L, B, A):
     ((lp_k * w1).sum() + (v_k * w2).sum() + (ent_k * w3).sum()).backward()
     torch.cuda.synchronize()
     assert m._mdl_train_state[0].ctx is None      # ... and its backward consumed them
-    bad = []
+    bad, margins = [], []
     params = dict(m.named_parameters())
     for n, r in ref.items():
         gg = params[n].grad
@@ -309,8 +313,10 @@ def test_hybrid_available_continuous_grads(gpu, L, B, A):
         else:
             e = rel(gg, r)
             lim = max(6e-2, 2.5 * rel(refb[n], r))
+        margins.append((e / lim, n))
         if e > lim:
             bad.append((n, round(e, 4), round(rel(refb[n], r), 4)))
+    print("[grad-margin] worst error / limit:", [(round(x, 3), n) for x, n in sorted(margins, reverse=True)[:4]])
     assert not bad, bad
 
 
