@@ -195,7 +195,10 @@ class MATTrainer:
             drep = dec.backward(dlp, dent)
             enc.backward(drep, dv)
         m._mdl_gws_active = False
-        mat_train.reduce_grad_workspace(m)
+        # one process: the workspace reduction also leaves the optimizer's Σ g² partials of the final gradient (no
+        # norm launch); under data parallelism the norm is the all-reduced gradient's, so the Adam step computes it
+        fuse_norm = self.comm.world_size == 1 and not self.poison
+        norm_ready = mat_train.reduce_grad_workspace(m, norm_into=pol.optimizer.scratch if fuse_norm else None)
         dec.ctx = None
         enc.ctx = None
         if self.poison:
@@ -206,7 +209,7 @@ class MATTrainer:
             # collective (round-1 variant)
             self.comm.grad_mean_(buf)
             self.collectives += 1
-        pol.optimizer.step()
+        pol.optimizer.step(norm_ready=norm_ready)
         mat_fused.bump_version(m)
         return pol.optimizer.grad_norm
 

@@ -216,8 +216,10 @@ struct AdamArgs {
 };
 
 // The norm pass writes one Σ g² partial per workgroup; every step workgroup sums the ADAM_NB partials itself in a
-// fixed order (bit-identical norm everywhere, run to run) — no memset, no same-address atomics.
-constexpr int ADAM_NB = 128;
+// fixed order (bit-identical norm everywhere, run to run) — no memset, no same-address atomics.  1024 partials: the
+// single-GPU trainer computes them inside the gradient-workspace reduction (grad_reduce_norm_kernel, one workgroup
+// per partial at the reduction's full width) and skips the norm launch.
+constexpr int ADAM_NB = 1024;
 
 __global__ __launch_bounds__(256) void adam_norm_kernel(AdamArgs a) {
   __shared__ float sm[4];
@@ -238,8 +240,10 @@ __global__ __launch_bounds__(256) void adam_norm_kernel(AdamArgs a) {
 
 __global__ __launch_bounds__(256) void adam_step_kernel(AdamArgs a) {
   __shared__ float snorm;
-  if (threadIdx.x < 64) {   // wave 0: Σ of the ADAM_NB partials (two per lane, fixed order)
-    const float v = a.sumsq[4 + threadIdx.x] + a.sumsq[4 + 64 + threadIdx.x];
+  if (threadIdx.x < 64) {   // wave 0: Σ of the ADAM_NB partials (ADAM_NB / 64 per lane, fixed order)
+    float v = 0.f;
+#pragma unroll
+    for (int j = 0; j < ADAM_NB / 64; ++j) v += a.sumsq[4 + 64 * j + threadIdx.x];
     const float tot = wave_sum(v);
     if (threadIdx.x == 0) snorm = sqrtf(tot);
   }
@@ -274,11 +278,14 @@ __global__ __launch_bounds__(256) void adam_step_kernel(AdamArgs a) {
 
 MDL_API int mdl_adam_scratch_floats() { return 4 + ADAM_NB; }
 
-MDL_API int mdl_adam(const AdamArgs* a, hipStream_t st) {
+// norm_ready: the Σ g² partials are already in sumsq[4..] (mdl_grad_reduce_norm over the same final gradient)
+MDL_API int mdl_adam(const AdamArgs* a, int norm_ready, hipStream_t st) {
   int g = (a->n + 255) / 256;
   if (g > 1024) g = 1024;
-  hipLaunchKernelGGL(adam_norm_kernel, dim3(ADAM_NB), dim3(256), 0, st, *a);
-  MDL_CHECK_LAUNCH();
+  if (!norm_ready) {
+    hipLaunchKernelGGL(adam_norm_kernel, dim3(ADAM_NB), dim3(256), 0, st, *a);
+    MDL_CHECK_LAUNCH();
+  }
   hipLaunchKernelGGL(adam_step_kernel, dim3(g), dim3(256), 0, st, *a);
   MDL_CHECK_LAUNCH();
   return 0;
@@ -304,6 +311,40 @@ __global__ __launch_bounds__(256) void grad_reduce_kernel(float* g, float* ws, i
     for (k = 0; k < copies; ++k) ws[(size_t)k * stride + i] = 0.f;
     g[i] += s;
   }
+}
+
+// ... and, for the whole flat buffer, the optimizer's Σ g² partials of the FINAL gradient in the same pass (one per
+// workgroup, sumsq[4 + blockIdx], ADAM_NB workgroups: the Adam step then skips its norm launch)
+__global__ __launch_bounds__(256) void grad_reduce_norm_kernel(float* g, float* ws, int n, long long stride, int copies,
+                                                               float* sumsq) {
+  __shared__ float sm[4];
+  float q = 0.f;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    float s = 0.f;
+    int k = 0;
+    for (; k + 8 <= copies; k += 8) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = ws[(size_t)(k + j) * stride + i];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[j];
+    }
+    for (; k < copies; ++k) s += ws[(size_t)k * stride + i];
+    for (k = 0; k < copies; ++k) ws[(size_t)k * stride + i] = 0.f;
+    const float gi = g[i] + s;
+    g[i] = gi;
+    q += gi * gi;
+  }
+  q = wave_sum(q);
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = q;
+  __syncthreads();
+  if (threadIdx.x == 0) sumsq[4 + blockIdx.x] = (sm[0] + sm[1]) + (sm[2] + sm[3]);
+}
+
+MDL_API int mdl_grad_reduce_norm(float* g, float* ws, int n, long long stride, int copies, float* sumsq, hipStream_t st) {
+  hipLaunchKernelGGL(grad_reduce_norm_kernel, dim3(ADAM_NB), dim3(256), 0, st, g, ws, n, stride, copies, sumsq);
+  MDL_CHECK_LAUNCH();
+  return 0;
 }
 
 MDL_API int mdl_grad_reduce(float* g, float* ws, int n, long long stride, int copies, hipStream_t st) {

@@ -74,6 +74,7 @@ sig("mdl_mat_enc_bwd_ct", ctypes.POINTER(EncP), VP, VP, ctypes.c_int, VP)
 sig("mdl_mat_dec_fwd_ct", ctypes.POINTER(DecP), ctypes.c_int, ctypes.c_int, VP)
 sig("mdl_mat_dec_bwd_ct", ctypes.POINTER(DecP), ctypes.c_int, VP)
 sig("mdl_grad_reduce", VP, VP, ctypes.c_int, ctypes.c_longlong, ctypes.c_int, VP)
+sig("mdl_grad_reduce_norm", VP, VP, ctypes.c_int, ctypes.c_longlong, ctypes.c_int, VP, VP)
 
 
 class OEArgs(ctypes.Structure):   # csrc/obs_embed.hip
@@ -588,17 +589,24 @@ def check_grad_ptrs(p, flat):
         raise RuntimeError(f"gradient pointers outside the flat gradient buffer: {bad[:6]} (flat {lo:#x}..{hi:#x})")
 
 
-def reduce_grad_workspace(model, lo=0, hi=None):
-    """Fold the workspace copies of flat-gradient elements [lo, hi) back into the flat buffer (and zero them)."""
+def reduce_grad_workspace(model, lo=0, hi=None, norm_into=None):
+    """Fold the workspace copies of flat-gradient elements [lo, hi) back into the flat buffer (and zero them).
+    ``norm_into`` (the whole buffer only): also write the optimizer's Σ g² partials of the final gradient into that
+    FlatAdam scratch (``FlatAdam.step(norm_ready=True)`` then skips its norm launch).  Returns whether it did."""
     st = getattr(model, "_mdl_gws_buf", None)
     if st is None:
-        return
+        return False
     ws, g, stride, copies = st
     hi = g.numel() if hi is None else hi
     if hi <= lo:
-        return
+        return False
+    if norm_into is not None and lo == 0 and hi == g.numel():
+        check(lib().mdl_grad_reduce_norm(g.data_ptr(), ws.data_ptr(), hi, stride, copies, norm_into.data_ptr(),
+                                         kernels._stream()), "grad_reduce_norm")
+        return True
     check(lib().mdl_grad_reduce(g.data_ptr() + 4 * lo, ws.data_ptr() + 4 * lo, hi - lo, stride, copies,
                                 kernels._stream()), "grad_reduce")
+    return False
 
 
 def flat_range(params, flat):

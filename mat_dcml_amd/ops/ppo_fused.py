@@ -42,7 +42,7 @@ class AdamArgs(ctypes.Structure):
 sig("mdl_ppo_loss", ctypes.POINTER(PPOArgs), vp)
 sig("mdl_ppo_reduce", ctypes.POINTER(PPOArgs), vp)
 sig("mdl_ppo_finish", ctypes.POINTER(PPOArgs), vp)
-sig("mdl_adam", ctypes.POINTER(AdamArgs), vp)
+sig("mdl_adam", ctypes.POINTER(AdamArgs), ctypes.c_int, vp)
 
 
 PAD = 16   # every parameter starts on a 64-byte boundary of the flat buffer (aligned float4 loads in the kernels)
@@ -96,7 +96,7 @@ def _adam_scratch_floats():
     try:
         return int(lib().mdl_adam_scratch_floats())
     except Exception:   # CPU-only state handling without the library: same layout (4 + ADAM_NB)
-        return 4 + 128
+        return 4 + 1024
 
 
 class FlatAdam:
@@ -136,14 +136,16 @@ class FlatAdam:
     def zero_grad(self, set_to_none=False):
         self.g.zero_()
 
-    def step(self):
+    def step(self, norm_ready=False):
+        """``norm_ready``: the Σ g² partials of this step's gradient are already in the scratch
+        (``mat_train.reduce_grad_workspace(..., norm_into=self.scratch)``): no norm launch."""
         g = self.param_groups[0]
         self.t += 1
         b1, b2 = g["betas"]
         a = AdamArgs(n=self.p.numel(), p=P(self.p), g=P(self.g), m=P(self.m), v=P(self.v), sumsq=P(self.scratch),
                      lr=g["lr"], beta1=b1, beta2=b2, eps=g["eps"], wd=g["weight_decay"], t=float(self.t),
                      max_norm=float(self.max_grad_norm or 0.0), clip=int(self.max_grad_norm is not None))
-        check(lib().mdl_adam(ctypes.byref(a), _stream()), "adam")
+        check(lib().mdl_adam(ctypes.byref(a), int(bool(norm_ready)), _stream()), "adam")
 
     def applied_steps(self) -> int:
         return self.t - int(round(float(self.scratch[2])))

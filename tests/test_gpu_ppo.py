@@ -85,6 +85,40 @@ def test_flat_adam_matches_torch_adam_with_clipping(gpu):
         assert torch.allclose(flat_p, p_ref.detach(), atol=1e-6, rtol=1e-5), (flat_p - p_ref).abs().max()
 
 
+def test_workspace_reduction_with_norm_partials_matches_adam_norm(gpu):
+    """The single-GPU update path: mdl_grad_reduce_norm folds the 32 gradient-workspace copies into the flat buffer
+    AND leaves the optimizer's Σ g² partials, so FlatAdam.step(norm_ready=True) skips its norm launch; same grad
+    norm (to fp32 summation order) and the same parameters as the unfused reduction + step."""
+    from types import SimpleNamespace
+
+    from mat_dcml_amd.ops import mat_train
+    from mat_dcml_amd.ops.ppo_fused import FlatAdam
+    g = torch.Generator(device=gpu).manual_seed(2)
+    n, copies = 151469, 32
+    p0 = torch.randn(n, device=gpu, generator=g)
+    res = []
+    for fused in (False, True):
+        flat_p, flat_g = p0.clone(), torch.zeros(n, device=gpu)
+        fa = FlatAdam(flat_p, flat_g, lr=5e-4, eps=1e-5, max_grad_norm=1.0)
+        m = SimpleNamespace()
+        ws = mat_train.attach_grad_workspace(m, flat_g, copies=copies)
+        stride = ws.numel() // copies
+        gg = torch.Generator(device=gpu).manual_seed(3)
+        for it in range(3):
+            for k in range(copies):
+                ws[k * stride:k * stride + n].copy_(torch.randn(n, device=gpu, generator=gg) * 0.1)
+            flat_g.zero_()
+            ready = mat_train.reduce_grad_workspace(m, norm_into=fa.scratch if fused else None)
+            assert ready == fused
+            assert float(ws.abs().max()) == 0.0   # the copies are zeroed for the next minibatch
+            fa.step(norm_ready=ready)
+        torch.cuda.synchronize()
+        res.append((flat_p.clone(), float(fa.grad_norm), flat_g.clone()))
+    assert torch.equal(res[0][2], res[1][2])   # the same folded gradient
+    assert abs(res[0][1] - res[1][1]) <= 1e-5 * res[0][1], (res[0][1], res[1][1])
+    assert torch.allclose(res[0][0], res[1][0], atol=1e-6, rtol=1e-6), (res[0][0] - res[1][0]).abs().max()
+
+
 @pytest.mark.parametrize("n_obj", [1, 2])
 def test_fused_trainer_step_matches_autograd_step(gpu, n_obj):
     """One PPO minibatch: fused loss + FlatAdam vs autograd loss + torch Adam (same fused fwd/bwd kernels); n_obj = 2
