@@ -359,6 +359,21 @@ __device__ __forceinline__ float rdlane(float x, int l) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
 }
 
+// Phase profile (-DMDL_SPEC_PROF, scripts/spec_prof.py): s_memtime cycles per phase of the main wave and of the first
+// speculative wave, summed over envs and agent steps (g_spprof[role][phase], read by mdl_spec_prof_read)
+#ifdef MDL_SPEC_PROF
+__device__ unsigned long long g_spprof[2][16];
+#define SPP_DECL unsigned long long spp_t = __builtin_amdgcn_s_memtime(), spp_acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}
+#define SPP(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); spp_acc[k] += t_ - spp_t; spp_t = t_; } while (0)
+#define SPP_END(role) do { if (lane == 0 && (role) >= 0) for (int k_ = 0; k_ < 16; ++k_) atomicAdd(&g_spprof[role][k_], spp_acc[k_]); } while (0)
+// inside the head helper (main wave): marks into the caller's accumulators through hp (unsigned long long[17])
+#define SPH(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); hp[k] += t_ - hp[16]; hp[16] = t_; } while (0)
+#else
+#define SPH(k) do { } while (0)
+#define SPP_DECL do { } while (0)
+#define SPP(k) do { } while (0)
+#define SPP_END(role) do { } while (0)
+#endif
 // folded head: W' = W_h2 diag(gamma_h) as hi / lo A fragments (rows = actions 16 ma + c, k in the CT order), and
 // G_a = Σ W'[a], C_a = W_h2 beta_h + b_h2 for this lane's logit slots a = 16 ma + 4 g + r
 template <int MA>
@@ -411,7 +426,8 @@ __device__ __forceinline__ WvNoise wv_noise_load(const DecParams& p, int env, in
 template <int NM, int NLDS, int NREG, int MA>
 __device__ __forceinline__ int wv_head_sample(const CT& x, const WvHeadW<MA>& hw, const WvNoise& nz, const RegW<NREG>& rw,
                                               const bf16_t* W, const float* BI, float* SC, const DecParams& p, int env,
-                                              int i, float avl, int tok, int lane) {
+                                              int i, float avl, int tok, int lane,
+                                              unsigned long long* hp = nullptr) {
   constexpr bool WIDE = MA > 1;
   const int g = lane >> 4, c = lane & 15, A = p.act_dim, L = p.L, n_disc = p.n_disc;
   const bool det = p.deterministic != 0;
@@ -422,7 +438,9 @@ __device__ __forceinline__ int wv_head_sample(const CT& x, const WvHeadW<MA>& hw
     wv_getw<NM - 1, NLDS, NREG>(w, rw, W, lane);
     mm(h, w, ct_pack(x));
   }
+  if (hp) SPH(8);
   h = gelu_dist(h, lane);
+  if (hp) SPH(9);
   WDBG(12, h);
   f32x4 s4 = (h.v[0] + h.v[1]) + (h.v[2] + h.v[3]);
   f32x4 q4 = h.v[0] * h.v[0];
@@ -432,6 +450,7 @@ __device__ __forceinline__ int wv_head_sample(const CT& x, const WvHeadW<MA>& hw
   const float rstd = rsqrtf(fmaxf(cross_row_sum((q4[0] + q4[1]) + (q4[2] + q4[3])) * (1.f / 64.f) - mean * mean, 0.f) + 1e-5f);
   CTr nh, nl;
   ct_split(h, nh, nl);
+  if (hp) SPH(10);
   f32x4 lg[MA];
 #pragma unroll
   for (int ma = 0; ma < MA; ++ma) {
@@ -453,6 +472,7 @@ __device__ __forceinline__ int wv_head_sample(const CT& x, const WvHeadW<MA>& hw
     WDBG(13, lgc);
   }
 #endif
+  if (hp) SPH(11);
   const size_t oi = (size_t)env * L + i;
   float a_out, lp_out;
   if constexpr (!WIDE) {   // A <= 4: the logits are registers r < A of lanes g = 0
@@ -527,10 +547,12 @@ __device__ __forceinline__ int wv_head_sample(const CT& x, const WvHeadW<MA>& hw
       lp_out = -0.5f * z * z - __logf(sd) - 0.91893853320467274f;
     }
   }
+  if (hp) SPH(12);
   if (lane == 0) {
     p.out_a[oi] = a_out;
     p.out_lp[oi] = lp_out;
   }
+  if (hp) SPH(13);
   return tok;
 }
 
@@ -890,8 +912,10 @@ __global__ __launch_bounds__(64 * (1 + NS), 1) void mat_decode_spec_kernel(DecPa
     int tok = p.tok_start;
     if (lane == 0) TOK[0] = tok;
     __syncthreads();   // (1) row 0's block 0 is staged
+    SPP_DECL;
 #pragma unroll 1
     for (int i = 0; i < L; ++i) {
+      SPP(0);   // 0: barrier wait
       const CT repi = ld_vec(rep + (size_t)i * 64, lane);
       const float avl = (ava && lane < A) ? ava[(size_t)i * A + lane] : 1.f;
       CT x = ld_vec(SLOT + (size_t)((i & 1) * A + (i == 0 ? 0 : tok - 1)) * 64, lane);
@@ -903,10 +927,21 @@ __global__ __launch_bounds__(64 * (1 + NS), 1) void mat_decode_spec_kernel(DecPa
       } else if constexpr (NB > 1) {
         wv_block<1, NB, NLDS, NREG>(x, k, rw, i, tok, repi);
       }
+      SPP(1);   // 1: slot read + block 1
+#ifdef MDL_SPEC_PROF
+      unsigned long long hp[17] = {0};
+      hp[16] = spp_t;
+      tok = wv_head_sample<NM, NLDS, NREG, MA>(x, hw, nz, rw, k.W, BI, SC, p, env, i, avl, tok, lane, hp);
+      for (int k_ = 8; k_ < 14; ++k_) spp_acc[k_] += hp[k_];
+      spp_t = hp[16];
+#else
       tok = wv_head_sample<NM, NLDS, NREG, MA>(x, hw, nz, rw, k.W, BI, SC, p, env, i, avl, tok, lane);
+#endif
       if (lane == 0) TOK[(i + 1) & 1] = tok;
+      SPP(2);   // 2: head + sampling (rest)
       __syncthreads();   // (2) token of row i + 1 published; block 0 of row i + 1 staged for every candidate
     }
+    SPP_END(0);
   } else {
     // ---------------------------------------------------------------- speculative waves: block 0 of the next row
     RegW<6> w0;
@@ -952,8 +987,10 @@ __global__ __launch_bounds__(64 * (1 + NS), 1) void mat_decode_spec_kernel(DecPa
     }
     const SpCand cd = sp_cand(QT, p.emb, min(1 + cand, p.n_tok - 1), lane);
     __syncthreads();   // (1)
+    SPP_DECL;
 #pragma unroll 1
     for (int i = 0; i < L; ++i) {
+      SPP(4);   // 4: barrier wait
       const CT repn = ld_vec(rep + (size_t)min(i + 1, L - 1) * 64, lane);
       // commit row i of the block-0 caches: the token's self-attention K / V table rows and the staged cross K / V
       // rows of its candidate; lane (kind, 16-byte chunk), kinds 0..3 = self K, self V, cross K, cross V
@@ -966,14 +1003,18 @@ __global__ __launch_bounds__(64 * (1 + NS), 1) void mat_decode_spec_kernel(DecPa
         *(uint4*)(wv_cache(KV, 0, kind, L) + tmo(i, 8 * ch)) = *(const uint4*)src;
       }
       asm volatile("" ::: "memory");   // the committed row is read back by other lanes below (LDS is in order per wave)
+      SPP(5);   // 5: commit
       if (i + 1 < L) {
         CT x = cd.e;
         CTr kp, vp;
         sp_block0(x, cd.q, cd.k, cd.v, w0, k, selfkv, i + 1, repn, q2row(i + 1, repn), kp, vp);
+        SPP(6);   // 6: block 0
         stage((i + 1) & 1, x, kp, vp);
+        SPP(7);   // 7: staging stores
       }
       __syncthreads();   // (2)
     }
+    SPP_END(wave == 1 ? 1 : -1);
   }
 }
 
@@ -1034,6 +1075,15 @@ static bool wv_eligible(const DecParams* p, int NB) {
   if (!p->deterministic && !p->gen && (!p->rnd_u || (p->n_disc < p->L && !p->rnd_n))) return false;
   return true;
 }
+#ifdef MDL_SPEC_PROF
+MDL_API int mdl_spec_prof_read(unsigned long long* out, int reset) {
+  if (reset) {
+    static const unsigned long long z[32] = {0};
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_spprof), z, sizeof(z));
+  }
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_spprof), sizeof(unsigned long long) * 32, 0, hipMemcpyDeviceToHost);
+}
+#endif
 MDL_API int mdl_decode_wave_plan(const DecParams* p, int NB) {
   if (!wv_eligible(p, NB)) return -1;
   for (int nreg = 0; nreg <= (NB == 1 ? 4 : 6); nreg += 2)
