@@ -919,6 +919,12 @@ __device__ __forceinline__ void self_attn_fwd_ct(const Mat* m, const LNp& ln, CT
 }
 
 // MLP: x <- LN(x + W2 GELU(W1 x + b1) + b2)   (ma_transformer.py:84-86,91-92)
+// MDL_SAVE_PREACT (A/B): the training forward saves the pre-activation h (bf16) instead of GELU(h) and GELU'(h) — 128 B
+// per token and MLP less in both directions; the W2 operand is GELU(bf16(h)) in both passes (autocast's rounding
+// point), and the backward re-derives GELU and GELU' from h with one erf
+#ifndef MDL_SAVE_PREACT
+#define MDL_SAVE_PREACT 0
+#endif
 template <bool SAVE>
 __device__ __forceinline__ void mlp_fwd_ct(const Mat& m1, const Mat& m2, const LNp& ln, CT* xr, bf16_t* sv_x, bf16_t* sv_g,
                                            bf16_t* sv_gp, bf16_t* sv_xh, float* sv_rs, const Ctx& c) {
@@ -936,7 +942,13 @@ __device__ __forceinline__ void mlp_fwd_ct(const Mat& m1, const Mat& m2, const L
       CT h = b1;
       mm(h, W1, x);
       CTr gr;
-      if (SAVE) {   // GELU(h) (the W2 operand) and GELU'(h) for the backward, from one erf
+      if (SAVE && MDL_SAVE_PREACT) {   // h for the backward; GELU of its bf16 value as the W2 operand
+        const CTr hb = ct_pack(h);
+        st_g(sv_g, c.tok0, rt, c.NR, hb, lane);
+        h = ct_unpack(hb);
+        gelu_ct(h);
+        gr = ct_pack(h);
+      } else if (SAVE) {   // GELU(h) (the W2 operand) and GELU'(h) for the backward, from one erf
         CT gp;
         gelu_ct_both(h, gp);
         gr = ct_pack(h);
@@ -966,6 +978,7 @@ __device__ __forceinline__ void mlp_bwd_ct(const Mat& m1, const Mat& m2, const L
                                            const bf16_t* sv_g, const bf16_t* sv_gp, const bf16_t* sv_xh,
                                            const float* sv_rs, const Ctx& c, int vslot) {
   const int lane = c.lane;
+  CTr gps[MAXRT];   // MDL_SAVE_PREACT: GELU'(h) from pass 1 for pass 2
   {   // pass 1: LN backward from the saved x-hat / rstd -> ds (dx) ; DA = dY of W2, XB = X of W2 (GELU(h))
     CT dlg, dlb;
     ct_zero(dlg);
@@ -973,6 +986,7 @@ __device__ __forceinline__ void mlp_bwd_ct(const Mat& m1, const Mat& m2, const L
     const CT gam = ld_vec(ln.g, lane);
     CTr xs[MAXRT], hs[MAXRT], xhs[MAXRT];
     float rsv[MAXRT];
+    if (MDL_SAVE_PREACT) (void)sv_gp;
 #pragma unroll
     for (int k = 0; k < MAXRT; ++k) {   // every saved-activation load of the wave issued up front
       const int rt = c.wave + NW * k;
@@ -988,7 +1002,13 @@ __device__ __forceinline__ void mlp_bwd_ct(const Mat& m1, const Mat& m2, const L
       const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         const bool ok = tok_ok(rt, c);
-        const CTr glr = hs[k];   // GELU(h): the forward's own W2 operand
+        CTr glr = hs[k];   // GELU(h): the forward's own W2 operand
+        if (MDL_SAVE_PREACT) {   // hs = h: GELU(h) -> XB, GELU'(h) kept (packed) for pass 2
+          CT hv = ct_unpack(hs[k]), gp;
+          gelu_ct_both(hv, gp);
+          glr = ct_pack(hv);
+          gps[k] = ct_pack(gp);
+        }
         CT ds;
         ln_bwd_ct(dx[k], ct_unpack(xhs[k]), rsv[k], gam, ok, ds, dlg, dlb);
         st_lds(c.DA, rt, ct_pack(ds), ok, lane);   // dY of W2
@@ -1008,7 +1028,7 @@ __device__ __forceinline__ void mlp_bwd_ct(const Mat& m1, const Mat& m2, const L
       const int rt = c.wave + NW * k;
       if (rt < c.NT) {
         const bool ok = tok_ok(rt, c);
-        const CT gp = ct_unpack(ld_g(sv_gp, c.tok0, rt, c.NR, lane));   // GELU'(h), saved by the forward
+        const CT gp = ct_unpack(MDL_SAVE_PREACT ? gps[k] : ld_g(sv_gp, c.tok0, rt, c.NR, lane));   // GELU'(h)
         CT dg;
         ct_zero(dg);
         mm(dg, W2b, ld_lds(c.DA, rt, lane));
