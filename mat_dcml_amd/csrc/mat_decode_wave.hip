@@ -262,9 +262,11 @@ struct WvCtx {
 
 // one decoder block for the live row i (ma_transformer.py:95-98): x <- LN1(x + attn1(x)); x <- LN2(rep_i + attn2(q =
 // rep_i, k = v = x)); x <- LN3(x + mlp(x)).  Block 0's q / K / V of x come from the token table (x = ET[tok]).
-template <int B, int NB, int NLDS, int NREG>
+// STQ (the speculative kernel's PAIR main wave): block B's q / K / V rows of x were computed ahead by the speculative
+// wave and staged at stq ([q, k, v][64] bf16): the row's K / V are copied into the caches, the three products skipped
+template <int B, int NB, int NLDS, int NREG, bool STQ = false>
 __device__ __forceinline__ void wv_block(CT& x, const WvCtx& k, const RegW<NREG>& rw, int i, int tok, const CT& repi,
-                                         const CTr* q2in = nullptr) {
+                                         const CTr* q2in = nullptr, const bf16_t* stq = nullptr) {
   const int lane = k.lane, g = lane >> 4, L = k.L;
   CT xh;
   AFr w;
@@ -281,6 +283,13 @@ __device__ __forceinline__ void wv_block(CT& x, const WvCtx& k, const RegW<NREG>
       }
     }
     x = ld_vec(k.ET + tok * 64, lane);
+  } else if constexpr (STQ) {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) qr.q[mt] = *(const uint2*)(stq + 16 * mt + 4 * g);
+    if (lane < 16) {   // lane (kind, 16-byte chunk): staged K / V row -> swizzled cache row i
+      const int kind = lane >> 3, ch = lane & 7;
+      *(uint4*)(wv_cache(k.KV, B, kind, L) + tmo(i, 8 * ch)) = *(const uint4*)(stq + 64 * (kind + 1) + 8 * ch);
+    }
   } else {
     const CTr xp = ct_pack(x);
     CT q = ld_vec(k.BI + 64 * (10 * B + 0), lane), kk = ld_vec(k.BI + 64 * (10 * B + 1), lane);
@@ -660,6 +669,17 @@ __global__ __launch_bounds__(64, 1) void mat_decode_wave_kernel(DecParams p) {
 struct SpLds { int w, kv, q2, qt, bi, lp, sc, slot, stg, tok, rowtok, total; };
 // Q2F (L = 129): no cross-attention query table either — the main wave computes block 1's query of its row from
 // W_q2 (one more LDS matrix), the speculative waves block 0's from a register copy of W_q2
+// PAIR (act_dim <= 2): MDL_SPEC_PAIR=0 builds keep the 16-candidate layout (A/B).  MDL_SPEC_STQ=1 (A/B, off: 256 x 33
+// 147.2 -> 151.5 us, 256 x 101 534 -> 528, 256 x 129 720 -> 697 us — the speculative wave became the critical path at
+// the headline shape): PAIR also stages block 1's q / k / v rows of every candidate and the main wave skips them
+#ifndef MDL_SPEC_PAIR
+#define MDL_SPEC_PAIR 1
+#endif
+#ifndef MDL_SPEC_STQ
+#define MDL_SPEC_STQ 0
+#endif
+// (when block 1's q / k / v weights are LDS-resident: at most 6 main-wave register matrices)
+__host__ __device__ inline bool sp_stq(int A, int nreg) { return MDL_SPEC_STQ && MDL_SPEC_PAIR && A <= 2 && nreg <= 6; }
 __host__ __device__ inline SpLds sp_lds(int NB, int L, int n_tok, int nlds_main, int A, bool ind, bool q2f = false) {
   SpLds o;
   int off = 0;
@@ -672,7 +692,8 @@ __host__ __device__ inline SpLds sp_lds(int NB, int L, int n_tok, int nlds_main,
   o.lp = take((3 * NB + 1) * 512);
   o.sc = take(64 * 4);
   o.slot = take(2 * A * 256);                // [parity][candidate][64] f32 block-0 outputs
-  o.stg = take(2 * A * 256);                 // [parity][candidate][K, V][64] bf16 cross-attention cache rows
+  o.stg = take(2 * A * (sp_stq(A, wv_nm(NB) - 6 - nlds_main) ? 640 : 256));   // [parity][candidate][rows][64] bf16: block 0's cross K / V
+                                                    // (+ block 1's q, k, v: PAIR)
   o.tok = take(16);                          // [parity] token of the next row
   o.rowtok = take(ind ? ((L + 31) & ~31) * 4 : 0);   // IND: input token of every committed row (0 beyond)
   o.total = off;
@@ -779,16 +800,120 @@ __device__ __forceinline__ CT sp_attn(const KVS& kvs, const CTr& q, const CTr& k
   return O;
 }
 
+// PAIR (act_dim <= 2, the DCML rollout): two candidates, so the 16 token columns hold (candidate c >> 3, head
+// (c >> 2) & 1, 4 replicas) instead of 16 candidates.  Both heads then share one online-softmax pass (each column
+// scores only its head's 32 dims; the other head's half of O comes from the partner column c ^ 4 by a bank-masked
+// DPP rotation), and GELU costs 2 erf per lane (each lane evaluates one packed feature pair of its candidate, 8
+// row broadcasts + a half select hand every lane its candidate's 8 packed words) instead of 16.
+template <int CTRL, int BANKS>
+__device__ __forceinline__ float dpp_banks(float x) {
+  const int a = __builtin_bit_cast(int, x);
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(a, a, CTRL, 0xF, BANKS, false));
+}
+template <int CTRL, int BANKS>
+__device__ __forceinline__ f32x4 dpp_banks4(f32x4 v) {
+  return f32x4{dpp_banks<CTRL, BANKS>(v.x), dpp_banks<CTRL, BANKS>(v.y), dpp_banks<CTRL, BANKS>(v.z),
+               dpp_banks<CTRL, BANKS>(v.w)};
+}
+template <class KVS>
+__device__ __forceinline__ CT sp_attn_pair(const KVS& kvs, const CTr& q, const CTr& ks, const CTr& vs, int i, int lane) {
+  const int g = lane >> 4, c = lane & 15, hd = (c >> 2) & 1;
+  float m, l;
+  f32x4 o[4];
+  {
+    const CT qf = ct_unpack(q), kf = ct_unpack(ks), vf = ct_unpack(vs);
+    const f32x4 d = hd ? qf.v[2] * kf.v[2] + qf.v[3] * kf.v[3] : qf.v[0] * kf.v[0] + qf.v[1] * kf.v[1];
+    m = cross_row_sum((d[0] + d[1]) + (d[2] + d[3])) * ATT_L2;
+    l = g == 0 ? 1.f : 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) o[mt] = vf.v[mt];
+  }
+  const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+  const bf16x8 qb0 = hd ? z8 : rb(q, 0), qb1 = hd ? rb(q, 1) : z8;
+  for (int kb = 0; kb < i; kb += 32) {
+    float sc[8];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int key = kb + pi_row(t, c);
+      const uint2 p0 = kvs.k4(key, 4 * g), p1 = kvs.k4(key, 16 + 4 * g);
+      const uint2 p2 = kvs.k4(key, 32 + 4 * g), p3 = kvs.k4(key, 48 + 4 * g);
+      f32x4 r = __builtin_amdgcn_mfma_f32_16x16x32_bf16(mk8(p0.x, p0.y, p1.x, p1.y), qb0, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      r = __builtin_amdgcn_mfma_f32_16x16x32_bf16(mk8(p2.x, p2.y, p3.x, p3.y), qb1, r, 0, 0, 0);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) sc[4 * t + rr] = r[rr];
+    }
+    const int d0 = i - 1 - kb - 8 * g;   // key kb + 8g + j is committed (< i) iff j <= d0
+    float cm = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sc[j] = j <= d0 ? sc[j] : -INFINITY;
+      cm = fmaxf(cm, sc[j]);
+    }
+    const float nm = fmaxf(m, cross_row_max(cm) * ATT_L2);
+    const float alpha = fast_exp2(m - nm);
+    float ps = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sc[j] = fast_exp2(fmaf(sc[j], ATT_L2, -nm));
+      ps += sc[j];
+    }
+    l = l * alpha + ps;
+    bf16x8 ph, pl;
+    split8v(sc, ph, pl);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const bf16x8 va = kvs.vT(kb, 16 * mt, lane);
+      o[mt] *= alpha;
+      o[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, ph, o[mt], 0, 0, 0);
+      o[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pl, o[mt], 0, 0, 0);
+    }
+    m = nm;
+  }
+  const float il = 1.f / cross_row_sum(l);
+  CT O;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) O.v[mt] = o[mt] * il;
+  // head-0 columns (banks 0, 2) take head 1's dims from column c + 4, head-1 columns (banks 1, 3) head 0's from c - 4
+  O.v[2] = dpp_banks4<0x124, 0x5>(O.v[2]);
+  O.v[3] = dpp_banks4<0x124, 0x5>(O.v[3]);
+  O.v[0] = dpp_banks4<0x12C, 0xA>(O.v[0]);
+  O.v[1] = dpp_banks4<0x12C, 0xA>(O.v[1]);
+  return O;
+}
+// packed word K of this lane's candidate half: lane K (lower half) or 8 + K (upper half) of the row
+template <int K>
+__device__ __forceinline__ uint32_t pair_word(float pk, bool up) {
+  return __builtin_bit_cast(uint32_t, up ? row_bcast<8 + K>(pk) : row_bcast<K>(pk));
+}
+// GELU of the PAIR layout as the packed bf16 MFMA operand: lane (c & 7) = j evaluates features 2j, 2j + 1 of its row
+// (packed word j = CTr q[j >> 1] half j & 1); 8 row broadcasts per candidate half
+__device__ __forceinline__ CTr gelu_pair_pk(const CT& h, int lane) {
+  const int c = lane & 15, j = c & 7;
+  const f32x4 a01 = (j & 2) ? h.v[1] : h.v[0], a23 = (j & 2) ? h.v[3] : h.v[2];   // feature tile j >> 1
+  const f32x4 a = (j & 4) ? a23 : a01;
+  const float lo = (j & 1) ? a[2] : a[0], hi = (j & 1) ? a[3] : a[1];
+  const float pk = __builtin_bit_cast(float, pk2(gelu_erf(lo), gelu_erf(hi)));
+  const bool up = c & 8;
+  CTr o;
+  o.q[0] = make_uint2(pair_word<0>(pk, up), pair_word<1>(pk, up));
+  o.q[1] = make_uint2(pair_word<2>(pk, up), pair_word<3>(pk, up));
+  o.q[2] = make_uint2(pair_word<4>(pk, up), pair_word<5>(pk, up));
+  o.q[3] = make_uint2(pair_word<6>(pk, up), pair_word<7>(pk, up));
+  return o;
+}
+
 // block 0 (ma_transformer.py:95-98) of row i for the wave's 16 candidates: x = the candidates' embedded input rows in,
 // block 0's output out; kp / vp = their cross-attention K / V rows (staged for the commit)
-template <class KVS>
+template <bool PAIR, class KVS>
 __device__ __forceinline__ void sp_block0(CT& x, const CTr& cq, const CTr& ck, const CTr& cv, const RegW<6>& w0,
                                           const WvCtx& k, const KVS& selfkv, int i, const CT& repi, const CTr& q2,
                                           CTr& kp, CTr& vp) {
   const int lane = k.lane, g = lane >> 4, L = k.L;
   CT xh;
   {
-    const CT O = sp_attn(selfkv, cq, ck, cv, i, lane);
+    CT O;
+    if constexpr (PAIR) O = sp_attn_pair(selfkv, cq, ck, cv, i, lane);
+    else O = sp_attn(selfkv, cq, ck, cv, i, lane);
     CT t = ct_add(ld_vec(k.BI + 64 * 3, lane), x);
     mm(t, w0.w[0], ct_pack(O));
     ln_fwd_ct(t, xh, x, ld_vec(k.LP, lane), ld_vec(k.LP + 64, lane));
@@ -802,7 +927,10 @@ __device__ __forceinline__ void sp_block0(CT& x, const CTr& cq, const CTr& ck, c
     vp = ct_pack(vv);
   }
   {
-    const CT O = sp_attn(SpCache{wv_cache(k.KV, 0, 2, L), wv_cache(k.KV, 0, 3, L)}, q2, kp, vp, i, lane);
+    const SpCache cross{wv_cache(k.KV, 0, 2, L), wv_cache(k.KV, 0, 3, L)};
+    CT O;
+    if constexpr (PAIR) O = sp_attn_pair(cross, q2, kp, vp, i, lane);
+    else O = sp_attn(cross, q2, kp, vp, i, lane);
     CT t = ct_add(ld_vec(k.BI + 64 * 7, lane), repi);
     mm(t, w0.w[3], ct_pack(O));
     ln_fwd_ct(t, xh, x, ld_vec(k.LP + 128, lane), ld_vec(k.LP + 128 + 64, lane));
@@ -810,9 +938,15 @@ __device__ __forceinline__ void sp_block0(CT& x, const CTr& cq, const CTr& ck, c
   {
     CT h = ld_vec(k.BI + 64 * 8, lane);
     mm(h, w0.w[4], ct_pack(x));
-    gelu_ct(h);
+    CTr hp;
+    if constexpr (PAIR) {
+      hp = gelu_pair_pk(h, lane);
+    } else {
+      gelu_ct(h);
+      hp = ct_pack(h);
+    }
     CT t = ct_add(ld_vec(k.BI + 64 * 9, lane), x);
-    mm(t, w0.w[5], ct_pack(h));
+    mm(t, w0.w[5], hp);
     ln_fwd_ct(t, xh, x, ld_vec(k.LP + 256, lane), ld_vec(k.LP + 256 + 64, lane));
   }
 }
@@ -840,9 +974,12 @@ __device__ __forceinline__ CTr sp_q2(const AFr& wq, const float* bias, const CT&
   return ct_pack(q);
 }
 
-template <int NB, int NS, int NREG, int MA, bool IND, bool Q2F>
+template <int NB, int NS, int NREG, int MA, bool IND, bool Q2F, bool PAIR>
 __global__ __launch_bounds__(64 * (1 + NS), 1) void mat_decode_spec_kernel(DecParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+#ifdef MDL_SPEC_PROF
+  const unsigned long long spp_t0 = __builtin_amdgcn_s_memtime();
+#endif
   constexpr int NM = wv_nm(NB), NMM = NM - 6, NLDS = NM - NREG;   // main: slots 6 .. NM - 1, LDS: 6 .. NLDS - 1
   constexpr int NT = 64 * (1 + NS);
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, c = lane & 15;
@@ -861,6 +998,8 @@ __global__ __launch_bounds__(64 * (1 + NS), 1) void mat_decode_spec_kernel(DecPa
   float* SLOT = (float*)(smem + lo.slot);
   bf16_t* STG = (bf16_t*)(smem + lo.stg);
   int* TOK = (int*)(smem + lo.tok);
+  constexpr bool STQ = MDL_SPEC_STQ && PAIR && NREG <= 6;   // = sp_stq
+  constexpr int SR = STQ ? 320 : 128;     // staged bf16 elements per candidate
   const float* rep = p.rep + (size_t)env * L * 64;
 
   // ---------------------------------------------------------------- setup (all waves)
@@ -913,19 +1052,24 @@ __global__ __launch_bounds__(64 * (1 + NS), 1) void mat_decode_spec_kernel(DecPa
     if (lane == 0) TOK[0] = tok;
     __syncthreads();   // (1) row 0's block 0 is staged
     SPP_DECL;
+#ifdef MDL_SPEC_PROF
+    spp_acc[3] = spp_t - spp_t0;   // 3: setup + row 0's block 0 (kernel start -> first agent step)
+#endif
 #pragma unroll 1
     for (int i = 0; i < L; ++i) {
       SPP(0);   // 0: barrier wait
       const CT repi = ld_vec(rep + (size_t)i * 64, lane);
       const float avl = (ava && lane < A) ? ava[(size_t)i * A + lane] : 1.f;
-      CT x = ld_vec(SLOT + (size_t)((i & 1) * A + (i == 0 ? 0 : tok - 1)) * 64, lane);
+      const int cidx = (i & 1) * A + (i == 0 ? 0 : tok - 1);
+      CT x = ld_vec(SLOT + (size_t)cidx * 64, lane);
+      const bf16_t* stq = STG + (size_t)cidx * SR + 128;   // PAIR: the staged q / k / v of block 1
       if constexpr (Q2F) {
         AFr wq;
         wv_getw<0, 1, 0>(wq, RegW<0>{}, Wl + (size_t)(NLDS - 6) * 4096, lane);
         const CTr q2 = sp_q2(wq, BI + 64 * (10 * 1 + 4), repi, lane);
-        wv_block<1, NB, NLDS, NREG>(x, k, rw, i, tok, repi, &q2);
+        wv_block<1, NB, NLDS, NREG, STQ>(x, k, rw, i, tok, repi, &q2, stq);
       } else if constexpr (NB > 1) {
-        wv_block<1, NB, NLDS, NREG>(x, k, rw, i, tok, repi);
+        wv_block<1, NB, NLDS, NREG, STQ>(x, k, rw, i, tok, repi, nullptr, stq);
       }
       SPP(1);   // 1: slot read + block 1
 #ifdef MDL_SPEC_PROF
@@ -963,17 +1107,39 @@ __global__ __launch_bounds__(64 * (1 + NS), 1) void mat_decode_spec_kernel(DecPa
       if constexpr (IND) return SpTokRows{QT, ROWTOK};
       else return SpCache{wv_cache(KV, 0, 0, L), wv_cache(KV, 0, 1, L)};
     }();
-    const int cand = 16 * (wave - 1) + c;   // this lane's candidate: input token 1 + cand (rows >= 1)
-    const bool own = cand < A;
+    // this lane's candidate: input token 1 + cand (rows >= 1); PAIR: columns c >> 3, one writer column each
+    const int cand = PAIR ? c >> 3 : 16 * (wave - 1) + c;
+    const bool own = cand < A && (!PAIR || (c & 7) == 0);
     auto stage = [&](int par, const CT& x, const CTr& kp, const CTr& vp) {
+      CTr pr[3];   // PAIR: block 1's q / k / v of the candidate's block-0 output (weights: the main wave's LDS slots)
+      if constexpr (STQ && NB > 1) {
+        const CTr xp = ct_pack(x);
+        AFr w;
+        wv_getw<wv_slot(1, 0), NLDS, 0>(w, RegW<0>{}, k.W, lane);
+        CT t0 = ld_vec(BI + 64 * 10, lane);
+        mm(t0, w, xp);
+        wv_getw<wv_slot(1, 1), NLDS, 0>(w, RegW<0>{}, k.W, lane);
+        CT t1 = ld_vec(BI + 64 * 11, lane);
+        mm(t1, w, xp);
+        wv_getw<wv_slot(1, 2), NLDS, 0>(w, RegW<0>{}, k.W, lane);
+        CT t2 = ld_vec(BI + 64 * 12, lane);
+        mm(t2, w, xp);
+        pr[0] = ct_pack(t0);
+        pr[1] = ct_pack(t1);
+        pr[2] = ct_pack(t2);
+      }
       if (own) {
         float* sl = SLOT + (size_t)(par * A + cand) * 64;
-        bf16_t* st = STG + (size_t)(par * A + cand) * 128;
+        bf16_t* st = STG + (size_t)(par * A + cand) * SR;
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
           *(f32x4*)(sl + 16 * mt + 4 * g) = x.v[mt];
           *(uint2*)(st + 16 * mt + 4 * g) = kp.q[mt];
           *(uint2*)(st + 64 + 16 * mt + 4 * g) = vp.q[mt];
+          if constexpr (STQ && NB > 1) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) *(uint2*)(st + 128 + 64 * j + 16 * mt + 4 * g) = pr[j].q[mt];
+          }
         }
       }
     };
@@ -982,12 +1148,15 @@ __global__ __launch_bounds__(64 * (1 + NS), 1) void mat_decode_spec_kernel(DecPa
       CT x = c0.e;
       CTr kp, vp;
       const CT rep0 = ld_vec(rep, lane);
-      sp_block0(x, c0.q, c0.k, c0.v, w0, k, selfkv, 0, rep0, q2row(0, rep0), kp, vp);
+      sp_block0<PAIR>(x, c0.q, c0.k, c0.v, w0, k, selfkv, 0, rep0, q2row(0, rep0), kp, vp);
       stage(0, x, kp, vp);
     }
     const SpCand cd = sp_cand(QT, p.emb, min(1 + cand, p.n_tok - 1), lane);
     __syncthreads();   // (1)
     SPP_DECL;
+#ifdef MDL_SPEC_PROF
+    spp_acc[3] = spp_t - spp_t0;
+#endif
 #pragma unroll 1
     for (int i = 0; i < L; ++i) {
       SPP(4);   // 4: barrier wait
@@ -999,7 +1168,7 @@ __global__ __launch_bounds__(64 * (1 + NS), 1) void mat_decode_spec_kernel(DecPa
       if (lane < 32 && (!IND || lane >= 16)) {
         const int kind = lane >> 3, ch = lane & 7;
         const bf16_t* src = kind < 2 ? QT + tk * 192 + 64 * (kind + 1) + 8 * ch
-                                     : STG + (size_t)((i & 1) * A + (i == 0 ? 0 : tk - 1)) * 128 + 64 * (kind - 2) + 8 * ch;
+                                     : STG + (size_t)((i & 1) * A + (i == 0 ? 0 : tk - 1)) * SR + 64 * (kind - 2) + 8 * ch;
         *(uint4*)(wv_cache(KV, 0, kind, L) + tmo(i, 8 * ch)) = *(const uint4*)src;
       }
       asm volatile("" ::: "memory");   // the committed row is read back by other lanes below (LDS is in order per wave)
@@ -1007,7 +1176,7 @@ __global__ __launch_bounds__(64 * (1 + NS), 1) void mat_decode_spec_kernel(DecPa
       if (i + 1 < L) {
         CT x = cd.e;
         CTr kp, vp;
-        sp_block0(x, cd.q, cd.k, cd.v, w0, k, selfkv, i + 1, repn, q2row(i + 1, repn), kp, vp);
+        sp_block0<PAIR>(x, cd.q, cd.k, cd.v, w0, k, selfkv, i + 1, repn, q2row(i + 1, repn), kp, vp);
         SPP(6);   // 6: block 0
         stage((i + 1) & 1, x, kp, vp);
         SPP(7);   // 7: staging stores
@@ -1018,12 +1187,23 @@ __global__ __launch_bounds__(64 * (1 + NS), 1) void mat_decode_spec_kernel(DecPa
   }
 }
 
-template <int NB, int NS, int NREG, int MA, bool IND = false, bool Q2F = false>
-int sp_launch(const DecParams* p, size_t lds, hipStream_t st) {
-  hipError_t e = hipFuncSetAttribute((const void*)mat_decode_spec_kernel<NB, NS, NREG, MA, IND, Q2F>,
+template <int NB, int NS, int NREG, int MA, bool IND, bool Q2F>
+int sp_launch_wide(const DecParams* p, size_t lds, hipStream_t st) {   // 3..4 narrow-head actions: 16-candidate layout
+  hipError_t e = hipFuncSetAttribute((const void*)mat_decode_spec_kernel<NB, NS, NREG, MA, IND, Q2F, false>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return -(int)e;
-  hipLaunchKernelGGL((mat_decode_spec_kernel<NB, NS, NREG, MA, IND, Q2F>), dim3(p->B), dim3(64 * (1 + NS)), lds, st, *p);
+  hipLaunchKernelGGL((mat_decode_spec_kernel<NB, NS, NREG, MA, IND, Q2F, false>), dim3(p->B), dim3(64 * (1 + NS)), lds, st, *p);
+  e = hipGetLastError();
+  return e == hipSuccess ? 0 : -(int)e;
+}
+template <int NB, int NS, int NREG, int MA, bool IND = false, bool Q2F = false>
+int sp_launch(const DecParams* p, size_t lds, hipStream_t st) {
+  constexpr bool PAIR = MDL_SPEC_PAIR && NS == 1 && MA == 1;
+  if (PAIR && p->act_dim > 2) return sp_launch_wide<NB, NS, NREG, MA, IND, Q2F>(p, lds, st);
+  hipError_t e = hipFuncSetAttribute((const void*)mat_decode_spec_kernel<NB, NS, NREG, MA, IND, Q2F, PAIR>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return -(int)e;
+  hipLaunchKernelGGL((mat_decode_spec_kernel<NB, NS, NREG, MA, IND, Q2F, PAIR>), dim3(p->B), dim3(64 * (1 + NS)), lds, st, *p);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : -(int)e;
 }

@@ -15,10 +15,10 @@ from test_gpu_decode import inputs, make  # noqa: E402
 from mat_dcml_amd.ops import mat_fused  # noqa: E402
 from mat_dcml_amd.ops.kernels import lib  # noqa: E402
 
-NAMES = {0: "main: barrier wait", 1: "main: slot read + block 1", 2: "main: head + sampling (rest)",
+NAMES = {3: "main: setup (per launch / L)", 0: "main: barrier wait", 1: "main: slot read + block 1", 2: "main: head + sampling (rest)",
          8: "main: head W_h1 product", 9: "main: head GELU", 10: "main: head LN stats + split",
          11: "main: head logit MFMAs", 12: "main: sampling", 13: "main: action / log-prob stores",
-         16 + 4: "spec: barrier wait", 16 + 5: "spec: commit", 16 + 6: "spec: block 0", 16 + 7: "spec: staging"}
+         16 + 3: "spec: setup (per launch / L)", 16 + 4: "spec: barrier wait", 16 + 5: "spec: commit", 16 + 6: "spec: block 0", 16 + 7: "spec: staging"}
 
 
 def main():
