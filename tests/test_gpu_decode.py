@@ -246,7 +246,11 @@ def _both_kernels(m, rep, ava, det, rand, spec=False):
 
 @pytest.mark.parametrize("L,B,nb,atype,A", [(33, 256, 2, "Semi_Discrete", 2), (33, 64, 1, "Semi_Discrete", 2),
                                             (5, 64, 2, "Semi_Discrete", 2), (101, 16, 1, "Semi_Discrete", 2),
-                                            (27, 32, 2, "Discrete", 36), (9, 48, 1, "Discrete", 3)])
+                                            (27, 32, 2, "Discrete", 36), (9, 48, 1, "Discrete", 3),
+                                            # the speculative kernel's other layouts: 3..4 narrow-head candidates
+                                            # (16-candidate layout, MA 1), one / two candidate waves of a wide head
+                                            (9, 48, 2, "Discrete", 3), (12, 32, 2, "Discrete", 6),
+                                            (10, 24, 2, "Discrete", 20)])
 @pytest.mark.parametrize("det", [False, True])
 @pytest.mark.parametrize("spec", [False, True])
 def test_wave_decode_matches_4wave_and_torch(gpu, L, B, nb, atype, A, det, spec):
