@@ -180,6 +180,19 @@ def build(verbose=True, jobs=None):
     return OUT
 
 
+def prune():
+    """Delete the cached objects the current sources / flags no longer use (content-hashed names accumulate)."""
+    keep = {os.path.basename(src) + "." + _hash(src) + ".o" for src in _sources()}
+    keep.add(f"buildinfo_{source_hash()}_{flags_hash()}.o")
+    d = os.path.join(OUT_DIR, "obj")
+    gone = [f for f in os.listdir(d) if f not in keep] if os.path.isdir(d) else []
+    for f in gone:
+        os.remove(os.path.join(d, f))
+    return len(gone)
+
+
 if __name__ == "__main__":
     build()
+    if "--prune" in sys.argv[1:]:
+        print(f"[build] pruned {prune()} stale cached objects")
     sys.exit(0)
