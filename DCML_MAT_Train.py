@@ -51,6 +51,11 @@ def main(args):
     device = comm.device
     if comm.is_main:
         print("choose to use gpu..." if device.type == "cuda" else "choose to use cpu...")
+    if device.type == "cuda" and all_args.cuda_deterministic:   # reference DCML_MAT_Train.py:108-110
+        # the eager torch parts deterministic too; the fused PPO update is bit-reproducible by construction (private
+        # gradient workspace, fixed-order reductions: algos/mat_trainer.py, tests/test_gpu_determinism.py)
+        torch.backends.cudnn.benchmark = False
+        torch.backends.cudnn.deterministic = True
     run_dir = make_run_dir(all_args, comm)
     if comm.is_main:
         with open(run_dir / "args.txt", "w") as f:

@@ -45,9 +45,12 @@ def parse():
     p.add_argument("--no_phase_timers", action="store_true",
                    help="skip the phase breakdown (extra instrumented steps after the timed loop; the timed loop "
                         "itself never records phase events)")
-    p.add_argument("--allreduce", default="rccl", choices=["rccl", "oneshot", "auto"],
-                   help="data-parallel gradient all-reduce: RCCL (default), the one-shot peer-memory kernel, or auto "
-                        "(one-shot only if it matches RCCL and is faster at start-up)")
+    p.add_argument("--allreduce", default="rccl", choices=["rccl", "oneshot", "auto", "ordered"],
+                   help="data-parallel gradient all-reduce: RCCL (default), the one-shot peer-memory kernel, auto "
+                        "(one-shot only if it matches RCCL and is faster at start-up), or ordered (all-gather + "
+                        "rank-order sum: bitwise independent of how the buffer is split)")
+    p.add_argument("--grad_overlap", action="store_true",
+                   help="data parallelism: all-reduce the decoder's gradient slice under the encoder backward")
     p.add_argument("--config", default="dcml", choices=["dcml", "smac"],
                    help="dcml: the headline 32-worker DCML config; smac: MAT on the SMAC-shaped 27m_vs_30m stress env")
     p.add_argument("--rollout_groups", type=int, default=1,
@@ -118,6 +121,8 @@ def main():
             "--seed", "1", "--rollout_groups", str(a.rollout_groups)]
     if a.phases:
         argv.append("--profile_phases")
+    if a.grad_overlap:
+        argv.append("--grad_overlap")
     args = parse_args(argv, get_config(), warn=False)
     runner = DCMLRunner({"all_args": args, "device": comm.device, "run_dir": None, "comm": comm})
     runner.warmup()
@@ -182,6 +187,10 @@ def main():
             "ranks": n, "backend": topo["backend"], "rank_devices": topo["devices"], "hosts": topo["hosts"],
             "kernels": paths, "native_build": _native_build(), "grad_allreduce": getattr(runner.trainer, "grad_allreduce", topo["backend"]) if n > 1 else None,
             "grad_allreduce_probe": comm.oneshot_probe,
+            # which gradient path ran: the workspace mode, bit-reproducibility, the update
+            # launch, and under data parallelism the single blocking all-reduce vs the overlapped two-slice schedule
+            "grad_path": _grad_path(runner.trainer, n),
+            "deterministic": bool(getattr(runner.trainer, "deterministic", False)),
             # scaling diagnostics: each rank's own ms per step (max = ms_per_step up to the closing barrier) and the
             # critical-path collective time per step (hipEvents on the compute stream, max over ranks)
             **diag,
@@ -222,6 +231,13 @@ def phase_breakdown(a, runner, comm, sync):
                                                if k in tot}}
 
 
+def _grad_path(tr, n):
+    m = tr.policy.transformer
+    return {"workspace": getattr(m, "_mdl_gws_mode", None), "fused_update": bool(getattr(tr, "_upd_fused", False)),
+            "allreduce": None if n == 1 else ("overlap(decoder slice under enc_bwd)" if tr.grad_overlap else
+                                              f"single blocking ({getattr(tr, 'grad_allreduce', 'rccl')})")}
+
+
 def _native_build():
     """Source hash of the loaded HIP library (ops/kernels.lib() checked it against the tree), or None."""
     from mat_dcml_amd.ops import kernels
@@ -240,7 +256,7 @@ def eval_block(a, args, runner, dev):
     ``--steps``: the benchmarked runner's weights are never used here."""
     from mat_dcml_amd.algos.policy import TransformerPolicy
     from mat_dcml_amd.envs.dcml.spaces import dcml_action_spaces
-    from mat_dcml_amd.runner.benchmark import eval_report, run_sweep
+    from mat_dcml_amd.runner.benchmark import eval_report, frontier_counts, run_sweep
 
     def fresh_policy():
         torch.manual_seed(1)
@@ -278,7 +294,11 @@ def eval_block(a, args, runner, dev):
                                        "beyond_per_point": [f["beyond"] for f in fr],
                                        "dominated_by_per_point": [f["dominated_by"] for f in fr],
                                        "payment_margin_per_point": [f["margin"] for f in fr],
-                                       "beyond_count": sum(f["beyond"] for f in fr)}
+                                       "outside_per_point": [f["outside"] for f in fr],
+                                       "dominates_per_point": [f["dominates"] for f in fr],
+                                       # only numeric positive margins count; points faster than every
+                                       # heuristic setting are counted apart, with no verdict
+                                       **{k + "_count": v for k, v in frontier_counts(fr).items()}}
     info["fixed_heuristic"] = summary(run_sweep(None, runner.dcml, dev, fixed=True, latency_b1=0, **kw))
     return info
 

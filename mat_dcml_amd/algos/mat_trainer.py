@@ -61,6 +61,9 @@ class MATTrainer:
         self._use_value_active_masks = args.use_value_active_masks
         self._use_policy_active_masks = args.use_policy_active_masks
         self.recompute_gae_every_epoch = getattr(args, "recompute_gae_every_epoch", True)
+        # data parallelism: the decoder's gradient slice all-reduced asynchronously, overlapped with the encoder
+        # backward (--grad_overlap, off by default: one blocking all-reduce of the flat buffer per minibatch)
+        self.grad_overlap = bool(getattr(args, "grad_overlap", False)) and comm is not None and comm.world_size > 1
         self.value_normalizer = ValueNorm(getattr(args, "n_objective", 1), device=self.device, comm=comm) \
             if self._use_valuenorm else None
         self.generator = None
@@ -107,8 +110,23 @@ class MATTrainer:
         if self.comm.world_size > 1:
             self.grad_allreduce = self.comm.maybe_enable_oneshot(flat.buf.numel())
         copies = int(os.environ.get("MAT_DCML_GRAD_COPIES", "32"))
+        # private per-workgroup copies (deterministic, no atomics; round 6) unless MAT_DCML_GRAD_MODE=atomic
+        mode = os.environ.get("MAT_DCML_GRAD_MODE", "private")
         if copies > 0:
-            mat_train.attach_grad_workspace(m, flat.buf, copies=copies)
+            mat_train.attach_grad_workspace(m, flat.buf, copies=copies, mode=mode)
+        # kernels that add into .grad directly, outside the workspace (the wide-observation embedding backward): the
+        # flat buffer is then zeroed per minibatch and the reduction adds to it; otherwise the reduction overwrites
+        self._direct_grads = m.encoder.obs_dim > mat_train.MAX_FUSED_OBS or mode != "private" or copies <= 0
+        self.deterministic = mode == "private" and copies > 0 and not self._direct_grads
+        self._upd_fused = (mode == "private" and copies > 0 and self.comm.world_size == 1
+                           and os.environ.get("MAT_DCML_FUSED_UPDATE", "1") != "0")
+        # the reference's cuda_deterministic (store_false: ON unless --cuda_deterministic is passed,
+        # DCML_MAT_Train.py:108-110): the fused trainer's PPO update is bit-reproducible with the private gradient
+        # workspace (tests/test_gpu_determinism.py); wide observations keep fp32 atomics in their embedding backward
+        if getattr(args, "cuda_deterministic", False) and not self.deterministic and self.device.type == "cuda":
+            import warnings
+            warnings.warn("cuda_deterministic: this configuration's fused update is not bit-reproducible "
+                          f"(gradient mode {mode}, direct gradient writers {self._direct_grads})")
         pol.optimizer = ppo_fused.FlatAdam(fp, flat.buf, lr=pol.optimizer.param_groups[0]["lr"], eps=args.opti_eps,
                                            weight_decay=args.weight_decay,
                                            max_grad_norm=args.max_grad_norm if self._use_max_grad_norm else None,
@@ -155,12 +173,21 @@ class MATTrainer:
             flat.buf.zero_()
         else:
             pol.optimizer.zero_grad(set_to_none=False)
+        split = self._overlap_split() if self.grad_overlap and flat is not None and not self.poison else None
         with self.timers("train_bwd"):
-            loss.backward()
+            if split is None:
+                loss.backward()
+            else:   # decoder slice first, its all-reduce in flight while the encoder's gradients are computed
+                dec_params, enc_params, (lo, hi), rest = split
+                loss.backward(inputs=dec_params, retain_graph=True)
+                work = self.comm.all_reduce_sum_async(flat.buf[lo:hi], grad=True)
+                loss.backward(inputs=enc_params)
         if self.poison:
             for p in self.params:
                 p.grad.fill_(float("nan"))
-        if self.comm is not None and self.comm.world_size > 1:
+        if split is not None:
+            self._finish_overlap(flat.buf, work, rest)
+        elif self.comm is not None and self.comm.world_size > 1:
             self.comm.all_reduce_grads_(self.params)
             self.collectives += 1
         if flat is not None:
@@ -188,17 +215,42 @@ class MATTrainer:
             v, rep = enc.forward(mb["obs"], save=True)
             logp, ent = dec.forward(rep, mb["actions"], mb["ava"], save=True)
         buf = self.comm._flat.buf
-        buf.zero_()
+        if self._direct_grads:
+            buf.zero_()
         dv, dlp, dent = self.loss_fused.run(v, logp, ent, mb, self.comm, pre_stats=pre_stats)
-        m._mdl_gws_active = hasattr(m, "_mdl_gws")   # weight-gradient atomics into the 8-copy workspace
+        m._mdl_gws_active = hasattr(m, "_mdl_gws")   # weight gradients into the workspace copies
+        split = self._overlap_split() if self.grad_overlap and not self.poison else None
+        work = None
         with tm("train_bwd"):
             drep = dec.backward(dlp, dent)
+            if split is not None:   # the decoder slice is final: reduce its copies, all-reduce it under enc_bwd
+                lo, hi = split[2]
+                mat_train.reduce_grad_workspace(m, lo, hi, accumulate=self._direct_grads, last=False)
+                work = self.comm.all_reduce_sum_async(buf[lo:hi], grad=True)
             enc.backward(drep, dv)
         m._mdl_gws_active = False
+        if split is not None:
+            for lo, hi in split[3]:
+                mat_train.reduce_grad_workspace(m, lo, hi, accumulate=self._direct_grads, last=(lo, hi) == split[3][-1])
+            dec.ctx = None
+            enc.ctx = None
+            self._finish_overlap(buf, work, split[3])
+            pol.optimizer.step(norm_ready=False)
+            mat_fused.bump_version(m)
+            return pol.optimizer.grad_norm
         # one process: the workspace reduction also leaves the optimizer's Σ g² partials of the final gradient (no
         # norm launch); under data parallelism the norm is the all-reduced gradient's, so the Adam step computes it
         fuse_norm = self.comm.world_size == 1 and not self.poison
-        norm_ready = mat_train.reduce_grad_workspace(m, norm_into=pol.optimizer.scratch if fuse_norm else None)
+        if fuse_norm and self._upd_fused:
+            # round 6: reduction + clip + Adam + weight repack in ONE cooperative launch (csrc/ppo.hip)
+            mat_train.update_fused(m, pol.optimizer, accumulate=self._direct_grads)
+            dec.ctx = None
+            enc.ctx = None
+            mat_fused.bump_version(m)
+            mat_train.mark_packs_current(m)
+            return pol.optimizer.grad_norm
+        norm_ready = mat_train.reduce_grad_workspace(m, norm_into=pol.optimizer.scratch if fuse_norm else None,
+                                                     accumulate=self._direct_grads)
         dec.ctx = None
         enc.ctx = None
         if self.poison:
@@ -214,6 +266,39 @@ class MATTrainer:
         return pol.optimizer.grad_norm
 
     # ------------------------------------------------------------------------------------------------
+    def _overlap_split(self):
+        """(decoder params, encoder params, decoder flat range, other flat ranges) of the overlapped gradient
+        all-reduce, or None when the decoder's gradients are not one contiguous range of the flat buffer."""
+        cached = getattr(self, "_split", False)
+        if cached is not False:
+            return cached
+        from ..ops import mat_train
+        m = self.policy.transformer
+        flat = self.comm._flat
+        dec = [p for p in m.decoder.parameters() if p.requires_grad]
+        ids = {id(p) for p in dec}
+        enc = [p for p in self.params if id(p) not in ids]
+        flat.ensure_views()
+        r = mat_train.flat_range(dec, flat.buf) if dec and enc else None
+        if r is None:
+            self._split = None
+            return None
+        lo, hi = r
+        hi = min(flat.buf.numel(), (hi + 15) // 16 * 16)   # the per-parameter padding belongs to the slice
+        rest = [x for x in ((0, lo), (hi, flat.buf.numel())) if x[1] > x[0]]
+        self._split = (dec, enc, (lo, hi), rest)
+        return self._split
+
+    def _finish_overlap(self, buf, work, rest):
+        """All-reduce the remaining ranges (blocking), wait for the decoder slice, average."""
+        for lo, hi in rest:
+            self.comm.grad_sum_(buf[lo:hi])
+        if work is not None:
+            with self.comm._timed("grad_allreduce"):
+                work.wait()
+        buf.mul_(1.0 / self.comm.world_size)
+        self.collectives += 1 + len(rest)
+
     def _epoch_stats(self, buffer, idx_list, native):
         """Advantage moments (masked Σ, Σ², n) and, under data parallelism with a value normaliser, every
         minibatch's return moments of this epoch — ONE all-reduce per epoch (the reference's per-minibatch

@@ -176,6 +176,8 @@ _FRAMEWORK_FLAGS = [
     ("rollout_groups", int, 1, "env groups of the rollout, each on its own HIP stream: one group's env step / insert / "
      "encoder overlap the other groups' decode (SURVEY §2.4); the rollout is identical for any group count"),
     ("eval_stride", int, 2, "batch decision stride for evaluation (dcml_runner.py:320)"),
+    ("grad_overlap", "true", F, "data parallelism: all-reduce the decoder's gradient slice asynchronously while the "
+     "encoder backward runs (two collectives per minibatch instead of one blocking all-reduce)"),
     ("recompute_gae_every_epoch", "false", T, "recompute next-value/GAE every PPO epoch (reference semantics)"),
     ("results_dir", str, None, "root of results/ (default: ./results)"),
     ("resume", "true", F, "resume from the latest trainer_state_*.pt in the run dir"),

@@ -648,7 +648,7 @@ __device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c)
   }
   __syncthreads();
   CP_MARK(1);
-  wgrad_g(c.DA, c.XB, c.KP, c.g(p.d_wh2), 64, p.A, 64, c.g(p.d_bh2), c.wave, lane);
+  wgrad_g(c.DA, c.XB, c.KP, c.g(p.d_wh2), 64, p.A, 64, c.g(p.d_bh2), c.wave, lane, c.gm);
   wgrad64(c.DQ, c.KB, p.h1, c);
   __syncthreads();
   CP_MARK(19);
@@ -719,8 +719,8 @@ __global__ __launch_bounds__(NTHR, FWD_WGPC) void mat_dec_fwd_ct(DecP p) {
 
 // ============================================================================================== backward
 template <int NB, int MA, bool CONT>
-__device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0, int nseq) {
-  const Ctx c = make_ctx(p, smem, seq0, nseq);
+__device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0, int nseq, bool first) {
+  const Ctx c = make_ctx(p, smem, seq0, nseq, first);
   if (c.nseq <= 0) return;
   zero_pad_rows(c);
   __syncthreads();
@@ -801,8 +801,9 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
     flush_vec(dlb, c.g(p.d_lnd_b), 3, c);
     __syncthreads();
     if (p.d_wa) {
-      wgrad_g(c.DA, c.XB, c.KP, c.g(p.d_wa), p.A + 1, 64, p.A + 1, nullptr, c.wave, lane);
-      wgrad_g(c.DQ, c.XB, c.KP, c.g(p.d_wa), p.A + 1, 64, p.A + 1, nullptr, c.wave, lane);
+      wgrad_g(c.DA, c.XB, c.KP, c.g(p.d_wa), p.A + 1, 64, p.A + 1, nullptr, c.wave, lane, c.gm);
+      // the lo half adds onto the hi half's flush (private copies: same lanes, same addresses, program order)
+      wgrad_g(c.DQ, c.XB, c.KP, c.g(p.d_wa), p.A + 1, 64, p.A + 1, nullptr, c.wave, lane, GradMode{c.gm.priv, false});
     }
   } else {
     float* EMB = (float*)c.QB;   // [(A+1)][64] f32 accumulators (QB + KB: 2 NRP x 128 B >= 65 x 256 B)
@@ -845,8 +846,10 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
     __syncthreads();
     for (int i = c.tid; i < (p.A + 1) * 64; i += NTHR) {   // W_a [64][A] and b_a
       const int t = i / 64, col = i % 64;
-      if (t < p.A) { if (p.d_wa) atomicAdd(c.g(p.d_wa) + col * p.A + t, EMB[i]); }
-      else if (p.d_ba) atomicAdd(c.g(p.d_ba) + col, EMB[i]);
+      float* d = t < p.A ? (p.d_wa ? c.g(p.d_wa) + col * p.A + t : nullptr) : (p.d_ba ? c.g(p.d_ba) + col : nullptr);
+      if (!d) continue;
+      if (c.gm.priv) *d = c.gm.first ? EMB[i] : *d + EMB[i];   // this thread owns the element in every chunk
+      else atomicAdd(d, EMB[i]);
     }
   }
   CP_MARK(30);
@@ -858,7 +861,7 @@ __global__ __launch_bounds__(NTHR, WGPC) void mat_dec_bwd_ct(DecP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   CP_BEGIN();
   vacc_begin(p, smem);
-  FOR_TILES(p, (dec_bwd_tile<NB, MA, CONT>(p, smem, s0, ns)));
+  FOR_TILES(p, (dec_bwd_tile<NB, MA, CONT>(p, smem, s0, ns, it_ == 0)));
   vacc_end(p, smem);
   CP_END();
 }

@@ -675,6 +675,9 @@ struct SpLds { int w, kv, q2, qt, bi, lp, sc, slot, stg, tok, rowtok, total; };
 #ifndef MDL_SPEC_PAIR
 #define MDL_SPEC_PAIR 1
 #endif
+#ifndef MDL_PAIR_ROR_OLD
+#define MDL_PAIR_ROR_OLD 0
+#endif
 #ifndef MDL_SPEC_STQ
 #define MDL_SPEC_STQ 0
 #endif
@@ -873,11 +876,20 @@ __device__ __forceinline__ CT sp_attn_pair(const KVS& kvs, const CTr& q, const C
   CT O;
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) O.v[mt] = o[mt] * il;
-  // head-0 columns (banks 0, 2) take head 1's dims from column c + 4, head-1 columns (banks 1, 3) head 0's from c - 4
-  O.v[2] = dpp_banks4<0x124, 0x5>(O.v[2]);
-  O.v[3] = dpp_banks4<0x124, 0x5>(O.v[3]);
-  O.v[0] = dpp_banks4<0x12C, 0xA>(O.v[0]);
-  O.v[1] = dpp_banks4<0x12C, 0xA>(O.v[1]);
+  // head-0 columns (banks 0, 2) take head 1's dims from column c + 4, head-1 columns (banks 1, 3) head 0's from c - 4.
+  // row_ror:N moves a value N lanes UP the row (lane c reads lane c - N mod 16, tests/native/dpp_ror_probe.hip), so
+  // "from c + 4" is row_ror:12 and "from c - 4" row_ror:4.  (Rounds 5: the two were swapped — each candidate took the
+  // OTHER candidate's second head, invisible with near-identical candidates (random-init weights) but 0.1 nats of
+  // log-prob error per row with a trained policy; MDL_PAIR_ROR_OLD=1 rebuilds that variant for the A/B check.)
+#if MDL_PAIR_ROR_OLD
+  constexpr int ROR_UP = 0x124, ROR_DN = 0x12C;
+#else
+  constexpr int ROR_UP = 0x12C, ROR_DN = 0x124;
+#endif
+  O.v[2] = dpp_banks4<ROR_UP, 0x5>(O.v[2]);
+  O.v[3] = dpp_banks4<ROR_UP, 0x5>(O.v[3]);
+  O.v[0] = dpp_banks4<ROR_DN, 0xA>(O.v[0]);
+  O.v[1] = dpp_banks4<ROR_DN, 0xA>(O.v[1]);
   return O;
 }
 // packed word K of this lane's candidate half: lane K (lower half) or 8 + K (upper half) of the row

@@ -197,8 +197,8 @@ __global__ __launch_bounds__(NTHR, FWD_WGPC) void mat_enc_fwd_ct(EncP p, EncX ex
 
 // ============================================================================================== backward
 template <int NB>
-__device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char* smem, int seq0, int nseq) {
-  const Ctx c = make_ctx(p, smem, seq0, nseq);
+__device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char* smem, int seq0, int nseq, bool first) {
+  const Ctx c = make_ctx(p, smem, seq0, nseq, first);
   if (c.nseq <= 0) return;
   zero_pad_rows(c);
   __syncthreads();
@@ -375,7 +375,7 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
         if (p.d_lno_b) vacc_add(c.g(p.d_lno_b), 9, dim, ob, c);
       }
       __syncthreads();
-      wgrad_g(c.DA, c.XB, c.KP, c.g(p.d_we), p.od, 64, p.od, nullptr, c.wave, lane);
+      wgrad_g(c.DA, c.XB, c.KP, c.g(p.d_we), p.od, 64, p.od, nullptr, c.wave, lane, c.gm);
     }
   }
   CP_MARK(30);
@@ -387,7 +387,7 @@ __global__ __launch_bounds__(NTHR, WGPC) void mat_enc_bwd_ct(EncP p, EncX ex) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   CP_BEGIN();
   vacc_begin(p, smem);
-  FOR_TILES(p, (enc_bwd_tile<NB>(p, ex, smem, s0, ns)));
+  FOR_TILES(p, (enc_bwd_tile<NB>(p, ex, smem, s0, ns, it_ == 0)));
   vacc_end(p, smem);
   CP_END();
 }
@@ -411,6 +411,12 @@ MDL_API int mdl_mat_train_geometry_ct(int L) {
   }
   if (mat_train_lds_bytes(NRP, SQ, L) > LDS_BUDGET || (SQ * L + 15) / 16 > 4 * MAXRT) return 0;
   return SQ | (NRP << 16);
+}
+
+// workgroups of a backward launch over Bs sequences in tiles of SQ (= the private gradient copies it writes)
+MDL_API int mdl_ct_bwd_grid(int Bs, int SQ) {
+  const int tiles = (Bs + SQ - 1) / SQ, cap = n_cus();
+  return tiles < cap ? tiles : cap;
 }
 
 MDL_API int mdl_mat_enc_fwd_ct(const EncP* p, const float* pre_in, int NB, int save, hipStream_t st) {

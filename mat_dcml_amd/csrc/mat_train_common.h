@@ -18,15 +18,24 @@ __host__ __device__ inline size_t mat_train_lds_main_bytes(int NRP) {
   const size_t aux = (size_t)NRP * 2 * 4 * 2;   // LSE / delta [2][NRP] f32 (also the decoder's embedding-grad scratch)
   return (size_t)NRP * 64 * 2 * 6 + (aux < 9 * 64 * 4 ? 9 * 64 * 4 : aux);
 }
-// Behind the token buffers (NRP <= 192: 150.5 KB + 6.2 KB < 160 KB):
-//  * the per-workgroup parameter-vector accumulators (VSLOTS x 64 f32) and their global destinations (VSLOTS
-//    pointers): LayerNorm / bias / log-std gradient partials are summed here with LDS atomics across ALL of the
-//    workgroup's chunks and leave by global fp32 atomics once, at the end of the launch.  A global atomic sits in
-//    the issuing wave's in-order vmcnt queue for ~3,000 cycles under load, so one flushed per LayerNorm made the
-//    next phase's saved-activation loads wait for it (~16 such stalls per chunk).
+// Behind the token buffers (NRP <= 192: 150.5 KB + 12.2 KB + 16 B < 160 KB):
+//  * the per-workgroup parameter-vector accumulators (VSLOTS x 64, int64 fixed point) and their global destinations
+//    (VSLOTS pointers): LayerNorm / bias / log-std gradient partials are summed here with LDS atomics across ALL of
+//    the workgroup's chunks and leave once, at the end of the launch.  A global atomic sits in the issuing wave's
+//    in-order vmcnt queue for ~3,000 cycles under load, so one flushed per LayerNorm made the next phase's
+//    saved-activation loads wait for it (~16 such stalls per chunk).
+//    Round 6: the partials are added as 2^-32 fixed-point int64 (ds_add_u64): integer addition is associative, so the
+//    sum no longer depends on the order in which the 8 waves reach their LDS atomics — the workgroup's vector
+//    gradients are bit-reproducible (fp32 LDS atomics were not).  A partial of magnitude >= 2^24 (or non-finite)
+//    raises the workgroup's overflow flag, and the flush then writes NaN: the optimizer skips such a step, exactly
+//    as it skips any non-finite gradient.
 constexpr int VSLOTS = 24;
+constexpr float VFX_SCALE = 4294967296.f;        // 2^32
+constexpr float VFX_INV = 1.f / 4294967296.f;
+constexpr float VFX_MAX = 16777216.f;            // 2^24: larger partials -> overflow flag (<= 2^7 adds per slot
+                                                 // element stay below 2^63)
 __host__ __device__ inline size_t mat_train_lds_bytes(int NRP, int SQ, int L) {
-  return mat_train_lds_main_bytes(NRP) + (size_t)VSLOTS * (64 * 4 + 8);
+  return mat_train_lds_main_bytes(NRP) + (size_t)VSLOTS * (64 * 8 + 8 + 4) + 16;
 }
 
 namespace {
@@ -81,6 +90,7 @@ struct EncP {
   int g_copies;                  // 0: atomics straight into the gradients
   float* d_bh2;                  // value-head bias gradient Σ dv (round-2 backward; null: summed by the caller)
   HSv hs, es;                    // value head, observation embedding (round 4)
+  int g_mode;                    // 1: one PRIVATE workspace copy per workgroup, plain stores (GradMode below)
 };
 
 struct DecP {
@@ -117,16 +127,33 @@ struct DecP {
   const float* ba;
   float* d_ba;
   HSv hs;                // action head (round 4)
+  int g_mode;            // 1: one PRIVATE workspace copy per workgroup, plain stores (GradMode below)
 };
+
+// Weight-gradient flush modes (round 6).  ATOMIC (rounds 2-5): fp32 atomics into a workspace copy shared by
+// g_copies / G workgroups — the memory-side atomic unit (~1.35 TB/s chip-wide) made them cost ~121 us per
+// minibatch, and their order made every run's gradient differ in the last bits.  PRIVATE: the gradient workspace
+// has ONE copy per workgroup of the launch; a workgroup's first chunk STORES its partial gradients, its later chunks
+// load + add + store their own earlier values (the loads issued before the weight-gradient MFMA loop, so their
+// latency hides under it).  No atomics, no cross-workgroup races, a fixed summation order: the gradient is
+// bit-reproducible, and csrc/ppo.hip:grad_reduce_priv folds the copies in copy order.  The 64 x 64 weight
+// gradients sit in the copies in the MFMA fragment order (each lane stores its two f32x4 accumulators as 16-byte
+// pieces: 1 KB per wave-instruction pair) and the reduction maps them back to row-major.
+// Micro-benchmark (tests/native/wgrad_flush_bench.hip, 256 workgroups x 8 waves x 22 matrices x 3 chunks):
+// atomics 207 us + 6 us reduction, private copies 73 us + 17 us.
+struct GradMode { bool priv, first; };
 
 struct Ctx {
   int tid, lane, wave, L, nseq, NR, NT, NRP, KP, tok0;   // KP: rows [0, KP) = NR rounded up to 32 (<= NRP)
-  ptrdiff_t gofs;   // gradient-copy offset (floats): this block's slice of the 8-way dW workspace, 0 = direct
+  ptrdiff_t gofs;   // gradient-copy offset (floats): this block's copy of the dW workspace, 0 = direct
+  GradMode gm;      // flush mode of this chunk (private copies: first chunk of the workgroup stores)
   __device__ __forceinline__ float* g(float* p) const { return p ? p + gofs : p; }
   bf16_t *QB, *KB, *VB, *DA, *DQ, *XB;
   float *LSE, *DEL;
-  float* VACC;  // [VSLOTS][64] parameter-vector gradient accumulators (LDS, per workgroup, all chunks)
-  float** VPT;  // [VSLOTS] their global destinations (null = unused slot)
+  unsigned long long* VACC;  // [VSLOTS][64] parameter-vector gradient accumulators (LDS, 2^-32 fixed point)
+  float** VPT;               // [VSLOTS] their global destinations (null = unused slot)
+  int* VLEN;                 // [VSLOTS] 1 + the largest element index added (the flush writes no further)
+  int* VOVF;                 // overflow / non-finite flag of the accumulators
 };
 
 constexpr float ATT_SCALE = 0.17677669529663687f;  // 1/sqrt(32)
@@ -232,7 +259,7 @@ __device__ __forceinline__ void zero_lds(char* smem, size_t bytes, int tid) {
 
 // ------------------------------------------------------------------------------------------ context
 template <typename PT>
-__device__ __forceinline__ Ctx make_ctx(const PT& p, char* smem, int seq0, int nseq) {
+__device__ __forceinline__ Ctx make_ctx(const PT& p, char* smem, int seq0, int nseq, bool first_chunk = true) {
   Ctx c;
   c.tid = threadIdx.x;
   asm volatile("" : "+v"(c.tid));   // opaque per tile: lane-derived addresses are not hoisted out of the tile loop
@@ -248,41 +275,62 @@ __device__ __forceinline__ Ctx make_ctx(const PT& p, char* smem, int seq0, int n
   // spread the fp32 weight-gradient atomics over g_copies copies (blockIdx % 8 ~ the XCD the block runs on):
   // 8x fewer adders per address than every workgroup hitting the same 16 KB matrix
   c.gofs = p.g_copies > 0 ? (ptrdiff_t)p.g_delta + (ptrdiff_t)(blockIdx.x % p.g_copies) * (ptrdiff_t)p.g_stride : 0;
+  c.gm.priv = p.g_copies > 0 && p.g_mode == 1;   // private mode: the host sized g_copies >= gridDim.x
+  c.gm.first = first_chunk;
   const size_t bs = (size_t)p.NRP * 64;
   bf16_t* base = (bf16_t*)smem;
   c.QB = base; c.KB = base + bs; c.VB = base + 2 * bs; c.DA = base + 3 * bs; c.DQ = base + 4 * bs; c.XB = base + 5 * bs;
   c.LSE = (float*)(base + 6 * bs);
   c.DEL = c.LSE + 2 * p.NRP;
-  c.VACC = (float*)(smem + mat_train_lds_main_bytes(p.NRP));
+  c.VACC = (unsigned long long*)(smem + mat_train_lds_main_bytes(p.NRP));
   c.VPT = (float**)(c.VACC + VSLOTS * 64);
+  c.VLEN = (int*)(c.VPT + VSLOTS);
+  c.VOVF = c.VLEN + VSLOTS;
   return c;
 }
 
 // parameter-vector accumulators: zeroed before a workgroup's first chunk, flushed after its last (backward kernels)
 template <typename PT>
 __device__ __forceinline__ void vacc_begin(const PT& p, char* smem) {
-  float* V = (float*)(smem + mat_train_lds_main_bytes(p.NRP));
+  unsigned long long* V = (unsigned long long*)(smem + mat_train_lds_main_bytes(p.NRP));
   float** P = (float**)(V + VSLOTS * 64);
-  for (int i = threadIdx.x; i < VSLOTS * 64; i += NTHR) V[i] = 0.f;
-  for (int i = threadIdx.x; i < VSLOTS; i += NTHR) P[i] = nullptr;
+  int* N = (int*)(P + VSLOTS);   // VLEN [VSLOTS], then the overflow flag
+  for (int i = threadIdx.x; i < VSLOTS * 64; i += NTHR) V[i] = 0ull;
+  for (int i = threadIdx.x; i < VSLOTS; i += NTHR) {
+    P[i] = nullptr;
+    N[i] = 0;
+  }
+  if (threadIdx.x == 0) N[VSLOTS] = 0;
   __syncthreads();
 }
+// private mode: every element [0, VLEN) of a used slot is STORED (its workgroup's copy holds nothing else there:
+// zeros included, so a stale value of an earlier launch never survives) and nothing past it — a slot shorter than 64
+// (log_std, value-head bias, LN_obs) must not touch the neighbouring parameters' entries; shared copies: fp32 atomics
 template <typename PT>
 __device__ __forceinline__ void vacc_end(const PT& p, char* smem) {
   __syncthreads();
-  const float* V = (const float*)(smem + mat_train_lds_main_bytes(p.NRP));
+  const unsigned long long* V = (const unsigned long long*)(smem + mat_train_lds_main_bytes(p.NRP));
   float* const* P = (float* const*)(V + VSLOTS * 64);
+  const int* N = (const int*)(P + VSLOTS);
+  const bool bad = N[VSLOTS] != 0;
+  const bool priv = p.g_copies > 0 && p.g_mode == 1;
   for (int i = threadIdx.x; i < VSLOTS * 64; i += NTHR) {
     float* d = P[i >> 6];
-    const float v = V[i];
-    if (d && v != 0.f) atomicAdd(d + (i & 63), v);
+    if (!d || (i & 63) >= N[i >> 6]) continue;
+    const float v = bad ? __builtin_nanf("") : (float)(long long)V[i] * VFX_INV;
+    if (priv) d[i & 63] = v;
+    else if (v != 0.f) atomicAdd(d + (i & 63), v);
   }
 }
 // add v to element idx (< 64) of the parameter-vector gradient dst (already offset to this block's gradient copy)
 __device__ __forceinline__ void vacc_add(float* dst, int slot, int idx, float v, const Ctx& c) {
   if (!dst) return;
-  atomicAdd(c.VACC + slot * 64 + idx, v);   // LDS atomic (ds_add_f32): no vmcnt entry
-  c.VPT[slot] = dst;                        // every writer stores the same pointer
+  const float s = v * VFX_SCALE;
+  if (!(fabsf(s) < VFX_MAX * VFX_SCALE)) *c.VOVF = 1;   // also catches NaN / inf
+  const long long q = fabsf(s) < VFX_MAX * VFX_SCALE ? (long long)__builtin_rintf(s) : 0ll;
+  atomicAdd(c.VACC + slot * 64 + idx, (unsigned long long)q);   // LDS integer atomic (ds_add_u64): order-free
+  atomicMax(c.VLEN + slot, idx + 1);
+  c.VPT[slot] = dst;                                           // every writer stores the same pointer
 }
 
 }  // namespace

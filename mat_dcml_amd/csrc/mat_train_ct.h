@@ -69,7 +69,11 @@ static int launch_ct(K kern, const PT* p, bool fwd, hipStream_t st, X... extra) 
   if (e != hipSuccess) return (int)e;
   const int tiles = (p->Bs + p->SQ - 1) / p->SQ;
   const int cap = n_cus() * (fwd ? FWD_WGPC : 1);
-  hipLaunchKernelGGL(kern, dim3(tiles < cap ? tiles : cap), dim3(NTHR), lds, st, *p, extra...);
+  const int grid = tiles < cap ? tiles : cap;
+  // private gradient copies (GradMode): one copy per workgroup of THIS launch, and the fragment layout of the
+  // 8-wave block mapping (grad_reduce_priv folds exactly `grid` copies)
+  if (!fwd && p->g_copies > 0 && p->g_mode == 1 && (NW != 8 || grid > p->g_copies)) return -5;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(NTHR), lds, st, *p, extra...);
   MDL_CHECK_LAUNCH();
   return 0;
 }
@@ -461,13 +465,21 @@ __device__ __forceinline__ void flush_rows2(const f32x4& acc0, const f32x4& acc1
     WATOM(dW + (16 * rb + 8 + 4 * s + r) * 64 + col, __builtin_bit_cast(float, (unsigned)q[1]));
   }
 }
+// Private-copy position of a lane's accumulator j (an f32x4 over r) of a 64 x 64 weight gradient: FRAGMENT order
+// (wave, lane, j, r) with the 8-wave block mapping above (row 16 (w & 3) + 4 g + r, column 16 (2 (w >> 2) + j) + c);
+// csrc/ppo.hip grad_reduce_priv folds the copies and writes each element to its row-major place.
+__device__ __forceinline__ f32x4* frag_slot(float* dW, int wave, int lane, int j) {
+  return reinterpret_cast<f32x4*>(dW + wave * 512 + lane * 8 + 4 * j);
+}
+
 // dW[n][k] (row stride ld) += Σ_t Y[t][n] X[t][k] for n < nrows, k < ncols, and db[n] += Σ_t Y[t][n], from
 // token-major swizzled LDS tiles of KP rows (KP % 32 == 0, padded rows zero).  The 16 output blocks (row block
 // j & 3, column tile j >> 2) are dealt round robin, j = wave + NW i: a wave's blocks share one row block (NW % 4 == 0)
 // and so one Y fragment per k-step.  The bias gradient is one extra MFMA per k-step against a ones fragment (the
-// waves holding column tile 0).  fp32 atomics.
+// waves holding column tile 0).  Shared workspace copies: fp32 atomics; private copies (GradMode): row-major
+// stores, or load + add + store after the workgroup's first chunk (loads issued before the MFMA loop).
 __device__ __forceinline__ void wgrad_g(const bf16_t* Y, const bf16_t* X, int KP, float* dW, int ld, int nrows, int ncols,
-                                        float* db, int wave, int lane) {
+                                        float* db, int wave, int lane, GradMode gm) {
   static_assert(NW % 4 == 0, "row block per wave");
   constexpr int NCT = (16 + NW - 1) / NW;           // column tiles per wave (at most)
   const int rb = wave & 3;
@@ -475,6 +487,20 @@ __device__ __forceinline__ void wgrad_g(const bf16_t* Y, const bf16_t* X, int KP
   const int nct = dW ? (ncols + 15) >> 4 : 0;
   if ((!db && wg_ct(wave, 0) >= nct) || 16 * rb >= nrows) return;
   const int g = lane >> 4, c16 = lane & 15;
+  const bool rmw = gm.priv && !gm.first;
+  f32x4 old[NCT];
+  float oldb = 0.f;
+#pragma unroll
+  for (int j = 0; j < NCT; ++j) {
+    const int ct = wg_ct(wave, j);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = 16 * rb + 4 * g + r, k = 16 * ct + c16;
+      const bool ok = rmw && dW && wg_has(wave, j) && ct < nct && n < nrows && k < ncols;
+      old[j][r] = ok ? dW[n * ld + k] : 0.f;
+    }
+  }
+  if (rmw && db && c16 < 4 && 16 * rb + 4 * g + c16 < nrows) oldb = db[16 * rb + 4 * g + c16];
   f32x4 acc[NCT];
 #pragma unroll
   for (int j = 0; j < NCT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -492,7 +518,17 @@ __device__ __forceinline__ void wgrad_g(const bf16_t* Y, const bf16_t* X, int KP
     }
     if (db) accb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ones, accb, 0, 0, 0);
   }
-  if (dW && WG_ROWS2 && ld == 64 && nrows == 64 && ncols == 64) {
+  if (dW && gm.priv) {
+#pragma unroll
+    for (int j = 0; j < NCT; ++j) {
+      const int ct = wg_ct(wave, j);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = 16 * rb + 4 * g + r, k = 16 * ct + c16;
+        if (wg_has(wave, j) && ct < nct && n < nrows && k < ncols) dW[n * ld + k] = acc[j][r] + old[j][r];
+      }
+    }
+  } else if (dW && WG_ROWS2 && ld == 64 && nrows == 64 && ncols == 64) {
     if constexpr (WG_ROWS2) flush_rows2(acc[0], acc[1], dW, rb, wg_ct(wave, 0), lane);
   } else if (dW) {
 #pragma unroll
@@ -509,31 +545,38 @@ __device__ __forceinline__ void wgrad_g(const bf16_t* Y, const bf16_t* X, int KP
   if (db && c16 < 4) {
     const float v = c16 == 0 ? accb[0] : c16 == 1 ? accb[1] : c16 == 2 ? accb[2] : accb[3];
     const int n = 16 * rb + 4 * g + c16;
-    if (n < nrows) atomicAdd(db + n, v);
+    if (n < nrows) {
+      if (gm.priv) db[n] = v + oldb;
+      else atomicAdd(db + n, v);
+    }
   }
 }
-__device__ __forceinline__ void wgrad64(const bf16_t* Y, const bf16_t* X, const Mat& m, const Ctx& c) {
-  wgrad_g(Y, X, c.KP, c.g(m.dW), 64, 64, 64, c.g(m.db), c.wave, c.lane);
-}
 
-// The weight gradients of TWO or THREE 64x64 matrices that share their input X (dW_q / dW_k / dW_v of an attention,
-// dW_k / dW_v of the cross attention): one pass over the token axis reads each X fragment once for all of them
-// (wgrad64 per matrix re-read X: 6 transposed LDS reads per 2 MFMAs; here 2 + 2 NM per 2 NM).
+// The weight gradients of ONE, TWO or THREE 64x64 matrices that share their input X (dW_q / dW_k / dW_v of an
+// attention, dW_k / dW_v of the cross attention): one pass over the token axis reads each X fragment once for all
+// of them (a pass per matrix re-read X: 6 transposed LDS reads per 2 MFMAs; here 2 + 2 NM per 2 NM).  Private copies:
+// fragment-order 16-byte stores (frag_slot), the earlier chunks' partials loaded before the MFMA loop.
 template <int NM>
 __device__ __forceinline__ void wgrad64_shared_x(const bf16_t* const (&Y)[NM], const bf16_t* X, const Mat* const (&m)[NM],
                                                  const Ctx& c) {
-#ifdef MDL_WG_SEQ
-  // A/B: one matrix at a time (its atomics issued before the next matrix's MFMAs: bursts of 8, not 8 NM)
-#pragma unroll
-  for (int i = 0; i < NM; ++i) wgrad64(Y[i], X, *m[i], c);
-  return;
-#endif
   static_assert(NW % 4 == 0, "row block per wave");
   constexpr int NCT = (16 + NW - 1) / NW;
   const int wave = c.wave, lane = c.lane, KP = c.KP;
   const int rb = wave & 3;
   const bool bias = wave < 4;
   const int g = lane >> 4, c16 = lane & 15;
+  // private copies need the 8-wave block mapping of frag_slot (the host refuses the mode otherwise)
+  const bool priv = NW == 8 && c.gm.priv, rmw = priv && !c.gm.first;
+  f32x4 old[NM][NCT];
+  float oldb[NM];
+#pragma unroll
+  for (int i = 0; i < NM; ++i) {
+    float* dW = c.g(m[i]->dW);
+    float* db = c.g(m[i]->db);
+#pragma unroll
+    for (int j = 0; j < NCT; ++j) old[i][j] = (rmw && dW) ? *frag_slot(dW, wave, lane, j) : f32x4{0.f, 0.f, 0.f, 0.f};
+    oldb[i] = (rmw && bias && db && c16 < 4) ? db[16 * rb + 4 * g + c16] : 0.f;
+  }
   f32x4 acc[NM][NCT], accb[NM];
 #pragma unroll
   for (int i = 0; i < NM; ++i) {
@@ -561,7 +604,10 @@ __device__ __forceinline__ void wgrad64_shared_x(const bf16_t* const (&Y)[NM], c
     float* dW = c.g(m[i]->dW);
     float* db = c.g(m[i]->db);
     if (dW) {
-      if constexpr (WG_ROWS2) {
+      if (priv) {
+#pragma unroll
+        for (int j = 0; j < NCT; ++j) *frag_slot(dW, wave, lane, j) = acc[i][j] + old[i][j];
+      } else if constexpr (WG_ROWS2) {
         flush_rows2(acc[i][0], acc[i][1], dW, rb, wg_ct(wave, 0), lane);
       } else {
 #pragma unroll
@@ -573,9 +619,15 @@ __device__ __forceinline__ void wgrad64_shared_x(const bf16_t* const (&Y)[NM], c
     }
     if (bias && db && c16 < 4) {
       const float v = c16 == 0 ? accb[i][0] : c16 == 1 ? accb[i][1] : c16 == 2 ? accb[i][2] : accb[i][3];
-      atomicAdd(db + 16 * rb + 4 * g + c16, v);
+      if (priv) db[16 * rb + 4 * g + c16] = v + oldb[i];
+      else atomicAdd(db + 16 * rb + 4 * g + c16, v);
     }
   }
+}
+__device__ __forceinline__ void wgrad64(const bf16_t* Y, const bf16_t* X, const Mat& m, const Ctx& c) {
+  const bf16_t* const ys[1] = {Y};
+  const Mat* const ms[1] = {&m};
+  wgrad64_shared_x<1>(ys, X, ms, c);
 }
 
 // q / k / v projections of the packed tiles xp (one weight matrix live at a time) -> QB / KB / VB; m0 = index of

@@ -213,6 +213,7 @@ struct AdamArgs {
                       // [4 .. 4 + ADAM_NB) per-workgroup Σ g² partials
   float lr, beta1, beta2, eps, wd, t, max_norm;   // t = optimizer steps attempted so far, this one included
   int clip;
+  int npart;          // Σ g² partials written (the step sums exactly these; 0 = ADAM_NB)
 };
 
 // The norm pass writes one Σ g² partial per workgroup; every step workgroup sums the ADAM_NB partials itself in a
@@ -220,6 +221,7 @@ struct AdamArgs {
 // single-GPU trainer computes them inside the gradient-workspace reduction (grad_reduce_norm_kernel, one workgroup
 // per partial at the reduction's full width) and skips the norm launch.
 constexpr int ADAM_NB = 1024;
+constexpr int ADAM_NORM_NB = 128;   // the standalone norm pass (data-parallel path)
 
 __global__ __launch_bounds__(256) void adam_norm_kernel(AdamArgs a) {
   __shared__ float sm[4];
@@ -242,8 +244,8 @@ __global__ __launch_bounds__(256) void adam_step_kernel(AdamArgs a) {
   __shared__ float snorm;
   if (threadIdx.x < 64) {   // wave 0: Σ of the ADAM_NB partials (ADAM_NB / 64 per lane, fixed order)
     float v = 0.f;
-#pragma unroll
-    for (int j = 0; j < ADAM_NB / 64; ++j) v += a.sumsq[4 + 64 * j + threadIdx.x];
+    const int np = a.npart > 0 ? a.npart : ADAM_NB;
+    for (int j = threadIdx.x; j < np; j += 64) v += a.sumsq[4 + j];
     const float tot = wave_sum(v);
     if (threadIdx.x == 0) snorm = sqrtf(tot);
   }
@@ -282,11 +284,15 @@ MDL_API int mdl_adam_scratch_floats() { return 4 + ADAM_NB; }
 MDL_API int mdl_adam(const AdamArgs* a, int norm_ready, hipStream_t st) {
   int g = (a->n + 255) / 256;
   if (g > 1024) g = 1024;
+  AdamArgs b = *a;
+  // the standalone norm pass (data parallelism: the all-reduced gradient) runs its round-4 grid of 128 workgroups and
+  // the step sums exactly those partials; norm_ready: ADAM_NB partials from the workspace reduction
+  b.npart = norm_ready ? ADAM_NB : ADAM_NORM_NB;
   if (!norm_ready) {
-    hipLaunchKernelGGL(adam_norm_kernel, dim3(ADAM_NB), dim3(256), 0, st, *a);
+    hipLaunchKernelGGL(adam_norm_kernel, dim3(ADAM_NORM_NB), dim3(256), 0, st, b);
     MDL_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL(adam_step_kernel, dim3(g), dim3(256), 0, st, *a);
+  hipLaunchKernelGGL(adam_step_kernel, dim3(g), dim3(256), 0, st, b);
   MDL_CHECK_LAUNCH();
   return 0;
 }
@@ -347,10 +353,193 @@ MDL_API int mdl_grad_reduce_norm(float* g, float* ws, int n, long long stride, i
   return 0;
 }
 
+// Private-copy workspace (round 6, mat_train_common.h GradMode): one copy per workgroup of the backward launches,
+// every entry a workgroup writes rewritten by its first chunk — so no zero fill, and a fixed summation order:
+//   g[dst[s]] = (accumulate ? g[dst[s]] : 0) + Σ_{k < copies} ws[k * stride + s]   (k ascending)
+// dst maps the fragment-order 64 x 64 weight gradients back to row-major (identity elsewhere); the loads run along
+// the copies' own order (coalesced), the stores are the permuted ones.  sumsq (optional): the optimizer's Σ g²
+// partial of the FINAL gradient per workgroup (sumsq[4 + blockIdx], ADAM_NB workgroups), as grad_reduce_norm.
+__global__ __launch_bounds__(256) void grad_reduce_priv_kernel(float* g, const float* ws, const int* dst, int lo,
+                                                               int n, long long stride, int copies, int accumulate,
+                                                               float* sumsq) {
+  __shared__ float sm[4];
+  float q = 0.f;
+  for (int i = lo + blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    float s = 0.f;
+    int k = 0;
+    for (; k + 8 <= copies; k += 8) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = ws[(size_t)(k + j) * stride + i];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[j];
+    }
+    for (; k < copies; ++k) s += ws[(size_t)k * stride + i];
+    const int d = dst[i];
+    const float gi = accumulate ? g[d] + s : s;
+    g[d] = gi;
+    q += gi * gi;
+  }
+  if (!sumsq) return;
+  q = wave_sum(q);
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = q;
+  __syncthreads();
+  if (threadIdx.x == 0) sumsq[4 + blockIdx.x] = (sm[0] + sm[1]) + (sm[2] + sm[3]);
+}
+
+// elements [lo, hi) of the flat gradient (a parameter range: no 64 x 64 matrix straddles it); sumsq whole-buffer only
+MDL_API int mdl_grad_reduce_priv(float* g, const float* ws, const int* dst, int lo, int hi, long long stride,
+                                 int copies, int accumulate, float* sumsq, hipStream_t st) {
+  if (copies < 1 || lo < 0 || hi < lo || (sumsq && lo != 0)) return -1;
+  hipLaunchKernelGGL(grad_reduce_priv_kernel, dim3(ADAM_NB), dim3(256), 0, st, g, ws, dst, lo, hi, stride, copies,
+                     accumulate, sumsq);
+  MDL_CHECK_LAUNCH();
+  return 0;
+}
+
 MDL_API int mdl_grad_reduce(float* g, float* ws, int n, long long stride, int copies, hipStream_t st) {
   int grid = (n + 255) / 256;
   if (grid > 1024) grid = 1024;
   hipLaunchKernelGGL(grad_reduce_kernel, dim3(grid), dim3(256), 0, st, g, ws, n, stride, copies);
   MDL_CHECK_LAUNCH();
   return 0;
+}
+
+// ------------------------------------------------------------------------------------------- fused update (round 6)
+// ONE cooperative launch per single-GPU minibatch replaces grad_reduce + adam_norm / adam_step + pack_weights (and the
+// flat-buffer memset): (1) fold the private workspace copies into the flat gradient (grad_reduce_priv's loop) with
+// per-workgroup Σ g² partials; (2) one grid barrier; (3) every workgroup sums the partials in a fixed order (the
+// same norm everywhere, run to run), workgroups 0 .. nmat-1 each apply clip + Adam to ONE 64 x 64 weight matrix and
+// repack it from LDS into the forward / backward fragment orders of the training kernels (csrc/rl_ops.hip
+// pack_weights layout), the other workgroups update the remaining parameters (rest[] indices).  The grid barrier's
+// co-residency is guaranteed by hipLaunchCooperativeKernel; its wait is bounded (an error word, never a hang).
+struct PackEntU { const float* src; unsigned short* fw; unsigned short* bw; unsigned short* fa; unsigned short* ba; };
+struct UpdArgs {
+  float* g; const float* ws; const int* dst; int n; long long stride; int copies; int accumulate;
+  AdamArgs a;
+  const PackEntU* tab; const int* mat_off; int nmat;   // packed matrices and their flat offsets
+  const int* rest; int n_rest;                         // flat indices of every other parameter element
+  unsigned int* bar;                                   // [0] arrivals, [1] generation, [2] error word
+};
+
+__device__ __forceinline__ bool upd_grid_barrier(unsigned int* bar) {
+  __threadfence();   // this thread's phase-1 stores visible at agent scope
+  __syncthreads();
+  __shared__ int ok;
+  if (threadIdx.x == 0) {
+    ok = 1;
+    const unsigned gen = __hip_atomic_load(bar + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned arrived = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (arrived == gridDim.x - 1) {
+      __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(bar + 1, gen + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      long long spins = 0;
+      while (__hip_atomic_load(bar + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1ll << 26)) {   // ~seconds: never hang the device on a broken co-residency assumption
+          __hip_atomic_store(bar + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = 0;
+          break;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  __threadfence();
+  return ok != 0;
+}
+
+__device__ __forceinline__ float adam_elem(const AdamArgs& a, int i, float scale, float ib1, float ib2) {
+  float g = a.g[i] * scale;
+  float p = a.p[i];
+  if (a.wd != 0.f) g += a.wd * p;
+  const float m = a.m[i] * a.beta1 + (1.f - a.beta1) * g;
+  const float v = a.v[i] * a.beta2 + (1.f - a.beta2) * g * g;
+  a.m[i] = m;
+  a.v[i] = v;
+  p -= a.lr * (m * ib1) / (sqrtf(v * ib2) + a.eps);
+  a.p[i] = p;
+  return p;
+}
+
+__global__ __launch_bounds__(256) void update_fused_kernel(UpdArgs u) {
+  __shared__ float sm[4];
+  __shared__ float snorm;
+  __shared__ float Mf[4096];
+  // (1) private workspace copies -> flat gradient, Σ g² partial of this workgroup
+  float q = 0.f;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < u.n; i += gridDim.x * blockDim.x) {
+    float s = 0.f;
+    int k = 0;
+    for (; k + 8 <= u.copies; k += 8) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = u.ws[(size_t)(k + j) * u.stride + i];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[j];
+    }
+    for (; k < u.copies; ++k) s += u.ws[(size_t)k * u.stride + i];
+    const int d = u.dst[i];
+    const float gi = u.accumulate ? u.g[d] + s : s;
+    u.g[d] = gi;
+    q += gi * gi;
+  }
+  q = wave_sum(q);
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = q;
+  __syncthreads();
+  if (threadIdx.x == 0) u.a.sumsq[4 + blockIdx.x] = (sm[0] + sm[1]) + (sm[2] + sm[3]);
+  // (2)
+  if (!upd_grid_barrier(u.bar)) return;
+  // (3) norm of the final gradient: Σ of the gridDim.x partials in a fixed order
+  const AdamArgs& a = u.a;
+  if (threadIdx.x < 64) {
+    float v = 0.f;
+    for (int j = threadIdx.x; j < (int)gridDim.x; j += 64) v += a.sumsq[4 + j];
+    const float tot = wave_sum(v);
+    if (threadIdx.x == 0) snorm = sqrtf(tot);
+  }
+  __syncthreads();
+  const float norm = snorm;
+  const float skipped = a.sumsq[2];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    a.sumsq[1] = norm;
+    a.sumsq[3] += norm;
+  }
+  if (!isfinite(norm)) {   // non-finite guard: params, moments and packs untouched
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.sumsq[2] = skipped + 1.f;
+    return;
+  }
+  const float scale = a.clip ? fminf(1.f, a.max_norm / (norm + 1e-6f)) : 1.f;
+  const float t = a.t - skipped;
+  const float ib1 = 1.f / (1.f - powf(a.beta1, t)), ib2 = 1.f / (1.f - powf(a.beta2, t));
+  if ((int)blockIdx.x < u.nmat) {
+    const int off = u.mat_off[blockIdx.x];
+    for (int e = threadIdx.x; e < 4096; e += 256) Mf[e] = adam_elem(a, off + e, scale, ib1, ib2);
+    __syncthreads();
+    const PackEntU pe = u.tab[blockIdx.x];
+    for (int idx = threadIdx.x; idx < 4096; idx += 256) {
+      const int j = idx & 7, lane = (idx >> 3) & 63, ks = (idx >> 9) & 1, ct = idx >> 10;
+      const int n = 16 * ct + (lane & 15), k = 32 * ks + 8 * (lane >> 4) + j;
+      if (pe.fw) pe.fw[idx] = mdl::f2bf(Mf[n * 64 + k]);
+      if (pe.bw) pe.bw[idx] = mdl::f2bf(Mf[k * 64 + n]);
+      const int kp = 32 * ks + 16 * (j >> 2) + 4 * (lane >> 4) + (j & 3);
+      if (pe.fa) pe.fa[idx] = mdl::f2bf(Mf[n * 64 + kp]);
+      if (pe.ba) pe.ba[idx] = mdl::f2bf(Mf[kp * 64 + n]);
+    }
+  } else {
+    const int nb = gridDim.x - u.nmat;
+    for (int r = (blockIdx.x - u.nmat) * blockDim.x + threadIdx.x; r < u.n_rest; r += nb * blockDim.x)
+      adam_elem(a, u.rest[r], scale, ib1, ib2);
+  }
+}
+
+constexpr int UPD_NB = 1024;   // = ADAM_NB: one Σ g² partial per workgroup
+MDL_API int mdl_update_fused_grid() { return UPD_NB; }
+MDL_API int mdl_update_fused(const UpdArgs* u, hipStream_t st) {
+  if (u->copies < 1 || u->nmat >= UPD_NB || u->n_rest < 0) return -1;
+  UpdArgs a = *u;
+  void* args[] = {&a};
+  hipError_t e = hipLaunchCooperativeKernel((const void*)update_fused_kernel, dim3(UPD_NB), dim3(256), args, 0, st);
+  return e == hipSuccess ? 0 : (int)e;
 }

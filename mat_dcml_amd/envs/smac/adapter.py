@@ -51,6 +51,7 @@ class SC2Game:
         """Close the game process and launch a new one (StarCraft2_Env.full_restart).  smac's env relaunches its own
         process in place; an env object without that method is rebuilt with its episode counters carried over."""
         self.force_restarts += 1
+        self._win_counted = bool(getattr(self.env, "win_counted", False))   # the live env's value (ADVICE r5)
         if hasattr(self.env, "full_restart"):
             self.env.full_restart()
             return
@@ -66,9 +67,11 @@ class SC2Game:
     def _error_info(self):
         """The info dict of a step that hit a protocol error (StarCraft2_Env.py:517-524)."""
         e = self.env
+        # win_counted as the env object had it when the error hit (read before a rebuild replaced the object: a
+        # rebuilt env starts with False); the in-place full_restart keeps the object, so its own value still holds
+        won = getattr(e, "win_counted", False) if hasattr(e, "full_restart") else getattr(self, "_win_counted", False)
         return {"battles_won": getattr(e, "battles_won", 0), "battles_game": getattr(e, "battles_game", 0),
-                "battles_draw": getattr(e, "timeouts", 0), "bad_transition": False,
-                "won": bool(getattr(e, "win_counted", False))}
+                "battles_draw": getattr(e, "timeouts", 0), "bad_transition": False, "won": bool(won)}
 
     def _observe(self):
         obs = np.array(self.env.get_obs())

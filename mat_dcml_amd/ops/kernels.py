@@ -78,6 +78,7 @@ class _BuildLock:
 
     def __enter__(self):
         import fcntl
+        os.makedirs(os.path.dirname(self.path), exist_ok=True)   # fresh checkout: nothing under _lib is tracked
         self.f = open(self.path, "a")
         fcntl.flock(self.f, fcntl.LOCK_EX)
         return self

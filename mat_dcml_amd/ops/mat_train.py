@@ -17,6 +17,7 @@ import torch
 
 from . import kernels
 from .kernels import P, check, lib, sig
+from .ppo_fused import AdamArgs
 
 VP = ctypes.c_void_p
 
@@ -51,7 +52,8 @@ class EncP(ctypes.Structure):
                                   "d_be", "d_ln0_g", "d_ln0_b")] + \
                [("blk", Blk * 3), ("h1", Mat), ("lnh", LNp), ("wh2", VP), ("bh2", VP), ("d_wh2", VP), ("rep", VP),
                 ("v", VP), ("sv", Sv * 3), ("drep", VP), ("dv", VP), ("g_delta", ctypes.c_longlong),
-                ("g_stride", ctypes.c_longlong), ("g_copies", ctypes.c_int), ("d_bh2", VP), ("hs", HSv), ("es", HSv)]
+                ("g_stride", ctypes.c_longlong), ("g_copies", ctypes.c_int), ("d_bh2", VP), ("hs", HSv), ("es", HSv),
+                ("g_mode", ctypes.c_int)]
 
 
 class DecP(ctypes.Structure):
@@ -62,7 +64,7 @@ class DecP(ctypes.Structure):
                                   "ent")] + \
                [("sv", Sv * 3)] + [(n, VP) for n in ("dlogp", "dent", "drep", "sv_head")] + \
                [("g_delta", ctypes.c_longlong), ("g_stride", ctypes.c_longlong), ("g_copies", ctypes.c_int)] + \
-               [("cont", ctypes.c_int), ("ba", VP), ("d_ba", VP), ("hs", HSv)]
+               [("cont", ctypes.c_int), ("ba", VP), ("d_ba", VP), ("hs", HSv), ("g_mode", ctypes.c_int)]
 
 
 # Training kernels (csrc/mat_train_ct.h): token-on-lane tiles, weight A fragments in permuted k order, register-
@@ -75,6 +77,8 @@ sig("mdl_mat_dec_fwd_ct", ctypes.POINTER(DecP), ctypes.c_int, ctypes.c_int, VP)
 sig("mdl_mat_dec_bwd_ct", ctypes.POINTER(DecP), ctypes.c_int, VP)
 sig("mdl_grad_reduce", VP, VP, ctypes.c_int, ctypes.c_longlong, ctypes.c_int, VP)
 sig("mdl_grad_reduce_norm", VP, VP, ctypes.c_int, ctypes.c_longlong, ctypes.c_int, VP, VP)
+sig("mdl_grad_reduce_priv", VP, VP, VP, ctypes.c_int, ctypes.c_int, ctypes.c_longlong, ctypes.c_int, ctypes.c_int, VP, VP)
+sig("mdl_ct_bwd_grid", ctypes.c_int, ctypes.c_int)
 
 
 class OEArgs(ctypes.Structure):   # csrc/obs_embed.hip
@@ -392,9 +396,7 @@ class EncoderFused:
         p.obs, p.rep, p.v, p.drep, p.dv = obs.data_ptr(), rep.data_ptr(), v.data_ptr(), drep.data_ptr(), dv.data_ptr()
         for i, s in enumerate(svs):
             p.sv[i] = s
-        p.g_delta, p.g_stride, p.g_copies = m._mdl_gws if getattr(m, "_mdl_gws_active", False) else (0, 0, 0)
-        if p.g_copies:
-            check_grad_ptrs(p, m._mdl_gws_buf[1])
+        _set_workspace(p, m, B, SQ)
         dpre = torch.empty_like(pre) if pre is not None else None
         b = m.encoder.head[3].bias
         in_kernel = b.grad is not None   # the backward kernel sums dv into the bias gradient itself
@@ -517,9 +519,7 @@ class DecoderFused:
         p.hs = hs
         for i, s in enumerate(svs):
             p.sv[i] = s
-        p.g_delta, p.g_stride, p.g_copies = m._mdl_gws if getattr(m, "_mdl_gws_active", False) else (0, 0, 0)
-        if p.g_copies:
-            check_grad_ptrs(p, m._mdl_gws_buf[1])
+        _set_workspace(p, m, B, p.SQ)
         check(getattr(lib(), "mdl_mat_dec_bwd" + sfx)(ctypes.byref(p), m.n_block, kernels._stream()), "mat_dec_bwd")
         return drep
 
@@ -551,18 +551,72 @@ class _MATFusedFn(torch.autograd.Function):
         return torch.zeros((), device=drep.device), None, None, None, None, None
 
 
-def attach_grad_workspace(model, flat_grads: torch.Tensor, copies: int = 32):
-    """Spread the backward kernels' weight-gradient atomics over ``copies`` workspace copies of the flat gradient
-    buffer (every parameter's ``.grad`` must be a view of ``flat_grads``); ``reduce_grad_workspace`` folds them
-    back.  Cuts the number of workgroups adding into one 16 KB weight matrix by ``copies``."""
+GRAD_MODES = ("private", "atomic")
+
+
+def attach_grad_workspace(model, flat_grads: torch.Tensor, copies: int = 32, mode: str = "atomic"):
+    """Gradient workspace of the backward kernels (every parameter's ``.grad`` must be a view of ``flat_grads``);
+    ``reduce_grad_workspace`` folds it back.
+    * ``atomic`` (rounds 2-5): the weight-gradient fp32 atomics spread over ``copies`` shared copies (fewer
+      workgroups adding into one 16 KB matrix);
+    * ``private`` (round 6, the trainer's default): ONE copy per workgroup of the persistent backward launches
+      (``copies`` is raised to the device's CU count), written with plain stores / read-modify-writes — no atomics,
+      a fixed summation order, a bit-reproducible gradient (csrc/mat_train_common.h GradMode).  The 64 x 64 weight
+      gradients sit in the copies in MFMA fragment order; ``dst`` maps them back."""
+    assert mode in GRAD_MODES, mode
     n = flat_grads.numel()
+    if mode == "private":
+        copies = max(copies, int(lib().mdl_ct_bwd_grid(1 << 30, 1)))   # = n_cus(): the largest backward grid
     stride = (n + 63) // 64 * 64
     ws = torch.zeros(copies * stride, dtype=torch.float32, device=flat_grads.device)
     delta = (ws.data_ptr() - flat_grads.data_ptr()) // 4
     assert (ws.data_ptr() - flat_grads.data_ptr()) % 4 == 0
     model._mdl_gws = (delta, stride, copies)
     model._mdl_gws_buf = (ws, flat_grads, stride, copies)
+    model._mdl_gws_mode = mode
+    model._mdl_gws_grid = None
+    if mode == "private":
+        model._mdl_gws_dst = _fragment_dst(model, flat_grads)
     return ws
+
+
+def _fragment_dst(model, flat):
+    """int32 [n]: where element s of a private workspace copy goes in the flat gradient.  Identity, except inside the
+    64 x 64 weight gradients the kernels flush in fragment order (wgrad64 / wgrad64_shared_x: every ModelPack linear):
+    s = o + wave * 512 + lane * 8 + 4 j + r  ->  o + 64 (16 (wave & 3) + 4 (lane >> 4) + r) + 16 (2 (wave >> 2) + j)
+    + (lane & 15)."""
+    n = flat.numel()
+    dst = torch.arange(n, dtype=torch.int64)
+    f = torch.arange(4096)
+    wave, lane, j, r = f >> 9, (f >> 3) & 63, (f >> 2) & 1, f & 3
+    row = 16 * (wave & 3) + 4 * (lane >> 4) + r
+    col = 16 * (2 * (wave >> 2) + j) + (lane & 15)
+    perm = row * 64 + col
+    assert torch.equal(perm.sort().values, f)
+    for lin in decoder_linears(model) + encoder_linears(model):
+        g = lin.weight.grad
+        if g is None or g.numel() != 4096:
+            continue
+        o = (g.data_ptr() - flat.data_ptr()) // 4
+        assert 0 <= o and o + 4096 <= n
+        dst[o:o + 4096] = o + perm
+    return dst.to(torch.int32).to(flat.device)
+
+
+def _set_workspace(p, m, B, SQ):
+    """Point the backward's gradient fields at the model's workspace (when the trainer activated it)."""
+    if getattr(m, "_mdl_gws_active", False):
+        p.g_delta, p.g_stride, p.g_copies = m._mdl_gws
+        p.g_mode = int(getattr(m, "_mdl_gws_mode", "atomic") == "private")
+        check_grad_ptrs(p, m._mdl_gws_buf[1])
+        if p.g_mode:
+            grid = int(lib().mdl_ct_bwd_grid(B, SQ))
+            if m._mdl_gws_grid not in (None, grid):
+                raise RuntimeError(f"private gradient workspace: backward grids {m._mdl_gws_grid} and {grid} differ "
+                                   "within one minibatch")
+            m._mdl_gws_grid = grid
+    else:
+        p.g_delta, p.g_stride, p.g_copies, p.g_mode = 0, 0, 0, 0
 
 
 def _grad_ptr_fields(st, prefix=""):
@@ -589,10 +643,14 @@ def check_grad_ptrs(p, flat):
         raise RuntimeError(f"gradient pointers outside the flat gradient buffer: {bad[:6]} (flat {lo:#x}..{hi:#x})")
 
 
-def reduce_grad_workspace(model, lo=0, hi=None, norm_into=None):
-    """Fold the workspace copies of flat-gradient elements [lo, hi) back into the flat buffer (and zero them).
+def reduce_grad_workspace(model, lo=0, hi=None, norm_into=None, accumulate=True, last=True):
+    """Fold the workspace copies of flat-gradient elements [lo, hi) back into the flat buffer.
     ``norm_into`` (the whole buffer only): also write the optimizer's Σ g² partials of the final gradient into that
-    FlatAdam scratch (``FlatAdam.step(norm_ready=True)`` then skips its norm launch).  Returns whether it did."""
+    FlatAdam scratch (``FlatAdam.step(norm_ready=True)`` then skips its norm launch).  Returns whether it did.
+    Atomic copies are added to the buffer and zeroed; private copies are summed in copy order over the workgroups of
+    the minibatch's backward launches, and ``accumulate=False`` overwrites the buffer (no zero fill needed when
+    nothing else wrote gradients into it).  A private range [lo, hi) must be whole parameters; ``last=False`` keeps
+    the minibatch's copy count for the reductions of the other ranges (the overlapped data-parallel schedule)."""
     st = getattr(model, "_mdl_gws_buf", None)
     if st is None:
         return False
@@ -600,6 +658,19 @@ def reduce_grad_workspace(model, lo=0, hi=None, norm_into=None):
     hi = g.numel() if hi is None else hi
     if hi <= lo:
         return False
+    if getattr(model, "_mdl_gws_mode", "atomic") == "private":
+        grid = model._mdl_gws_grid
+        if grid is None:   # no backward since the last reduction: nothing in the copies
+            if not accumulate:
+                g[lo:hi].zero_()
+            return False
+        if last:
+            model._mdl_gws_grid = None
+        fuse = norm_into is not None and lo == 0 and hi == g.numel()
+        check(lib().mdl_grad_reduce_priv(g.data_ptr(), ws.data_ptr(), model._mdl_gws_dst.data_ptr(), lo, hi, stride,
+                                         grid, int(bool(accumulate)), norm_into.data_ptr() if fuse else None,
+                                         kernels._stream()), "grad_reduce_priv")
+        return fuse
     if norm_into is not None and lo == 0 and hi == g.numel():
         check(lib().mdl_grad_reduce_norm(g.data_ptr(), ws.data_ptr(), hi, stride, copies, norm_into.data_ptr(),
                                          kernels._stream()), "grad_reduce_norm")
@@ -607,6 +678,66 @@ def reduce_grad_workspace(model, lo=0, hi=None, norm_into=None):
     check(lib().mdl_grad_reduce(g.data_ptr() + 4 * lo, ws.data_ptr() + 4 * lo, hi - lo, stride, copies,
                                 kernels._stream()), "grad_reduce")
     return False
+
+
+class UpdArgs(ctypes.Structure):   # csrc/ppo.hip update_fused_kernel
+    _fields_ = [("g", VP), ("ws", VP), ("dst", VP), ("n", ctypes.c_int), ("stride", ctypes.c_longlong),
+                ("copies", ctypes.c_int), ("accumulate", ctypes.c_int), ("a", AdamArgs), ("tab", VP),
+                ("mat_off", VP), ("nmat", ctypes.c_int), ("rest", VP), ("n_rest", ctypes.c_int), ("bar", VP)]
+
+
+sig("mdl_update_fused", ctypes.POINTER(UpdArgs), VP)
+
+
+class _UpdState:
+    """Device tables of the fused update: the packed matrices' flat offsets, every other parameter element's flat
+    index, and the grid barrier words."""
+
+    def __init__(self, model, opt):
+        mp = model_pack(model)
+        lins = decoder_linears(model) + encoder_linears(model)
+        base = opt.p.data_ptr()
+        offs = [(l.weight.data_ptr() - base) // 4 for l in lins]
+        n = opt.p.numel()
+        is_mat = torch.zeros(n, dtype=torch.bool)
+        for o in offs:
+            assert 0 <= o and o + 4096 <= n
+            is_mat[o:o + 4096] = True
+        dev = opt.p.device
+        self.mp = mp
+        self.mat_off = torch.tensor(offs, dtype=torch.int32, device=dev)
+        self.rest = torch.nonzero(~is_mat).flatten().to(torch.int32).to(dev)
+        self.bar = torch.zeros(4, dtype=torch.int32, device=dev)
+        self.nmat = len(offs)
+
+
+def update_fused(model, opt, accumulate=False):
+    """Single-GPU end of a minibatch in ONE cooperative launch (csrc/ppo.hip update_fused_kernel): fold the private
+    gradient workspace into the flat gradient, clip + Adam over every parameter, and repack the 64 x 64 linears'
+    bf16 fragments the training kernels read — replacing grad_reduce, adam_step and pack_weights (and the memset).
+    The caller bumps the model version; the ModelPack is marked current (its packs were written here)."""
+    st = getattr(model, "_mdl_upd", None)
+    if st is None or st.mp is not getattr(model, "_mdl_pack", None):
+        st = _UpdState(model, opt)
+        model._mdl_upd = st
+    ws, g, stride, copies = model._mdl_gws_buf
+    grid = model._mdl_gws_grid
+    if grid is None:
+        raise RuntimeError("update_fused: no backward wrote the private workspace this minibatch")
+    model._mdl_gws_grid = None
+    u = UpdArgs(g=g.data_ptr(), ws=ws.data_ptr(), dst=model._mdl_gws_dst.data_ptr(), n=g.numel(), stride=stride,
+                copies=grid, accumulate=int(bool(accumulate)), a=opt.next_args(), tab=st.mp.table.data_ptr(),
+                mat_off=st.mat_off.data_ptr(), nmat=st.nmat, rest=st.rest.data_ptr(), n_rest=st.rest.numel(),
+                bar=st.bar.data_ptr())
+    check(lib().mdl_update_fused(ctypes.byref(u), kernels._stream()), "update_fused")
+    return st
+
+
+def mark_packs_current(model):
+    """After update_fused + bump_version: the ModelPack already holds the new weights' fragments."""
+    mp = getattr(model, "_mdl_pack", None)
+    if mp is not None:
+        mp.version = getattr(model, "_mdl_version", 0)
 
 
 def flat_range(params, flat):

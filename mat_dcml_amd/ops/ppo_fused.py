@@ -36,7 +36,7 @@ class PPOArgs(ctypes.Structure):
 class AdamArgs(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int)] + [(k, vp) for k in ("p", "g", "m", "v", "sumsq")] + \
                [(k, ctypes.c_float) for k in ("lr", "beta1", "beta2", "eps", "wd", "t", "max_norm")] + \
-               [("clip", ctypes.c_int)]
+               [("clip", ctypes.c_int), ("npart", ctypes.c_int)]
 
 
 sig("mdl_ppo_loss", ctypes.POINTER(PPOArgs), vp)
@@ -136,15 +136,19 @@ class FlatAdam:
     def zero_grad(self, set_to_none=False):
         self.g.zero_()
 
-    def step(self, norm_ready=False):
-        """``norm_ready``: the Σ g² partials of this step's gradient are already in the scratch
-        (``mat_train.reduce_grad_workspace(..., norm_into=self.scratch)``): no norm launch."""
+    def next_args(self):
+        """AdamArgs of the next step (advances the attempted-step counter)."""
         g = self.param_groups[0]
         self.t += 1
         b1, b2 = g["betas"]
-        a = AdamArgs(n=self.p.numel(), p=P(self.p), g=P(self.g), m=P(self.m), v=P(self.v), sumsq=P(self.scratch),
-                     lr=g["lr"], beta1=b1, beta2=b2, eps=g["eps"], wd=g["weight_decay"], t=float(self.t),
-                     max_norm=float(self.max_grad_norm or 0.0), clip=int(self.max_grad_norm is not None))
+        return AdamArgs(n=self.p.numel(), p=P(self.p), g=P(self.g), m=P(self.m), v=P(self.v), sumsq=P(self.scratch),
+                        lr=g["lr"], beta1=b1, beta2=b2, eps=g["eps"], wd=g["weight_decay"], t=float(self.t),
+                        max_norm=float(self.max_grad_norm or 0.0), clip=int(self.max_grad_norm is not None), npart=0)
+
+    def step(self, norm_ready=False):
+        """``norm_ready``: the Σ g² partials of this step's gradient are already in the scratch
+        (``mat_train.reduce_grad_workspace(..., norm_into=self.scratch)``): no norm launch."""
+        a = self.next_args()
         check(lib().mdl_adam(ctypes.byref(a), int(bool(norm_ready)), _stream()), "adam")
 
     def applied_steps(self) -> int:

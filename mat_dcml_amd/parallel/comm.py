@@ -36,6 +36,8 @@ class Comm:
         self.oneshot = None          # OneShotAllReduce of the flat gradient (opt-in)
         self.oneshot_probe = None    # start-up check / timing of the one-shot path (mode "auto")
         self._timing = None          # {name: [event pairs | seconds]} while enable_timing(True)
+        # MAT_DCML_ALLREDUCE=ordered: gradients by all-gather + rank-order sum (see _ordered_sum_)
+        self.ordered = os.environ.get("MAT_DCML_ALLREDUCE", "").lower() == "ordered"
 
     # -------------------------------------------------------------------------------- timing (bench.py)
     def enable_timing(self, on: bool = True):
@@ -79,6 +81,39 @@ class Comm:
             with self._timed("stats_allreduce"):
                 dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
         return t
+
+    def grad_sum_(self, t: torch.Tensor):
+        """SUM all-reduce of a gradient slice, timed as gradient traffic (the overlapped schedule's remaining range)."""
+        if self.world_size > 1:
+            with self._timed("grad_allreduce"):
+                if self.ordered:
+                    self._ordered_sum_(t)
+                else:
+                    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return t
+
+    # ordered gradient reduction (MAT_DCML_ALLREDUCE=ordered): all-gather, then a rank-order sum on every rank.  A ring
+    # all-reduce sums each element in an order set by the message's chunking, so the same gradient all-reduced as one
+    # buffer or as two slices can differ in the last bit at >= 3 ranks; the ordered sum does not depend on how the
+    # buffer is split (the overlapped schedule is then bitwise the blocking one) and is identical on every rank
+    ordered = False
+
+    def _gather(self, t, async_op=False):
+        out = torch.empty(self.world_size * t.numel(), dtype=t.dtype, device=t.device)
+        w = dist.all_gather_into_tensor(out, t.contiguous().view(-1), group=self.group, async_op=async_op)
+        return out.view(self.world_size, -1), w
+
+    @staticmethod
+    def _fold(t, out):
+        acc = out[0].clone()
+        for r in range(1, out.shape[0]):
+            acc += out[r]
+        t.copy_(acc.view_as(t))
+        return t
+
+    def _ordered_sum_(self, t):
+        out, _ = self._gather(t)
+        return self._fold(t, out)
 
     def all_reduce_max_(self, t: torch.Tensor):
         if self.world_size > 1:
@@ -138,7 +173,10 @@ class Comm:
         with self._timed("grad_allreduce"):
             if self.oneshot is not None and buf.numel() == self.oneshot.n and buf.is_cuda:
                 return self.oneshot(buf, scale=1.0 / self.world_size)
-            dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
+            if self.ordered:
+                self._ordered_sum_(buf)
+            else:
+                dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
             return buf.mul_(1.0 / self.world_size)
 
     def maybe_enable_oneshot(self, n: int, mode: str | None = None):
@@ -148,6 +186,9 @@ class Comm:
         mode = (mode or os.environ.get("MAT_DCML_ALLREDUCE", "rccl")).lower()
         if self.world_size == 1:
             return "none"
+        if mode == "ordered":
+            self.ordered = True
+            return "ordered"
         if mode not in ("oneshot", "auto") or self.device.type != "cuda":
             return self.backend
         if self.oneshot is not None and self.oneshot.n == n:
@@ -166,12 +207,22 @@ class Comm:
         if self.oneshot is not None:
             self.oneshot.poll()
 
-    def all_reduce_sum_async(self, t: torch.Tensor):
+    def all_reduce_sum_async(self, t: torch.Tensor, grad=False):
         """Start a SUM all-reduce of ``t``; returns a work handle (``wait()`` makes the current stream wait) or None.
         With the nccl (RCCL) backend the collective runs on the process group's own HIP stream, ordered after the
-        work already queued on the current stream, so kernels launched afterwards overlap it."""
+        work already queued on the current stream, so kernels launched afterwards overlap it.  ``grad``: a gradient
+        slice (the ordered reduction applies, folded into ``t`` at ``wait()``)."""
         if self.world_size == 1:
             return None
+        if grad and self.ordered:
+            out, w = self._gather(t, async_op=True)
+            fold = self._fold
+
+            class _Work:
+                def wait(self_):
+                    w.wait()
+                    fold(t, out)
+            return _Work()
         return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     def describe(self) -> dict:

@@ -165,11 +165,16 @@ def frontier_verdict(ct: float, pay: float, pts) -> dict:
     * ``beyond``: the point lies strictly below the lower-left convex hull of the heuristic points in the
       (ct, payment) plane, i.e. no mixture of heuristic settings reaches it — a policy that merely moves along the
       heuristic's trade-off lies ON the curve, not beyond it;
-    * ``margin``: payment of the frontier at this ct minus the policy's payment (> 0 = beyond), None outside the
-      frontier's ct range."""
+    * ``margin``: payment of the frontier at this ct minus the policy's payment (> 0 = beyond); slower than every
+      heuristic point: the cheapest point's payment minus the policy's; None when the policy is FASTER than every
+      heuristic point (the frontier is not measured there);
+    * ``outside``: "faster" in that last case — then ``beyond`` is None (no verdict: nothing is extrapolated) and
+      ``dominates`` lists the heuristic ratios the policy beats on both objectives (a measured comparison).
+    Only a numeric positive margin counts as beyond (an unmeasured extrapolation is not evidence)."""
     import numpy as np
     P = sorted((float(c), float(p), r) for r, (c, p) in pts.items())
     dominated = [r for c, p, r in P if c <= ct and p <= pay]
+    dominates = [r for c, p, r in P if ct < c and pay < p]
     # lower convex hull (monotone chain), ct ascending
     hull = []
     for c, p, _ in P:
@@ -177,13 +182,26 @@ def frontier_verdict(ct: float, pay: float, pts) -> dict:
             hull.pop()
         hull.append((c, p))
     xs, ys = np.array([h[0] for h in hull]), np.array([h[1] for h in hull])
-    margin = None
+    margin, outside = None, None
     if xs[0] <= ct <= xs[-1]:
         margin = float(np.interp(ct, xs, ys) - pay)
     elif ct > xs[-1]:
         margin = float(ys[-1] - pay)   # slower than every heuristic point: beyond only if cheaper than the cheapest
-    beyond = (not dominated) and (margin is None or margin > 0)
-    return {"dominated_by": dominated, "beyond": bool(beyond), "margin": None if margin is None else round(margin, 4)}
+    else:
+        outside = "faster"
+    beyond = None if margin is None else bool((not dominated) and margin > 0)
+    return {"dominated_by": dominated, "dominates": dominates, "beyond": beyond, "outside": outside,
+            "margin": None if margin is None else round(margin, 4)}
+
+
+def frontier_counts(verdicts) -> dict:
+    """Summary of ``frontier_verdict`` results: beyond (numeric positive margin), on / behind the frontier, and the
+    points faster than every heuristic setting (no verdict) with how many of those still dominate a heuristic point."""
+    return {"beyond": sum(v["beyond"] is True for v in verdicts),
+            "not_beyond": sum(v["beyond"] is False for v in verdicts),
+            "faster_than_frontier": sum(v["outside"] == "faster" for v in verdicts),
+            "faster_and_dominating": sum(v["outside"] == "faster" and bool(v["dominates"]) for v in verdicts),
+            "points": len(verdicts)}
 
 
 def eval_report(policy, cfg: DCMLConfig, device, samples=(1,) + HELDOUT_SAMPLES, frontier: bool = True, **kw):

@@ -32,7 +32,7 @@ def main():
     from mat_dcml_amd.config import get_config, parse_args
     from mat_dcml_amd.envs.dcml.config import DCMLConfig
     from mat_dcml_amd.envs.dcml.spaces import dcml_action_spaces
-    from mat_dcml_amd.runner.benchmark import eval_report
+    from mat_dcml_amd.runner.benchmark import eval_report, frontier_counts
     dev = torch.device("cuda:0" if torch.cuda.is_available() else "cpu")
     args = parse_args(["--env_name", "DCML", "--n_workers", str(a.n_workers)], get_config(), warn=False)
     cfg = DCMLConfig(n_workers=a.n_workers)
@@ -51,14 +51,16 @@ def main():
         h = rep["heldout"]
         held_rew = float(np.mean([np.mean(rep["per_sample"][s]["policy"]["reward"]) for s in h["samples"]]))
         s1 = rep["per_sample"][1]
-        beyond = sum(f["beyond"] for f in rep["frontier"])
+        fc = frontier_counts(rep["frontier"])
+        beyond = fc["beyond"]
         ent = {"heldout_both": sum(h["both_wins_per_sample"]), "heldout_ct": sum(h["ct_wins_per_sample"]),
                "heldout_payment": sum(h["payment_wins_per_sample"]), "heldout_reward": held_rew,
                "sample1": {k: s1[k] for k in ("ct_wins", "payment_wins", "both_wins")}, "frontier_beyond": beyond,
-               "report": rep}
+               "frontier_counts": fc, "report": rep}
         out["ckpts"][ck] = ent
         print(f"| {ck} | {ent['heldout_both']} | {ent['heldout_ct']} / {ent['heldout_payment']} | {held_rew:.2f} | "
-              f"{s1['ct_wins']} / {s1['payment_wins']} / {s1['both_wins']} | {beyond} |", flush=True)
+              f"{s1['ct_wins']} / {s1['payment_wins']} / {s1['both_wins']} | {beyond} "
+              f"(+{fc['faster_than_frontier']} faster than every setting) |", flush=True)
     best = max(out["ckpts"], key=lambda k: (out["ckpts"][k]["heldout_both"], out["ckpts"][k]["heldout_reward"]))
     out["selected_on_heldout"] = best
     b = out["ckpts"][best]

@@ -39,3 +39,26 @@ def perf_record(name, value, bound, unit="us"):
             f.write(json.dumps(line) + "\n")
     except OSError:
         pass
+
+
+# Performance guards: a bound is 1.25x a recorded measurement, and the measured value is the MEDIAN of
+# several timed windows, so the run-to-run jitter of a shared or throttled MI355X does not fail a guard.
+GUARD_MARGIN = 1.25
+
+
+def median_us(fn, iters=10, windows=5, warm=3):
+    """Median over ``windows`` hipEvent windows of ``iters`` back-to-back calls: microseconds per call."""
+    import torch
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(windows):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        ts.append(s.elapsed_time(e) / iters * 1e3)
+    return sorted(ts)[len(ts) // 2]

@@ -79,8 +79,16 @@ def test_frontier_verdict_geometry():
     assert below["beyond"] and abs(below["margin"] - 1.0) < 1e-9
     dom = frontier_verdict(2.5, 6.5, pts)
     assert dom["dominated_by"] == [0.7] and not dom["beyond"]
-    fast = frontier_verdict(0.9, 12.0, pts)       # faster than every heuristic setting: nothing dominates it
-    assert fast["beyond"] and fast["margin"] is None
+    fast = frontier_verdict(0.9, 12.0, pts)       # faster than every heuristic setting: no verdict
+    assert fast["beyond"] is None and fast["margin"] is None and fast["outside"] == "faster"
+    assert fast["dominates"] == []
+    fast_cheap = frontier_verdict(0.9, 9.0, pts)  # faster AND cheaper than the fastest setting: a measured dominance
+    assert fast_cheap["beyond"] is None and fast_cheap["dominates"] == [0.5]
+    slow = frontier_verdict(5.0, 4.0, pts)        # slower than every setting: beyond only if cheaper than the cheapest
+    assert slow["beyond"] and abs(slow["margin"] - 1.0) < 1e-9
+    from mat_dcml_amd.runner.benchmark import frontier_counts
+    c = frontier_counts([on, below, dom, fast, fast_cheap, slow])
+    assert c == {"beyond": 2, "not_beyond": 2, "faster_than_frontier": 2, "faster_and_dominating": 1, "points": 6}
 
 
 def test_eval_report_heldout_and_frontier_cpu():

@@ -100,3 +100,23 @@ def test_concurrent_ranks_rebuild_stale_library_once(tmp_path):
     assert sum(o.count("rebuilding") for o in outs) == 1, outs
     links = [l for l in log.read_text().splitlines() if ".so" in l]
     assert len(links) == 1, log.read_text()
+
+
+def test_missing_lib_dir_reaches_the_build(tmp_path):
+    """on a fresh checkout nothing under ``_lib/`` exists; ``lib()`` must create the directory for its
+    build lock and get as far as the build (here a failing stand-in hipcc) instead of dying on the lock file."""
+    pkg = tmp_path / "mat_dcml_amd"
+    shutil.copytree(os.path.join(ROOT, "mat_dcml_amd"), pkg, ignore=shutil.ignore_patterns("__pycache__", "_lib"))
+    fake = tmp_path / "hipcc"
+    fake.write_text("#!/bin/sh\necho fake-hipcc-called >&2\nexit 1\n")
+    fake.chmod(0o755)
+    code = ("from mat_dcml_amd.ops import kernels\n"
+            "try:\n    kernels.lib()\nexcept FileNotFoundError as e:\n    print('LOCKFAIL', e)\n"
+            "except Exception as e:\n    print('BUILDFAIL', type(e).__name__)\nelse:\n    print('LOADED')\n")
+    env = dict(os.environ, HIPCC=str(fake), PYTHONPATH=str(tmp_path))
+    env.pop("MAT_DCML_LIBNAME", None)
+    r = subprocess.run([sys.executable, "-c", code], cwd=str(tmp_path), env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert "LOCKFAIL" not in r.stdout, r.stdout + r.stderr
+    assert (pkg / "_lib").is_dir()
+    assert "rebuilding" in r.stdout and "BUILDFAIL" in r.stdout, r.stdout + r.stderr

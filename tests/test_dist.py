@@ -331,3 +331,69 @@ def test_rollout_is_identical_at_one_and_two_ranks_gpu(gpu):
     two = spawn(_rollout_gpu_e8, world=2, gpu=True)
     assert one["fused"] and two[0]["fused"]
     _assert_rank_split_equal(one, two)
+
+
+# ------------------------------------------------------------------------------------------ overlapped gradient all-reduce
+def _overlap_case(comm, overlap, gpu_fused=False):
+    """One full PPO iteration with (overlap=True) the decoder's gradient slice all-reduced asynchronously under the
+    encoder backward, or (False) the single blocking all-reduce of the flat buffer; the parameters afterwards.
+    At >= 3 ranks the gradients go through the ordered reduction (all-gather + rank-order sum): a ring all-reduce's
+    per-element summation order depends on the message's chunking, so one buffer and two slices can differ in the
+    last bit (measured: 1.2e-7 at 4 gloo ranks), while the ordered sum cannot."""
+    from mat_dcml_amd.config import get_config, parse_args
+    from mat_dcml_amd.runner.dcml_runner import DCMLRunner
+    comm.ordered = comm.world_size > 2
+    argv = ["--n_workers", "32" if gpu_fused else "4", "--n_rollout_threads", "4", "--episode_length", "4",
+            "--ppo_epoch", "2", "--num_mini_batch", "2", "--use_valuenorm", "--env_name", "DCML", "--seed", "5"]
+    if overlap:
+        argv.append("--grad_overlap")
+    args = parse_args(argv, get_config(), warn=False)
+    r = DCMLRunner({"all_args": args, "device": comm.device, "run_dir": None, "comm": comm})
+    assert r.trainer.grad_overlap == overlap
+    assert bool(r.trainer.fused) == gpu_fused
+    if overlap:
+        assert r.trainer._overlap_split() is not None   # the decoder's gradients are one contiguous slice
+    r.warmup()
+    r.train_iteration()
+    flat = torch.cat([p.detach().reshape(-1) for p in r.policy.transformer.parameters()]).cpu().numpy().copy()
+    return flat, r.trainer.collectives
+
+
+def _overlap_on(comm):
+    return _overlap_case(comm, True)
+
+
+def _overlap_off(comm):
+    return _overlap_case(comm, False)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_grad_overlap_gives_identical_parameters(world):
+    """``--grad_overlap`` (decoder slice all-reduced while the encoder backward runs, then the rest)
+    leaves every rank with parameters torch.equal to the single blocking all-reduce after a full PPO iteration
+    (gloo, CPU ranks: the eager path's two-phase backward)."""
+    import numpy as np
+    on, off = spawn(_overlap_on, world=world), spawn(_overlap_off, world=world)
+    for r in range(world):
+        assert np.array_equal(on[r][0], off[r][0]), (r, np.abs(on[r][0] - off[r][0]).max())
+        assert np.array_equal(on[r][0], on[0][0])
+    # 2 epochs x (1 statistics + 2 minibatches x (2 overlapped collectives)) vs x 1
+    assert on[0][1] == 2 * (1 + 2 * 2) and off[0][1] == 2 * (1 + 2)
+
+
+def _overlap_on_gpu(comm):
+    return _overlap_case(comm, True, gpu_fused=True)
+
+
+def _overlap_off_gpu(comm):
+    return _overlap_case(comm, False, gpu_fused=True)
+
+
+@pytest.mark.gpu
+def test_grad_overlap_fused_gpu_identical_parameters(gpu):
+    """The fused trainer's overlapped schedule (decoder slice of the private workspace reduced right after dec_bwd
+    and all-reduced under enc_bwd) at 2 ranks sharing the GPU: parameters equal to the blocking path's."""
+    import numpy as np
+    on, off = spawn(_overlap_on_gpu, world=2, gpu=True), spawn(_overlap_off_gpu, world=2, gpu=True)
+    for r in range(2):
+        assert np.array_equal(on[r][0], off[r][0]), (r, np.abs(on[r][0] - off[r][0]).max())

@@ -5,11 +5,17 @@ bitwise-equal outputs — a missing barrier or an LDS race shows up as run-to-ru
 * persistent decode kernel (stochastic and deterministic, stride 1 and stride blocks): bitwise equal actions /
   log-probs for the same inputs and draws, also with other work interleaved on the stream;
 * fused training forward (values, log-probs, entropies): bitwise equal;
-* fused backward: weight gradients are accumulated with fp32 atomics into an 8-copy workspace, whose summation
-  order may differ between runs — required to agree to fp32 rounding (relative 1e-5), and the max deviation is
-  printed;
-* the whole fused PPO iteration (rollout + 2 epochs): parameters after two identical runs agree to 1e-5.
+* fused backward called through autograd (no trainer workspace): weight gradients are accumulated with fp32 atomics
+  straight into ``.grad``, whose summation order may differ between runs — required to agree to fp32 rounding
+  (relative 1e-5), and the max deviation is printed;
+* the trainer's fused PPO update (round 6, reference ``--cuda_deterministic``, DCML_MAT_Train.py:108-110): private
+  per-workgroup gradient copies, 2^-32 fixed-point vector accumulators and fixed-order reductions make two whole PPO
+  iterations (rollout + 2 epochs, the fused reduce / clip / Adam / repack launch included) BITWISE identical —
+  parameters, Adam moments and the optimizer scratch (grad norm, skipped-step count) — with the fused and the unfused
+  update alike.
 """
+import os
+
 import pytest
 import torch
 
@@ -85,21 +91,47 @@ def test_fused_training_repeatable(gpu):
     print(f"max relative run-to-run gradient deviation (fp32 atomic order): {worst:.2e}")
 
 
-def test_fused_ppo_iteration_repeatable(gpu):
+def _ppo_run(gpu, iters=2, fused_update=True):
     from mat_dcml_amd.config import get_config, parse_args
     from mat_dcml_amd.parallel.comm import Comm
     from mat_dcml_amd.runner.dcml_runner import DCMLRunner
-    flats = []
-    for _ in range(2):
+    old = os.environ.get("MAT_DCML_FUSED_UPDATE")
+    os.environ["MAT_DCML_FUSED_UPDATE"] = "1" if fused_update else "0"
+    try:
         args = parse_args(["--n_workers", "32", "--n_rollout_threads", "32", "--episode_length", "10", "--ppo_epoch",
                            "2", "--num_mini_batch", "2", "--use_valuenorm", "--env_name", "DCML", "--seed", "3"],
                           get_config(), warn=False)
         r = DCMLRunner({"all_args": args, "device": gpu, "run_dir": None, "comm": Comm(device=gpu)})
-        assert r.trainer.fused
-        r.warmup()
+    finally:
+        if old is None:
+            os.environ.pop("MAT_DCML_FUSED_UPDATE", None)
+        else:
+            os.environ["MAT_DCML_FUSED_UPDATE"] = old
+    tr = r.trainer
+    assert tr.fused and tr.deterministic and tr._upd_fused == fused_update
+    r.warmup()
+    for _ in range(iters):
         r.train_iteration()
-        torch.cuda.synchronize()
-        flats.append(torch.cat([p.detach().reshape(-1) for p in r.policy.transformer.parameters()]).double())
-    d = ((flats[0] - flats[1]).norm() / flats[0].norm()).item()
-    print(f"run-to-run parameter deviation after one PPO iteration: {d:.2e}")
-    assert d < 1e-5
+    torch.cuda.synchronize()
+    opt = r.policy.optimizer
+    return {"params": torch.cat([p.detach().reshape(-1) for p in r.policy.transformer.parameters()]),
+            "exp_avg": opt.m.clone(), "exp_avg_sq": opt.v.clone(), "scratch": opt.scratch[:4].clone()}
+
+
+def test_fused_ppo_iteration_bitwise_repeatable(gpu):
+    a, b = _ppo_run(gpu), _ppo_run(gpu)
+    for k in a:
+        assert torch.equal(a[k], b[k]), (k, (a[k] - b[k]).abs().max().item())
+    print("two fused PPO iterations x 2 runs: parameters, Adam moments and optimizer scratch bitwise equal")
+
+
+def test_fused_update_matches_unfused_update(gpu):
+    """The one-launch reduce / clip / Adam / repack (csrc/ppo.hip update_fused_kernel) against the separate
+    grad_reduce_priv + adam_step + pack_weights launches: the same norm partials in the same order, so the runs agree
+    to the last bits of the Adam arithmetic (the two kernels' FMA contraction may differ)."""
+    a, b = _ppo_run(gpu, fused_update=True), _ppo_run(gpu, fused_update=False)
+    assert torch.equal(a["scratch"][1:3], b["scratch"][1:3]) or \
+        abs(float(a["scratch"][1]) - float(b["scratch"][1])) <= 1e-6 * float(b["scratch"][1])
+    d = ((a["params"] - b["params"]).norm() / b["params"].norm()).item()
+    print(f"fused vs unfused update: relative parameter difference {d:.2e}")
+    assert d < 1e-6, d

@@ -376,14 +376,14 @@ def test_mat_dec_runner_trains_through_the_hybrid_path(gpu):
     assert r.policy.transformer._mdl_train_state[0].ctx is None   # every fused encoder forward got its backward
 
 
-# 1.10 x the round-5 measurement taken exactly this way (profiles/r5_final/perf_guards.jsonl)
-TRAIN_KERNELS_BOUND_MS = 1.26   # 1.149 ms measured (round 5, backward stagger)
+# 1.25 x the round-5 measurement taken exactly this way (median of 20 steps; profiles/r5_final/perf_guards.jsonl)
+TRAIN_KERNELS_BOUND_MS = 1.44   # 1.149 ms measured (round 5, backward stagger)
 
 
 def test_training_kernels_time_bound(gpu):
     """The four fused training kernels at the bench minibatch (3,200 sequences x 33 agents, n_block 2): hipEvent time
     per minibatch (printed; launch gaps included: 1.149 ms measured this way in round 5, 0.99 ms of kernel time under
-    rocprofv3) under a regression bound of 1.10x."""
+    rocprofv3) under a regression bound of 1.25x (median of 20 steps)."""
     B, L = 3200, 33
     m = make(L, gpu, seed=0, scale=0.05)
     obs = torch.rand(B, L, 7, device=gpu)

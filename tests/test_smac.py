@@ -167,3 +167,23 @@ def test_sc2_restart_keeps_episode_counters():
     g.reset()
     o, s, r, d, info, a = g.step([0, 1, 2])
     assert g.env is e and e.relaunched and info[0]["battles_won"] == 7 and info[0]["restarts"] == 1
+
+
+def test_sc2_rebuild_reports_live_win_counted():
+    """on the rebuild path the error step's ``won`` is the value the LIVE env object had when the error
+    hit (StarCraft2_Env.py:517-524 reads it from the env that is still there), not the fresh object's False."""
+    from mat_dcml_amd.envs.smac.adapter import SC2Game
+    made = []
+
+    def make_env():
+        e = _FlakySC2(fail_on=(2,) if not made else ())
+        e.battles_won, e.battles_game, e.timeouts, e.win_counted = 0, 0, 0, False
+        made.append(e)
+        return e
+    g = SC2Game(make_env, errors=(ConnectionError,))
+    g.reset()
+    g.step([0, 1, 2])
+    made[0].win_counted = True                        # the battle was already won when the protocol error hit
+    o, s, r, d, info, a = g.step([0, 1, 2])
+    assert len(made) == 2 and made[1].win_counted is False
+    assert all(i["won"] is True for i in info)
