@@ -212,8 +212,8 @@ class MATTrainer:
         enc, dec, _ = mat_train._state(m, mb["obs"].device)
         tm = self.timers
         with tm("train_fwd"):
-            v, rep = enc.forward(mb["obs"], save=True)
-            logp, ent = dec.forward(rep, mb["actions"], mb["ava"], save=True)
+            v, rep = enc.forward(mb["obs"], save=True, idx=mb.get("idx"))
+            logp, ent = dec.forward(rep, mb["actions"], mb["ava"], save=True, idx=mb.get("idx"))
         buf = self.comm._flat.buf
         if self._direct_grads:
             buf.zero_()
@@ -242,7 +242,7 @@ class MATTrainer:
         # norm launch); under data parallelism the norm is the all-reduced gradient's, so the Adam step computes it
         fuse_norm = self.comm.world_size == 1 and not self.poison
         if fuse_norm and self._upd_fused:
-            # round 6: reduction + clip + Adam + weight repack in ONE cooperative launch (csrc/ppo.hip)
+            # round 6: workspace reduction, then clip + Adam + weight repack: two launches (csrc/ppo.hip)
             mat_train.update_fused(m, pol.optimizer, accumulate=self._direct_grads)
             dec.ctx = None
             enc.ctx = None
@@ -377,12 +377,14 @@ class MATTrainer:
                 if native and len(idx_list) == 1 and getattr(self, "inplace_single_minibatch", True):
                     # one minibatch = the whole batch: the permutation only reorders the rows the loss averages
                     # over, so the buffer's rows are used in place (SMAC: no 2 x 445 MB gather copy per epoch);
-                    # only the advantages are standardised (one gather launch over the identity rows)
-                    n = adv_f.shape[0]
-                    if getattr(self, "_ident", None) is None or self._ident.numel() != n:
-                        self._ident = torch.arange(n, device=adv_f.device, dtype=torch.int64)
-                    mb = dict(src)
-                    mb["adv"] = kernels.gather_rows({"adv": adv_f}, self._ident, sums, ("adv",))["adv"]
+                    # the loss kernel standardises the advantages itself (adv_sums)
+                    mb = dict(src, idx=None, adv_sums=sums)
+                elif native and self.fused and os.environ.get("MAT_DCML_MB_INDEX", "gather") == "kernel":
+                    # opt-in (round 6): no gather — the training kernels and the loss read the buffer's rows through
+                    # the epoch permutation (sequence index) and standardise the advantages in-kernel.  Measured at
+                    # the bench shape it is ~0.5 % slower than the gather (the indexed reads cost the four training
+                    # kernels more than the 2-launch gather costs), so the gather stays the default
+                    mb = dict(src, idx=idx, adv_sums=sums)
                 elif native:
                     mb = kernels.gather_rows(src, idx, sums, ("adv",))
                 else:

@@ -14,7 +14,7 @@ namespace {
 // token of row i: 0 = start, 1 + a = one-hot of the previous agent's (discrete) action   (transformer_act.py:103-111)
 __device__ __forceinline__ int dec_token_ct(const DecP& p, int tok, int i) {
   if (i == 0) return 0;
-  int a = (int)p.act[tok - 1];
+  int a = (int)p.act[src_tok(p.sidx, (size_t)tok, p.L) - 1];   // the previous agent of the same sequence
   a = a < 0 ? 0 : (a >= p.A ? p.A - 1 : a);
   return 1 + a;
 }
@@ -30,7 +30,7 @@ __device__ __forceinline__ CT dec_embed_pre_ct(const DecP& p, int rt, int& tokid
   if (CONT) {
     tokid = -1;
     const bool first = !ok || row % c.L == 0;
-    const float* prev = p.act + (size_t)(c.tok0 + (first ? 0 : row - 1)) * p.A;
+    const float* prev = p.act + (first ? 0 : src_tok(p.sidx, (size_t)(c.tok0 + row), c.L) - 1) * p.A;
     pre = ld_vec(p.ba, lane);
     for (int k = 0; k < p.A; ++k) {
       const float x = first ? 0.f : prev[k];
@@ -343,7 +343,7 @@ __device__ __forceinline__ void head_logits_ct(const DecP& p, const HeadW<MA>& W
   }
 }
 
-// availability bits of this lane's logit slots (a = 16ma + 4g + r): bit 4ma + r set = masked
+// availability bits of this lane's logit slots (a = 16ma + 4g + r): bit 4ma + r set = masked (tok: input row)
 template <int MA>
 __device__ __forceinline__ unsigned slot_mask(const DecP& p, size_t tok, int lane) {
   if (!p.ava) return 0u;
@@ -424,9 +424,9 @@ __device__ __forceinline__ void head_fwd_ct(const DecP& p, const CT* xr, bool sa
     if (rt < c.NT) {
       const int row = rt * 16 + (lane & 15);
       const bool ok = row < c.NR;
-      const size_t tok = (size_t)(c.tok0 + (ok ? row : 0));
-      const unsigned am = CONT ? 0u : slot_mask<MA>(p, tok, lane);
-      const float actf = CONT ? 0.f : p.act[tok];
+      const size_t tok = (size_t)(c.tok0 + (ok ? row : 0)), stok = src_tok(p.sidx, tok, c.L);
+      const unsigned am = CONT ? 0u : slot_mask<MA>(p, stok, lane);
+      const float actf = CONT ? 0.f : p.act[stok];
       const CTr x = ct_pack(xr[k]);
       if (save) st_g(p.sv_head, c.tok0, rt, c.NR, x, lane);
       CT hh = bh, xh, n;
@@ -451,7 +451,7 @@ __device__ __forceinline__ void head_fwd_ct(const DecP& p, const CT* xr, bool sa
           for (int r = 0; r < 4; ++r) {
             const int a = 16 * ma + 4 * g + r;
             if (ok && a < p.A) {
-              const float sd = head_sd(p, a), z = (p.act[tok * p.A + a] - L[ma][r]) / sd;
+              const float sd = head_sd(p, a), z = (p.act[stok * p.A + a] - L[ma][r]) / sd;
               p.logp[tok * p.A + a] = -0.5f * z * z - __logf(sd) - HALF_LOG_2PI;
               p.ent[tok * p.A + a] = 0.5f + HALF_LOG_2PI + __logf(sd);
             }
@@ -535,9 +535,9 @@ __device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c)
       if (rt < c.NT) {
         const int row = rt * 16 + (lane & 15);
         const bool ok = row < c.NR;
-        const size_t tok = (size_t)(c.tok0 + (ok ? row : 0));
-        const unsigned am = CONT ? 0u : slot_mask<MA>(p, tok, lane);
-        const float actf = CONT ? 0.f : p.act[tok];
+        const size_t tok = (size_t)(c.tok0 + (ok ? row : 0)), stok = src_tok(p.sidx, tok, c.L);
+        const unsigned am = CONT ? 0u : slot_mask<MA>(p, stok, lane);
+        const float actf = CONT ? 0.f : p.act[stok];
         const float dlp = (ok && !CONT) ? p.dlogp[tok] : 0.f, den = (ok && !CONT) ? p.dent[tok] : 0.f;
         const CT xh = ct_unpack(hxh[k]), ggp = ct_unpack(hgp[k]);
         const float rs = hrs[k];
@@ -560,7 +560,7 @@ __device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c)
             for (int r = 0; r < 4; ++r) {
               const int a = 16 * ma + 4 * g + r;
               if (ok && a < p.A) {
-                const float sd = head_sd(p, a), diff = p.act[tok * p.A + a] - L[ma][r];
+                const float sd = head_sd(p, a), diff = p.act[stok * p.A + a] - L[ma][r];
                 const float dl = p.dlogp[tok * p.A + a], de = p.dent[tok * p.A + a];
                 Z[ma][r] = dl * diff / (sd * sd);
                 const float dsd = dl * (diff * diff / (sd * sd * sd) - 1.f / sd) + de / sd;
@@ -640,11 +640,11 @@ __device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c)
       for (int r = 0; r < 4; ++r) {
         const float t = group_sum<16>(dlsv[ma][r]);
         const int a = 16 * ma + 4 * g + r;
-        if ((lane & 15) == 0 && a < p.A && p.d_log_std) vacc_add(c.g(p.d_log_std), 4, a, t, c);
+        if ((lane & 15) == 0 && a < p.A && p.d_log_std) vacc_add(c.g(p.d_log_std), 4, a, t, c, p.A);
       }
   } else {
     const float t = wave_sum(dls);
-    if (lane == 0 && p.d_log_std && p.n_disc < p.L) vacc_add(c.g(p.d_log_std), 4, p.A - 1, t, c);
+    if (lane == 0 && p.d_log_std && p.n_disc < p.L) vacc_add(c.g(p.d_log_std), 4, p.A - 1, t, c, p.A);
   }
   __syncthreads();
   CP_MARK(1);
@@ -827,7 +827,7 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
         if (ok) {   // EMB[k][f] += d pre_f * a_prev_k (k < A), EMB[A][f] += d pre_f (bias)
           const int row = rt * 16 + (lane & 15);
           const bool first = row % c.L == 0;
-          const float* prev = p.act + (size_t)(c.tok0 + (first ? 0 : row - 1)) * p.A;
+          const float* prev = p.act + (first ? 0 : src_tok(p.sidx, (size_t)(c.tok0 + row), c.L) - 1) * p.A;
 #pragma unroll
           for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
@@ -848,7 +848,7 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
       const int t = i / 64, col = i % 64;
       float* d = t < p.A ? (p.d_wa ? c.g(p.d_wa) + col * p.A + t : nullptr) : (p.d_ba ? c.g(p.d_ba) + col : nullptr);
       if (!d) continue;
-      if (c.gm.priv) *d = c.gm.first ? EMB[i] : *d + EMB[i];   // this thread owns the element in every chunk
+      if (c.gm.priv) priv_st1(d, EMB[i], (c.gm.first || !PRIV_LOADS) ? 0.f : priv_ld1(d), c.gm.first);   // owner thread
       else atomicAdd(d, EMB[i]);
     }
   }

@@ -20,7 +20,7 @@ __device__ __forceinline__ void obs_ln(const EncP& p, int rt, const Ctx& c, floa
   const int lane = c.lane, g = lane >> 4, od = p.od;
   const int row = rt * 16 + (lane & 15);
   const bool ok = row < c.NR;
-  const float* src = p.obs + (size_t)(c.tok0 + (ok ? row : 0)) * od;
+  const float* src = p.obs + src_tok(p.sidx, (size_t)(c.tok0 + (ok ? row : 0)), c.L) * od;
   float o[4];
   bool in[4];
 #pragma unroll
@@ -288,8 +288,8 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
     if (p.d_bh2) {   // lanes g = 0 carry each token once
       const float s0 = group_sum<16>(sdv0), s1 = group_sum<16>(sdv1);
       if (lane == 0) {
-        vacc_add(c.g(p.d_bh2), 4, 0, s0, c);
-        if (p.n_obj > 1) vacc_add(c.g(p.d_bh2), 4, 1, s1, c);
+        vacc_add(c.g(p.d_bh2), 4, 0, s0, c, p.n_obj);
+        if (p.n_obj > 1) vacc_add(c.g(p.d_bh2), 4, 1, s1, c, p.n_obj);
       }
     }
     __syncthreads();
@@ -371,8 +371,8 @@ __device__ __forceinline__ void enc_bwd_tile(const EncP& p, const EncX& ex, char
       }
       const int dim = 4 * g + c16;
       if (c16 < 4 && dim < p.od) {
-        if (p.d_lno_g) vacc_add(c.g(p.d_lno_g), 8, dim, og, c);
-        if (p.d_lno_b) vacc_add(c.g(p.d_lno_b), 9, dim, ob, c);
+        if (p.d_lno_g) vacc_add(c.g(p.d_lno_g), 8, dim, og, c, p.od);
+        if (p.d_lno_b) vacc_add(c.g(p.d_lno_b), 9, dim, ob, c, p.od);
       }
       __syncthreads();
       wgrad_g(c.DA, c.XB, c.KP, c.g(p.d_we), p.od, 64, p.od, nullptr, c.wave, lane, c.gm);

@@ -91,6 +91,7 @@ struct EncP {
   float* d_bh2;                  // value-head bias gradient Σ dv (round-2 backward; null: summed by the caller)
   HSv hs, es;                    // value head, observation embedding (round 4)
   int g_mode;                    // 1: one PRIVATE workspace copy per workgroup, plain stores (GradMode below)
+  const long long* sidx;         // minibatch sequence -> rollout-buffer sequence of `obs` (null: obs is dense)
 };
 
 struct DecP {
@@ -128,7 +129,20 @@ struct DecP {
   float* d_ba;
   HSv hs;                // action head (round 4)
   int g_mode;            // 1: one PRIVATE workspace copy per workgroup, plain stores (GradMode below)
+  const long long* sidx; // minibatch sequence -> rollout-buffer sequence of `act` / `ava` (null: dense)
 };
+
+// Round 6: the training kernels read the minibatch's INPUTS (observations, stored actions, availability) straight
+// from the rollout buffer through the epoch permutation (sidx), so no gather copy precedes them; token tok of the
+// dense minibatch order (outputs, saved activations, loss gradients) reads input row src_tok(tok).
+#ifndef MDL_NO_SIDX
+#define MDL_NO_SIDX 0   // A/B: compile the sequence index out (dense inputs only)
+#endif
+__device__ __forceinline__ size_t src_tok(const long long* sidx, size_t tok, int L) {
+  if (MDL_NO_SIDX || !sidx) return tok;
+  const int t = (int)tok, s = t / L;   // a minibatch has < 2^31 tokens: 32-bit division (64-bit is emulated)
+  return (size_t)sidx[s] * (size_t)L + (size_t)(t - s * L);
+}
 
 // Weight-gradient flush modes (round 6).  ATOMIC (rounds 2-5): fp32 atomics into a workspace copy shared by
 // g_copies / G workgroups — the memory-side atomic unit (~1.35 TB/s chip-wide) made them cost ~121 us per
@@ -142,6 +156,12 @@ struct DecP {
 // Micro-benchmark (tests/native/wgrad_flush_bench.hip, 256 workgroups x 8 waves x 22 matrices x 3 chunks):
 // atomics 207 us + 6 us reduction, private copies 73 us + 17 us.
 struct GradMode { bool priv, first; };
+#ifndef MDL_NO_PRIV
+#define MDL_NO_PRIV 0   // A/B: compile the private-copy flush paths out (shared-copy atomics only)
+#endif
+#ifndef MDL_VACC_F32
+#define MDL_VACC_F32 0  // A/B: fp32 LDS atomics for the vector accumulators (order-dependent; rounds 2-5)
+#endif
 
 struct Ctx {
   int tid, lane, wave, L, nseq, NR, NT, NRP, KP, tok0;   // KP: rows [0, KP) = NR rounded up to 32 (<= NRP)
@@ -275,7 +295,7 @@ __device__ __forceinline__ Ctx make_ctx(const PT& p, char* smem, int seq0, int n
   // spread the fp32 weight-gradient atomics over g_copies copies (blockIdx % 8 ~ the XCD the block runs on):
   // 8x fewer adders per address than every workgroup hitting the same 16 KB matrix
   c.gofs = p.g_copies > 0 ? (ptrdiff_t)p.g_delta + (ptrdiff_t)(blockIdx.x % p.g_copies) * (ptrdiff_t)p.g_stride : 0;
-  c.gm.priv = p.g_copies > 0 && p.g_mode == 1;   // private mode: the host sized g_copies >= gridDim.x
+  c.gm.priv = !MDL_NO_PRIV && p.g_copies > 0 && p.g_mode == 1;   // private mode: the host sized g_copies >= grid
   c.gm.first = first_chunk;
   const size_t bs = (size_t)p.NRP * 64;
   bf16_t* base = (bf16_t*)smem;
@@ -317,20 +337,31 @@ __device__ __forceinline__ void vacc_end(const PT& p, char* smem) {
   for (int i = threadIdx.x; i < VSLOTS * 64; i += NTHR) {
     float* d = P[i >> 6];
     if (!d || (i & 63) >= N[i >> 6]) continue;
-    const float v = bad ? __builtin_nanf("") : (float)(long long)V[i] * VFX_INV;
+    const float v = MDL_VACC_F32 ? *reinterpret_cast<const float*>(V + i)
+                                 : bad ? __builtin_nanf("") : (float)(long long)V[i] * VFX_INV;
     if (priv) d[i & 63] = v;
     else if (v != 0.f) atomicAdd(d + (i & 63), v);
   }
 }
-// add v to element idx (< 64) of the parameter-vector gradient dst (already offset to this block's gradient copy)
-__device__ __forceinline__ void vacc_add(float* dst, int slot, int idx, float v, const Ctx& c) {
+// add v to element idx (< len <= 64) of the parameter-vector gradient dst (already offset to this block's gradient
+// copy); len = the parameter's length (the flush writes [0, len) of the slot).  Every writer of a slot stores the same
+// pointer and length (plain LDS stores: an LDS atomic-max from 64 lanes onto one address serialised 64-fold).
+#ifndef MDL_VACC_NOCHECK
+#define MDL_VACC_NOCHECK 0   // A/B: no overflow / non-finite check on the fixed-point partials
+#endif
+__device__ __forceinline__ void vacc_add(float* dst, int slot, int idx, float v, const Ctx& c, int len = 64) {
   if (!dst) return;
-  const float s = v * VFX_SCALE;
-  if (!(fabsf(s) < VFX_MAX * VFX_SCALE)) *c.VOVF = 1;   // also catches NaN / inf
-  const long long q = fabsf(s) < VFX_MAX * VFX_SCALE ? (long long)__builtin_rintf(s) : 0ll;
-  atomicAdd(c.VACC + slot * 64 + idx, (unsigned long long)q);   // LDS integer atomic (ds_add_u64): order-free
-  atomicMax(c.VLEN + slot, idx + 1);
-  c.VPT[slot] = dst;                                           // every writer stores the same pointer
+  if constexpr (MDL_VACC_F32) {
+    atomicAdd(reinterpret_cast<float*>(c.VACC + slot * 64 + idx), v);
+  } else {
+    const float s = v * VFX_SCALE;
+    const bool in = fabsf(s) < VFX_MAX * VFX_SCALE;   // false for NaN / inf too
+    if (!MDL_VACC_NOCHECK && !in) *c.VOVF = 1;
+    const long long q = (MDL_VACC_NOCHECK || in) ? (long long)__builtin_rintf(s) : 0ll;
+    atomicAdd(c.VACC + slot * 64 + idx, (unsigned long long)q);   // LDS integer atomic (ds_add_u64): order-free
+  }
+  c.VLEN[slot] = len;
+  c.VPT[slot] = dst;
 }
 
 }  // namespace

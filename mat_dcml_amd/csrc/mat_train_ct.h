@@ -465,6 +465,52 @@ __device__ __forceinline__ void flush_rows2(const f32x4& acc0, const f32x4& acc1
     WATOM(dW + (16 * rb + 8 + 4 * s + r) * 64 + col, __builtin_bit_cast(float, (unsigned)q[1]));
   }
 }
+// Private-copy flush variants (A/B, MDL_PRIV_FLUSH): 0 = plain load + add + store after the first chunk; 1 = the same
+// with nontemporal loads / stores (the copies do not churn the L2 the saved activations stream through); 2 = the
+// first chunk stores (nontemporal), later chunks add with fp32 atomics — one writer per address and program order,
+// so still deterministic, and no load latency in the wave.
+#ifndef MDL_PRIV_FLUSH
+#define MDL_PRIV_FLUSH 0
+#endif
+__device__ __forceinline__ f32x4 priv_ld4(const f32x4* p) {
+  if constexpr (MDL_PRIV_FLUSH == 1) return __builtin_nontemporal_load(p);
+  return *p;
+}
+__device__ __forceinline__ float priv_ld1(const float* p) {
+  if constexpr (MDL_PRIV_FLUSH == 1) return __builtin_nontemporal_load(p);
+  return *p;
+}
+// v = this chunk's partial; old = the earlier chunks' (loaded, variants 0 / 1)
+__device__ __forceinline__ void priv_st4(f32x4* p, f32x4 v, f32x4 old, bool first) {
+  if constexpr (MDL_PRIV_FLUSH == 2) {
+    if (first) {
+      __builtin_nontemporal_store(v, p);
+    } else {
+      float* q = reinterpret_cast<float*>(p);
+      const float v0 = v[0], v1 = v[1], v2 = v[2], v3 = v[3];
+      atomicAdd(q, v0);
+      atomicAdd(q + 1, v1);
+      atomicAdd(q + 2, v2);
+      atomicAdd(q + 3, v3);
+    }
+  } else if constexpr (MDL_PRIV_FLUSH == 1) {
+    __builtin_nontemporal_store(v + old, p);
+  } else {
+    *p = v + old;
+  }
+}
+__device__ __forceinline__ void priv_st1(float* p, float v, float old, bool first) {
+  if constexpr (MDL_PRIV_FLUSH == 2) {
+    if (first) __builtin_nontemporal_store(v, p);
+    else atomicAdd(p, v);
+  } else if constexpr (MDL_PRIV_FLUSH == 1) {
+    __builtin_nontemporal_store(v + old, p);
+  } else {
+    *p = v + old;
+  }
+}
+constexpr bool PRIV_LOADS = MDL_PRIV_FLUSH != 2;   // variants that read the earlier chunks' partials
+
 // Private-copy position of a lane's accumulator j (an f32x4 over r) of a 64 x 64 weight gradient: FRAGMENT order
 // (wave, lane, j, r) with the 8-wave block mapping above (row 16 (w & 3) + 4 g + r, column 16 (2 (w >> 2) + j) + c);
 // csrc/ppo.hip grad_reduce_priv folds the copies and writes each element to its row-major place.
@@ -487,7 +533,8 @@ __device__ __forceinline__ void wgrad_g(const bf16_t* Y, const bf16_t* X, int KP
   const int nct = dW ? (ncols + 15) >> 4 : 0;
   if ((!db && wg_ct(wave, 0) >= nct) || 16 * rb >= nrows) return;
   const int g = lane >> 4, c16 = lane & 15;
-  const bool rmw = gm.priv && !gm.first;
+  gm.priv = gm.priv && !MDL_NO_PRIV;
+  const bool rmw = PRIV_LOADS && gm.priv && !gm.first;
   f32x4 old[NCT];
   float oldb = 0.f;
 #pragma unroll
@@ -497,10 +544,10 @@ __device__ __forceinline__ void wgrad_g(const bf16_t* Y, const bf16_t* X, int KP
     for (int r = 0; r < 4; ++r) {
       const int n = 16 * rb + 4 * g + r, k = 16 * ct + c16;
       const bool ok = rmw && dW && wg_has(wave, j) && ct < nct && n < nrows && k < ncols;
-      old[j][r] = ok ? dW[n * ld + k] : 0.f;
+      old[j][r] = ok ? priv_ld1(dW + n * ld + k) : 0.f;
     }
   }
-  if (rmw && db && c16 < 4 && 16 * rb + 4 * g + c16 < nrows) oldb = db[16 * rb + 4 * g + c16];
+  if (rmw && db && c16 < 4 && 16 * rb + 4 * g + c16 < nrows) oldb = priv_ld1(db + 16 * rb + 4 * g + c16);
   f32x4 acc[NCT];
 #pragma unroll
   for (int j = 0; j < NCT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -525,7 +572,7 @@ __device__ __forceinline__ void wgrad_g(const bf16_t* Y, const bf16_t* X, int KP
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int n = 16 * rb + 4 * g + r, k = 16 * ct + c16;
-        if (wg_has(wave, j) && ct < nct && n < nrows && k < ncols) dW[n * ld + k] = acc[j][r] + old[j][r];
+        if (wg_has(wave, j) && ct < nct && n < nrows && k < ncols) priv_st1(dW + n * ld + k, acc[j][r], old[j][r], gm.first);
       }
     }
   } else if (dW && WG_ROWS2 && ld == 64 && nrows == 64 && ncols == 64) {
@@ -546,7 +593,7 @@ __device__ __forceinline__ void wgrad_g(const bf16_t* Y, const bf16_t* X, int KP
     const float v = c16 == 0 ? accb[0] : c16 == 1 ? accb[1] : c16 == 2 ? accb[2] : accb[3];
     const int n = 16 * rb + 4 * g + c16;
     if (n < nrows) {
-      if (gm.priv) db[n] = v + oldb;
+      if (gm.priv) priv_st1(db + n, v, oldb, gm.first);
       else atomicAdd(db + n, v);
     }
   }
@@ -566,7 +613,7 @@ __device__ __forceinline__ void wgrad64_shared_x(const bf16_t* const (&Y)[NM], c
   const bool bias = wave < 4;
   const int g = lane >> 4, c16 = lane & 15;
   // private copies need the 8-wave block mapping of frag_slot (the host refuses the mode otherwise)
-  const bool priv = NW == 8 && c.gm.priv, rmw = priv && !c.gm.first;
+  const bool priv = !MDL_NO_PRIV && NW == 8 && c.gm.priv, rmw = PRIV_LOADS && priv && !c.gm.first;
   f32x4 old[NM][NCT];
   float oldb[NM];
 #pragma unroll
@@ -574,8 +621,8 @@ __device__ __forceinline__ void wgrad64_shared_x(const bf16_t* const (&Y)[NM], c
     float* dW = c.g(m[i]->dW);
     float* db = c.g(m[i]->db);
 #pragma unroll
-    for (int j = 0; j < NCT; ++j) old[i][j] = (rmw && dW) ? *frag_slot(dW, wave, lane, j) : f32x4{0.f, 0.f, 0.f, 0.f};
-    oldb[i] = (rmw && bias && db && c16 < 4) ? db[16 * rb + 4 * g + c16] : 0.f;
+    for (int j = 0; j < NCT; ++j) old[i][j] = (rmw && dW) ? priv_ld4(frag_slot(dW, wave, lane, j)) : f32x4{0.f, 0.f, 0.f, 0.f};
+    oldb[i] = (rmw && bias && db && c16 < 4) ? priv_ld1(db + 16 * rb + 4 * g + c16) : 0.f;
   }
   f32x4 acc[NM][NCT], accb[NM];
 #pragma unroll
@@ -606,7 +653,7 @@ __device__ __forceinline__ void wgrad64_shared_x(const bf16_t* const (&Y)[NM], c
     if (dW) {
       if (priv) {
 #pragma unroll
-        for (int j = 0; j < NCT; ++j) *frag_slot(dW, wave, lane, j) = acc[i][j] + old[i][j];
+        for (int j = 0; j < NCT; ++j) priv_st4(frag_slot(dW, wave, lane, j), acc[i][j], old[i][j], c.gm.first);
       } else if constexpr (WG_ROWS2) {
         flush_rows2(acc[i][0], acc[i][1], dW, rb, wg_ct(wave, 0), lane);
       } else {
@@ -619,7 +666,7 @@ __device__ __forceinline__ void wgrad64_shared_x(const bf16_t* const (&Y)[NM], c
     }
     if (bias && db && c16 < 4) {
       const float v = c16 == 0 ? accb[i][0] : c16 == 1 ? accb[i][1] : c16 == 2 ? accb[i][2] : accb[i][3];
-      if (priv) db[16 * rb + 4 * g + c16] = v + oldb[i];
+      if (priv) priv_st1(db + 16 * rb + 4 * g + c16, v, oldb[i], c.gm.first);
       else atomicAdd(db + 16 * rb + 4 * g + c16, v);
     }
   }

@@ -35,7 +35,31 @@ struct PPOArgs {
   float clip, coef_v, coef_e, huber_delta, beta, eps, omb;   // omb = 1 - beta computed in double on the host
   int use_huber, use_clip_v, use_vam, use_pam, use_vn, update_vn;
   int n_lp;         // log-prob / entropy entries per token (continuous action type: one per action dimension)
+  // round 6: old_logp / adv / vpred / ret / active are the rollout buffer's rows read through the epoch permutation
+  // (sidx[minibatch sequence] = buffer sequence of L tokens; null = dense minibatch arrays), and the advantages are
+  // standardised here from the epoch's masked sums ((x - mean) / (std + eps), rl_ops.hip gather_rows' arithmetic)
+  const long long* sidx;
+  int L;
+  const double* adv_sums;   // null: adv already standardised
+  float adv_eps;
 };
+
+__device__ __forceinline__ size_t ppo_src(const PPOArgs& a, int i) {
+  if (!a.sidx) return (size_t)i;
+  const int s = i / a.L;
+  return (size_t)a.sidx[s] * (size_t)a.L + (size_t)(i - s * a.L);
+}
+__device__ __forceinline__ void adv_norm_params(const PPOArgs& a, float& mean, float& sd) {
+  mean = 0.f;
+  sd = 1.f;
+  if (!a.adv_sums) return;
+  const double cnt = a.adv_sums[2] < 1.0 ? 1.0 : a.adv_sums[2];
+  const double m = a.adv_sums[0] / cnt;
+  double var = a.adv_sums[1] / cnt - m * m;
+  var = var < 0.0 ? 0.0 : var;
+  mean = (float)m;
+  sd = (float)sqrt(var) + a.adv_eps;
+}
 
 #define MAXOBJ 2
 
@@ -46,13 +70,14 @@ __global__ __launch_bounds__(256) void ppo_reduce_kernel(PPOArgs a) {
 #pragma unroll
   for (int k = 0; k < 2 * MAXOBJ + 2; ++k) acc[k] = 0.f;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
+    const size_t si = ppo_src(a, i);
     for (int o = 0; o < a.n_obj; ++o) {
-      const float r = a.ret[(size_t)i * a.n_obj + o];
+      const float r = a.ret[si * a.n_obj + o];
       acc[o] += r;
       acc[a.n_obj + o] += r * r;
     }
     acc[2 * a.n_obj] += 1.f;
-    acc[2 * a.n_obj + 1] += a.active[i];
+    acc[2 * a.n_obj + 1] += a.active[si];
   }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (int k = 0; k < K; ++k) {
@@ -87,24 +112,42 @@ __device__ __forceinline__ float huber(float e, float d) {
   return ae <= d ? 0.5f * e * e : d * (ae - 0.5f * d);
 }
 
-__global__ __launch_bounds__(256) void ppo_grad_kernel(PPOArgs a) {
+// FUSE_VN (round 6): the ValueNorm update of ppo_vn_update_kernel is computed by EVERY workgroup from the running
+// moments and this minibatch's statistics (the same fp32 expressions, so the same values), and the LAST workgroup to
+// finish (an arrival counter) writes the new moments back — all reads of the old moments precede every arrival, so
+// one launch replaces two.  ctr: a zeroed int the last workgroup re-zeroes.
+template <bool FUSE_VN>
+__device__ __forceinline__ void ppo_grad_body(const PPOArgs& a, unsigned int* ctr) {
   __shared__ float sm[4][4];
   const float sum_a = a.stats[2 * a.n_obj + 1], n = (float)a.n;
   const float inv_pa = a.use_pam ? 1.f / fmaxf(sum_a, 1.f) : 1.f / n;
   const float inv_va = (a.use_vam ? 1.f / fmaxf(sum_a, 1.f) : 1.f / n) / (float)a.n_obj;
-  float mean[MAXOBJ], istd[MAXOBJ];
+  float mean[MAXOBJ], istd[MAXOBJ], vnew[2 * MAXOBJ + 1];
   {
-    const float d = fmaxf(a.vn[2 * a.n_obj], a.eps);
+    const float cnt = a.stats[2 * a.n_obj];
+    for (int o = 0; o < 2 * a.n_obj + 1; ++o) {
+      float x = a.vn[o];
+      if (FUSE_VN) {   // ppo_vn_update_kernel's arithmetic
+        if (o < a.n_obj) x = x * a.beta + (a.stats[o] / cnt) * a.omb;
+        else if (o < 2 * a.n_obj) x = x * a.beta + (a.stats[o] / cnt) * a.omb;
+        else x = x * a.beta + a.omb;
+      }
+      vnew[o] = x;
+    }
+    const float d = fmaxf(vnew[2 * a.n_obj], a.eps);
     for (int o = 0; o < a.n_obj; ++o) {
-      const float m = a.vn[o] / d;
-      const float var = fmaxf(a.vn[a.n_obj + o] / d - m * m, 1e-2f);
+      const float m = vnew[o] / d;
+      const float var = fmaxf(vnew[a.n_obj + o] / d - m * m, 1e-2f);
       mean[o] = a.use_vn ? m : 0.f;
       istd[o] = a.use_vn ? rsqrtf(var) : 1.f;
     }
   }
+  float adv_mean, adv_sd;
+  adv_norm_params(a, adv_mean, adv_sd);
   float pl = 0.f, vl = 0.f, el = 0.f, rl = 0.f;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
-    const float act = a.active[i];
+    const size_t si = ppo_src(a, i);
+    const float act = a.active[si];
     // policy: -min(r A, clip(r) A)
     // multi-objective MAT (momat / dmomat): one advantage per objective, the surrogate summed over objectives
     // (mat_trainer.py:129-139 on (B, A, n_obj) advantages: min(...).sum(-1))
@@ -116,11 +159,12 @@ __global__ __launch_bounds__(256) void ppo_grad_kernel(PPOArgs a) {
     const float inv_lp = 1.f / (float)a.n_lp;
     for (int k = 0; k < a.n_lp; ++k) {
       const size_t q = (size_t)i * a.n_lp + k;
-      const float imp = __expf(a.logp[q] - a.old_logp[q]);
+      const float imp = __expf(a.logp[q] - a.old_logp[si * a.n_lp + k]);
       const float ic = fminf(fmaxf(imp, 1.f - a.clip), 1.f + a.clip);
       float dm = 0.f, sm_ = 0.f;
       for (int o = 0; o < a.n_obj; ++o) {
-        const float ad = a.adv[(size_t)i * a.n_obj + o];
+        float ad = a.adv[si * a.n_obj + o];
+        if (a.adv_sums) ad = (ad - adv_mean) / adv_sd;
         const float s1 = imp * ad, s2 = ic * ad;
         if (s1 <= s2) dm += imp * ad;
         else dm += (imp >= 1.f - a.clip && imp <= 1.f + a.clip) ? imp * ad : 0.f;  // clamp passes grad inclusively
@@ -136,11 +180,11 @@ __global__ __launch_bounds__(256) void ppo_grad_kernel(PPOArgs a) {
     // value
     const float wv = a.use_vam ? act * inv_va : inv_va;
     for (int o = 0; o < a.n_obj; ++o) {
-      const size_t j = (size_t)i * a.n_obj + o;
-      const float v = a.v[j], vp = a.vpred[j];
+      const size_t j = (size_t)i * a.n_obj + o, sj = si * a.n_obj + o;
+      const float v = a.v[j], vp = a.vpred[sj];
       const float dvc = v - vp;
       const float vc = vp + fminf(fmaxf(dvc, -a.clip), a.clip);
-      const float tgt = (a.ret[j] - mean[o]) * istd[o];
+      const float tgt = (a.ret[sj] - mean[o]) * istd[o];
       const float eo = tgt - v, ec = tgt - vc;
       const float lo = a.use_huber ? huber(eo, a.huber_delta) : 0.5f * eo * eo;
       const float lc = a.use_huber ? huber(ec, a.huber_delta) : 0.5f * ec * ec;
@@ -166,7 +210,17 @@ __global__ __launch_bounds__(256) void ppo_grad_kernel(PPOArgs a) {
     for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += sm[w][threadIdx.x];
     atomicAdd(a.out + threadIdx.x, s);
   }
+  if (FUSE_VN && threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(ctr, 1u) == gridDim.x - 1) {   // the last workgroup: every other one has read the old moments
+      for (int o = 0; o < 2 * a.n_obj + 1; ++o) a.vn[o] = vnew[o];
+      *ctr = 0u;
+      __threadfence();
+    }
+  }
 }
+__global__ __launch_bounds__(256) void ppo_grad_kernel(PPOArgs a) { ppo_grad_body<false>(a, nullptr); }
+__global__ __launch_bounds__(256) void ppo_grad_vn_kernel(PPOArgs a, unsigned int* ctr) { ppo_grad_body<true>(a, ctr); }
 
 static int ppo_grid(int n) {
   int g = (n + 255) / 256;
@@ -191,6 +245,17 @@ MDL_API int mdl_ppo_loss(const PPOArgs* a, hipStream_t st) {
 MDL_API int mdl_ppo_reduce(const PPOArgs* a, hipStream_t st) {
   hipMemsetAsync(a->stats, 0, sizeof(float) * (2 * a->n_obj + 2), st);
   hipLaunchKernelGGL(ppo_reduce_kernel, dim3(ppo_grid(a->n)), dim3(256), 0, st, *a);
+  MDL_CHECK_LAUNCH();
+  return 0;
+}
+
+// ValueNorm update + loss gradients in ONE launch (FUSE_VN); ctr: a zeroed device uint the kernel leaves zeroed
+MDL_API int mdl_ppo_finish_fused(const PPOArgs* a, unsigned int* ctr, hipStream_t st) {
+  if (!a->update_vn) {
+    hipLaunchKernelGGL(ppo_grad_kernel, dim3(ppo_grid(a->n)), dim3(256), 0, st, *a);
+  } else {
+    hipLaunchKernelGGL(ppo_grad_vn_kernel, dim3(ppo_grid(a->n)), dim3(256), 0, st, *a, ctr);
+  }
   MDL_CHECK_LAUNCH();
   return 0;
 }
@@ -353,6 +418,50 @@ MDL_API int mdl_grad_reduce_norm(float* g, float* ws, int n, long long stride, i
   return 0;
 }
 
+// Reduction of the private copies, one tile of 64 float4 (256 floats) per workgroup of 256 threads: wave w sums
+// copies [w C/4, (w+1) C/4) of the tile (16 loads in flight, 1 KB coalesced per wave-instruction), wave 0 adds the
+// four group sums in a fixed order — a fixed summation tree, so the result is deterministic, and 4x the memory
+// parallelism of one thread per element walking all C copies (the 256-copy reduction was latency-bound: 32 round
+// trips of 8 loads per thread).  Writes g[dst[.]] and returns this thread's Σ g² (wave 0's lanes; 0 elsewhere).
+__device__ __forceinline__ float priv_reduce_tile(float* g, const float* ws, const int* dst, int tile, int lo, int n,
+                                                  long long stride, int copies, int accumulate) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  __shared__ f4v part[4][64];
+  const int e = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int i4 = tile * 64 + e, n4 = n >> 2;
+  const bool in = i4 >= (lo >> 2) && i4 < n4;   // [lo, n): a tile straddling a range bound reduces only its part
+  const size_t st4 = (size_t)(stride >> 2);
+  const int k0 = (copies * grp) >> 2, k1 = (copies * (grp + 1)) >> 2;
+  f4v s = {0.f, 0.f, 0.f, 0.f};
+  if (in) {
+    const f4v* w4 = reinterpret_cast<const f4v*>(ws) + i4;
+    int k = k0;
+    for (; k + 16 <= k1; k += 16) {
+      f4v v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = __builtin_nontemporal_load(w4 + (size_t)(k + j) * st4);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) s += v[j];
+    }
+    for (; k < k1; ++k) s += __builtin_nontemporal_load(w4 + (size_t)k * st4);
+  }
+  part[grp][e] = s;
+  __syncthreads();
+  float q = 0.f;
+  if (grp == 0 && in) {
+    const f4v t = ((part[0][e] + part[1][e]) + part[2][e]) + part[3][e];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int d = dst[4 * i4 + j];
+      const float gi = accumulate ? g[d] + t[j] : t[j];
+      g[d] = gi;
+      q += gi * gi;
+    }
+  }
+  __syncthreads();   // part[] is reused by the next tile
+  return q;
+}
+
 // Private-copy workspace (round 6, mat_train_common.h GradMode): one copy per workgroup of the backward launches,
 // every entry a workgroup writes rewritten by its first chunk — so no zero fill, and a fixed summation order:
 //   g[dst[s]] = (accumulate ? g[dst[s]] : 0) + Σ_{k < copies} ws[k * stride + s]   (k ascending)
@@ -364,21 +473,11 @@ __global__ __launch_bounds__(256) void grad_reduce_priv_kernel(float* g, const f
                                                                float* sumsq) {
   __shared__ float sm[4];
   float q = 0.f;
-  for (int i = lo + blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    float s = 0.f;
-    int k = 0;
-    for (; k + 8 <= copies; k += 8) {
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = ws[(size_t)(k + j) * stride + i];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s += v[j];
-    }
-    for (; k < copies; ++k) s += ws[(size_t)k * stride + i];
-    const int d = dst[i];
-    const float gi = accumulate ? g[d] + s : s;
-    g[d] = gi;
-    q += gi * gi;
+  // [lo, n) in tiles of 256 floats (lo, n multiples of 4: parameter ranges are 16-float padded)
+  const int t0 = lo >> 8, t1 = (n + 255) >> 8;
+  for (int t = t0 + blockIdx.x; t < t1; t += gridDim.x) {
+    // a tile straddling lo / n reduces only its in-range float4s: the elements outside belong to another call
+    q += priv_reduce_tile(g, ws, dst, t, lo, n, stride, copies, accumulate);
   }
   if (!sumsq) return;
   q = wave_sum(q);
@@ -390,7 +489,7 @@ __global__ __launch_bounds__(256) void grad_reduce_priv_kernel(float* g, const f
 // elements [lo, hi) of the flat gradient (a parameter range: no 64 x 64 matrix straddles it); sumsq whole-buffer only
 MDL_API int mdl_grad_reduce_priv(float* g, const float* ws, const int* dst, int lo, int hi, long long stride,
                                  int copies, int accumulate, float* sumsq, hipStream_t st) {
-  if (copies < 1 || lo < 0 || hi < lo || (sumsq && lo != 0)) return -1;
+  if (copies < 1 || lo < 0 || hi < lo || (sumsq && lo != 0) || (lo & 3) || (hi & 3) || (stride & 3)) return -1;
   hipLaunchKernelGGL(grad_reduce_priv_kernel, dim3(ADAM_NB), dim3(256), 0, st, g, ws, dst, lo, hi, stride, copies,
                      accumulate, sumsq);
   MDL_CHECK_LAUNCH();
@@ -406,49 +505,22 @@ MDL_API int mdl_grad_reduce(float* g, float* ws, int n, long long stride, int co
 }
 
 // ------------------------------------------------------------------------------------------- fused update (round 6)
-// ONE cooperative launch per single-GPU minibatch replaces grad_reduce + adam_norm / adam_step + pack_weights (and the
-// flat-buffer memset): (1) fold the private workspace copies into the flat gradient (grad_reduce_priv's loop) with
-// per-workgroup Σ g² partials; (2) one grid barrier; (3) every workgroup sums the partials in a fixed order (the
-// same norm everywhere, run to run), workgroups 0 .. nmat-1 each apply clip + Adam to ONE 64 x 64 weight matrix and
-// repack it from LDS into the forward / backward fragment orders of the training kernels (csrc/rl_ops.hip
-// pack_weights layout), the other workgroups update the remaining parameters (rest[] indices).  The grid barrier's
-// co-residency is guaranteed by hipLaunchCooperativeKernel; its wait is bounded (an error word, never a hang).
+// The single-GPU end of a minibatch in TWO launches instead of four (grad_reduce + adam_norm / adam_step +
+// pack_weights, and the flat-buffer memset): grad_reduce_priv_kernel folds the private workspace copies with the
+// Σ g² partials, then adam_pack_kernel sums the partials in a fixed order (the same norm in every workgroup, run to
+// run), applies clip + Adam, and repacks each 64 x 64 weight matrix it owns from LDS into the training kernels'
+// fragment orders (csrc/rl_ops.hip pack_weights layout): workgroups 0 .. nmat-1 own one matrix each, the others
+// update the remaining parameters (rest[]).
+// (A one-launch cooperative variant with a grid barrier measured ~330 us per call: every workgroup's agent-scope
+// fences wrote back / invalidated its XCD's L2 — two launches cost ~40 us.)
 struct PackEntU { const float* src; unsigned short* fw; unsigned short* bw; unsigned short* fa; unsigned short* ba; };
 struct UpdArgs {
   float* g; const float* ws; const int* dst; int n; long long stride; int copies; int accumulate;
   AdamArgs a;
   const PackEntU* tab; const int* mat_off; int nmat;   // packed matrices and their flat offsets
   const int* rest; int n_rest;                         // flat indices of every other parameter element
-  unsigned int* bar;                                   // [0] arrivals, [1] generation, [2] error word
+  unsigned int* bar;                                   // (unused: the one-launch variant's barrier words)
 };
-
-__device__ __forceinline__ bool upd_grid_barrier(unsigned int* bar) {
-  __threadfence();   // this thread's phase-1 stores visible at agent scope
-  __syncthreads();
-  __shared__ int ok;
-  if (threadIdx.x == 0) {
-    ok = 1;
-    const unsigned gen = __hip_atomic_load(bar + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned arrived = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (arrived == gridDim.x - 1) {
-      __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(bar + 1, gen + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      long long spins = 0;
-      while (__hip_atomic_load(bar + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == gen) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1ll << 26)) {   // ~seconds: never hang the device on a broken co-residency assumption
-          __hip_atomic_store(bar + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          ok = 0;
-          break;
-        }
-      }
-    }
-  }
-  __syncthreads();
-  __threadfence();
-  return ok != 0;
-}
 
 __device__ __forceinline__ float adam_elem(const AdamArgs& a, int i, float scale, float ib1, float ib2) {
   float g = a.g[i] * scale;
@@ -463,39 +535,13 @@ __device__ __forceinline__ float adam_elem(const AdamArgs& a, int i, float scale
   return p;
 }
 
-__global__ __launch_bounds__(256) void update_fused_kernel(UpdArgs u) {
-  __shared__ float sm[4];
+__global__ __launch_bounds__(1024) void adam_pack_kernel(UpdArgs u) {
   __shared__ float snorm;
   __shared__ float Mf[4096];
-  // (1) private workspace copies -> flat gradient, Σ g² partial of this workgroup
-  float q = 0.f;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < u.n; i += gridDim.x * blockDim.x) {
-    float s = 0.f;
-    int k = 0;
-    for (; k + 8 <= u.copies; k += 8) {
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = u.ws[(size_t)(k + j) * u.stride + i];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s += v[j];
-    }
-    for (; k < u.copies; ++k) s += u.ws[(size_t)k * u.stride + i];
-    const int d = u.dst[i];
-    const float gi = u.accumulate ? u.g[d] + s : s;
-    u.g[d] = gi;
-    q += gi * gi;
-  }
-  q = wave_sum(q);
-  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = q;
-  __syncthreads();
-  if (threadIdx.x == 0) u.a.sumsq[4 + blockIdx.x] = (sm[0] + sm[1]) + (sm[2] + sm[3]);
-  // (2)
-  if (!upd_grid_barrier(u.bar)) return;
-  // (3) norm of the final gradient: Σ of the gridDim.x partials in a fixed order
   const AdamArgs& a = u.a;
-  if (threadIdx.x < 64) {
+  if (threadIdx.x < 64) {   // Σ of the ADAM_NB partials of grad_reduce_priv, fixed order
     float v = 0.f;
-    for (int j = threadIdx.x; j < (int)gridDim.x; j += 64) v += a.sumsq[4 + j];
+    for (int j = threadIdx.x; j < ADAM_NB; j += 64) v += a.sumsq[4 + j];
     const float tot = wave_sum(v);
     if (threadIdx.x == 0) snorm = sqrtf(tot);
   }
@@ -515,10 +561,10 @@ __global__ __launch_bounds__(256) void update_fused_kernel(UpdArgs u) {
   const float ib1 = 1.f / (1.f - powf(a.beta1, t)), ib2 = 1.f / (1.f - powf(a.beta2, t));
   if ((int)blockIdx.x < u.nmat) {
     const int off = u.mat_off[blockIdx.x];
-    for (int e = threadIdx.x; e < 4096; e += 256) Mf[e] = adam_elem(a, off + e, scale, ib1, ib2);
+    for (int e = threadIdx.x; e < 4096; e += blockDim.x) Mf[e] = adam_elem(a, off + e, scale, ib1, ib2);
     __syncthreads();
     const PackEntU pe = u.tab[blockIdx.x];
-    for (int idx = threadIdx.x; idx < 4096; idx += 256) {
+    for (int idx = threadIdx.x; idx < 4096; idx += blockDim.x) {
       const int j = idx & 7, lane = (idx >> 3) & 63, ks = (idx >> 9) & 1, ct = idx >> 10;
       const int n = 16 * ct + (lane & 15), k = 32 * ks + 8 * (lane >> 4) + j;
       if (pe.fw) pe.fw[idx] = mdl::f2bf(Mf[n * 64 + k]);
@@ -534,12 +580,13 @@ __global__ __launch_bounds__(256) void update_fused_kernel(UpdArgs u) {
   }
 }
 
-constexpr int UPD_NB = 1024;   // = ADAM_NB: one Σ g² partial per workgroup
-MDL_API int mdl_update_fused_grid() { return UPD_NB; }
 MDL_API int mdl_update_fused(const UpdArgs* u, hipStream_t st) {
-  if (u->copies < 1 || u->nmat >= UPD_NB || u->n_rest < 0) return -1;
-  UpdArgs a = *u;
-  void* args[] = {&a};
-  hipError_t e = hipLaunchCooperativeKernel((const void*)update_fused_kernel, dim3(UPD_NB), dim3(256), args, 0, st);
-  return e == hipSuccess ? 0 : (int)e;
+  if (u->copies < 1 || u->nmat < 0 || u->n_rest < 0 || (u->n & 3) || (u->stride & 3)) return -1;
+  hipLaunchKernelGGL(grad_reduce_priv_kernel, dim3(ADAM_NB), dim3(256), 0, st, u->g, u->ws, u->dst, 0, u->n, u->stride,
+                     u->copies, u->accumulate, u->a.sumsq);
+  MDL_CHECK_LAUNCH();
+  const int rest_wg = (u->n_rest + 1023) / 1024;   // 1024-thread workgroups: a matrix's 4096 elements in 4 steps
+  hipLaunchKernelGGL(adam_pack_kernel, dim3(u->nmat + (rest_wg < 64 ? rest_wg : 64)), dim3(1024), 0, st, *u);
+  MDL_CHECK_LAUNCH();
+  return 0;
 }

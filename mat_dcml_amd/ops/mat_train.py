@@ -53,7 +53,7 @@ class EncP(ctypes.Structure):
                [("blk", Blk * 3), ("h1", Mat), ("lnh", LNp), ("wh2", VP), ("bh2", VP), ("d_wh2", VP), ("rep", VP),
                 ("v", VP), ("sv", Sv * 3), ("drep", VP), ("dv", VP), ("g_delta", ctypes.c_longlong),
                 ("g_stride", ctypes.c_longlong), ("g_copies", ctypes.c_int), ("d_bh2", VP), ("hs", HSv), ("es", HSv),
-                ("g_mode", ctypes.c_int)]
+                ("g_mode", ctypes.c_int), ("sidx", VP)]
 
 
 class DecP(ctypes.Structure):
@@ -64,7 +64,7 @@ class DecP(ctypes.Structure):
                                   "ent")] + \
                [("sv", Sv * 3)] + [(n, VP) for n in ("dlogp", "dent", "drep", "sv_head")] + \
                [("g_delta", ctypes.c_longlong), ("g_stride", ctypes.c_longlong), ("g_copies", ctypes.c_int)] + \
-               [("cont", ctypes.c_int), ("ba", VP), ("d_ba", VP), ("hs", HSv), ("g_mode", ctypes.c_int)]
+               [("cont", ctypes.c_int), ("ba", VP), ("d_ba", VP), ("hs", HSv), ("g_mode", ctypes.c_int), ("sidx", VP)]
 
 
 # Training kernels (csrc/mat_train_ct.h): token-on-lane tiles, weight A fragments in permuted k order, register-
@@ -338,12 +338,14 @@ class EncoderFused:
                 self.emb = ObsEmbed(self.model)
             self.emb.refresh()
 
-    def forward(self, obs, save=True):
-        """obs (B, L, od) -> (v (B, L, n_obj), rep (B, L, 64) f32)."""
+    def forward(self, obs, save=True, idx=None):
+        """obs (B, L, od) -> (v (B, L, n_obj), rep (B, L, 64) f32).  ``idx`` (int64 [B]): obs is the rollout
+        buffer (N, L, od) and minibatch sequence s reads its row idx[s] in-kernel (no gather copy)."""
         m = self.model
         model_pack(m)
         self._build()
-        B, L, od = obs.shape
+        _, L, od = obs.shape
+        B = obs.shape[0] if idx is None else idx.numel()
         dev = obs.device
         SQ, NRP, sfx = geometry(L)
         if not save:   # rollout / value passes: small batches — spread them over every CU (nothing is saved, so
@@ -352,6 +354,8 @@ class EncoderFused:
         obs = obs.float().contiguous()
         pre = stat = None
         if od > MAX_FUSED_OBS:   # wide observations: embedding pre-activation from the obs-embedding kernel
+            if idx is not None:  # (the wide embedding reads dense rows)
+                obs, idx = obs[idx].contiguous(), None
             if getattr(self, "emb", None) is None:
                 self.emb = ObsEmbed(m)
             pre, stat = self.emb.forward(obs.view(n_tok, od))
@@ -359,7 +363,7 @@ class EncoderFused:
         v = torch.empty(B, L, m.n_objective, device=dev)
         p = self.p
         p.Bs, p.L, p.od, p.SQ, p.NRP, p.n_obj = B, L, od, SQ, NRP, m.n_objective
-        p.obs, p.rep, p.v = obs.data_ptr(), rep.data_ptr(), v.data_ptr()
+        p.obs, p.rep, p.v, p.sidx = obs.data_ptr(), rep.data_ptr(), v.data_ptr(), _ptr(idx)
         saves = []
         if save:
             for bi in range(m.n_block):
@@ -379,21 +383,22 @@ class EncoderFused:
             p.hs, p.es = HSv(), HSv()
         check(_enc_fwd(sfx, p, _ptr(pre), m.n_block, save), "mat_enc_fwd")
         self.ctx = (obs, rep, v, saves, [Sv.from_buffer_copy(p.sv[i]) for i in range(m.n_block)], pre, stat,
-                    HSv.from_buffer_copy(p.hs), HSv.from_buffer_copy(p.es))
+                    HSv.from_buffer_copy(p.hs), HSv.from_buffer_copy(p.es), idx)
         return v, rep
 
     def backward(self, drep, dv):
         m = self.model
-        obs, rep, v, saves, svs, pre, stat, hs, es = self.ctx
+        obs, rep, v, saves, svs, pre, stat, hs, es, idx = self.ctx
         self._build()
         p = self.p
         p.hs, p.es = hs, es
         drep = drep.float().contiguous()
         dv = dv.float().contiguous()
-        B, L, od = obs.shape
+        B, L, od = rep.shape[0], obs.shape[1], obs.shape[2]
         SQ, NRP, sfx = geometry(L)
         p.Bs, p.L, p.od, p.SQ, p.NRP, p.n_obj = B, L, od, SQ, NRP, m.n_objective
         p.obs, p.rep, p.v, p.drep, p.dv = obs.data_ptr(), rep.data_ptr(), v.data_ptr(), drep.data_ptr(), dv.data_ptr()
+        p.sidx = _ptr(idx)
         for i, s in enumerate(svs):
             p.sv[i] = s
         _set_workspace(p, m, B, SQ)
@@ -465,7 +470,8 @@ class DecoderFused:
         p.Bs, p.L, p.A, p.SQ, p.NRP, p.n_disc = B, L, self.model.action_dim, SQ, NRP, self._n_disc(L)
         return sfx
 
-    def forward(self, rep, actions, ava=None, save=True):
+    def forward(self, rep, actions, ava=None, save=True, idx=None):
+        """``idx`` (int64 [B]): actions / ava are the rollout buffer's (N, L, .) rows, read through idx in-kernel."""
         m = self.model
         model_pack(m)
         self._build()
@@ -474,13 +480,15 @@ class DecoderFused:
         n_tok = B * L
         rep = rep.float().contiguous()
         nlp = m.action_dim if self.cont else 1   # continuous: per-dimension actions / log-probs / entropies
-        act = actions.reshape(B, L, nlp).float().contiguous()
+        nrow = B if idx is None else actions.shape[0]
+        act = actions.reshape(nrow, L, nlp).float().contiguous()
         ava_c = ava.float().contiguous() if (ava is not None and not self.cont) else None
         logp = torch.empty(B, L, nlp, device=dev)
         ent = torch.empty(B, L, nlp, device=dev)
         sfx = self._geom(B, L)
         p = self.p
         p.act, p.ava, p.rep, p.logp, p.ent = act.data_ptr(), _ptr(ava_c), rep.data_ptr(), logp.data_ptr(), ent.data_ptr()
+        p.sidx = _ptr(idx)
         saves = []
         if save:
             for bi in range(m.n_block):
@@ -500,21 +508,21 @@ class DecoderFused:
             p.hs = HSv()
         check(getattr(lib(), "mdl_mat_dec_fwd" + sfx)(ctypes.byref(p), m.n_block, int(save), kernels._stream()), "mat_dec_fwd")
         self.ctx = (rep, act, ava_c, logp, ent, saves, [Sv.from_buffer_copy(p.sv[i]) for i in range(m.n_block)],
-                    p.sv_head, HSv.from_buffer_copy(p.hs))
+                    p.sv_head, HSv.from_buffer_copy(p.hs), idx)
         return logp, ent
 
     def backward(self, dlogp, dent):
         m = self.model
-        rep, act, ava_c, logp, ent, saves, svs, head, hs = self.ctx
+        rep, act, ava_c, logp, ent, saves, svs, head, hs, idx = self.ctx
         self._build()
-        B, L = act.shape[:2]
+        B, L = rep.shape[:2]
         sfx = self._geom(B, L)
         p = self.p
         dlogp = dlogp.reshape(-1).float().contiguous()
         dent = dent.reshape(-1).float().contiguous()
         # the backward writes every row of d rep (its last decoder block overwrites)
         drep = torch.empty_like(rep)
-        p.act, p.ava, p.rep = act.data_ptr(), _ptr(ava_c), rep.data_ptr()
+        p.act, p.ava, p.rep, p.sidx = act.data_ptr(), _ptr(ava_c), rep.data_ptr(), _ptr(idx)
         p.dlogp, p.dent, p.drep, p.sv_head = dlogp.data_ptr(), dent.data_ptr(), drep.data_ptr(), head
         p.hs = hs
         for i, s in enumerate(svs):
@@ -680,7 +688,7 @@ def reduce_grad_workspace(model, lo=0, hi=None, norm_into=None, accumulate=True,
     return False
 
 
-class UpdArgs(ctypes.Structure):   # csrc/ppo.hip update_fused_kernel
+class UpdArgs(ctypes.Structure):   # csrc/ppo.hip mdl_update_fused
     _fields_ = [("g", VP), ("ws", VP), ("dst", VP), ("n", ctypes.c_int), ("stride", ctypes.c_longlong),
                 ("copies", ctypes.c_int), ("accumulate", ctypes.c_int), ("a", AdamArgs), ("tab", VP),
                 ("mat_off", VP), ("nmat", ctypes.c_int), ("rest", VP), ("n_rest", ctypes.c_int), ("bar", VP)]
@@ -712,10 +720,11 @@ class _UpdState:
 
 
 def update_fused(model, opt, accumulate=False):
-    """Single-GPU end of a minibatch in ONE cooperative launch (csrc/ppo.hip update_fused_kernel): fold the private
-    gradient workspace into the flat gradient, clip + Adam over every parameter, and repack the 64 x 64 linears'
-    bf16 fragments the training kernels read — replacing grad_reduce, adam_step and pack_weights (and the memset).
-    The caller bumps the model version; the ModelPack is marked current (its packs were written here)."""
+    """Single-GPU end of a minibatch in TWO launches (csrc/ppo.hip mdl_update_fused: grad_reduce_priv +
+    adam_pack): fold the private gradient workspace into the flat gradient with the Σ g² partials, then clip + Adam
+    over every parameter and repack the 64 x 64 linears' bf16 fragments the training kernels read — replacing
+    grad_reduce, adam_norm / adam_step and pack_weights (and the memset).  The caller bumps the model version; the
+    ModelPack is marked current (its packs were written here)."""
     st = getattr(model, "_mdl_upd", None)
     if st is None or st.mp is not getattr(model, "_mdl_pack", None):
         st = _UpdState(model, opt)

@@ -30,7 +30,8 @@ class PPOArgs(ctypes.Structure):
                                   "dent", "stats", "out", "vn")] + \
                [(k, ctypes.c_float) for k in ("clip", "coef_v", "coef_e", "huber_delta", "beta", "eps", "omb")] + \
                [(k, ctypes.c_int) for k in ("use_huber", "use_clip_v", "use_vam", "use_pam", "use_vn", "update_vn",
-                                            "n_lp")]
+                                            "n_lp")] + \
+               [("sidx", vp), ("L", ctypes.c_int), ("adv_sums", vp), ("adv_eps", ctypes.c_float)]
 
 
 class AdamArgs(ctypes.Structure):
@@ -42,6 +43,7 @@ class AdamArgs(ctypes.Structure):
 sig("mdl_ppo_loss", ctypes.POINTER(PPOArgs), vp)
 sig("mdl_ppo_reduce", ctypes.POINTER(PPOArgs), vp)
 sig("mdl_ppo_finish", ctypes.POINTER(PPOArgs), vp)
+sig("mdl_ppo_finish_fused", ctypes.POINTER(PPOArgs), vp, vp)
 sig("mdl_adam", ctypes.POINTER(AdamArgs), ctypes.c_int, vp)
 
 
@@ -216,6 +218,7 @@ class PPOLossFused:
         self.out = torch.zeros(4, dtype=torch.float32, device=device)
         self._vn = None
         self._g = None
+        self._ctr = torch.zeros(1, dtype=torch.int32, device=device)   # ppo_finish_fused's arrival counter
 
     def _vn_buffer(self, n_obj, device):
         """ValueNorm moments as views of one flat buffer the kernels update in place (bound once)."""
@@ -251,6 +254,10 @@ class PPOLossFused:
         ts = [t.reshape(-1).contiguous() if t.is_contiguous() else t.contiguous() for t in
               (mb["old_logp"], mb["adv"], mb["value_preds"], mb["returns"], mb["active"])]
         stats = self.stats if pre_stats is None else pre_stats
+        # round 6: mb may carry the rollout buffer's rows + the epoch permutation ("idx") and the advantage sums
+        # ("adv_sums"): the kernels read through the index and standardise the advantages themselves (no gather)
+        idx, adv_sums = mb.get("idx"), mb.get("adv_sums")
+        L = values.shape[1] if values.dim() == 3 else 1
         a = PPOArgs(n=N, n_obj=n_obj, v=P(values), logp=P(logp), ent=P(ent), old_logp=P(ts[0]), adv=P(ts[1]),
                     vpred=P(ts[2]), ret=P(ts[3]), active=P(ts[4]), dv=P(dv), dlogp=P(dlp), dent=P(dent),
                     stats=P(stats), out=P(self.out), vn=P(vn), clip=tr.clip_param, coef_v=tr.value_loss_coef,
@@ -259,10 +266,16 @@ class PPOLossFused:
                     omb=(1.0 - vnm.beta) if vnm is not None else 0.0, use_huber=int(tr._use_huber_loss),
                     use_clip_v=int(tr._use_clipped_value_loss), use_vam=int(tr._use_value_active_masks),
                     use_pam=int(tr._use_policy_active_masks), use_vn=int(vnm is not None),
-                    update_vn=int(vnm is not None), n_lp=n_lp)
+                    update_vn=int(vnm is not None), n_lp=n_lp, sidx=P(idx) if idx is not None else None, L=L,
+                    adv_sums=P(adv_sums) if adv_sums is not None else None, adv_eps=1e-5)
+        if idx is not None:
+            assert idx.dtype == torch.int64 and idx.is_contiguous() and idx.numel() * L == N
+        if adv_sums is not None:
+            assert adv_sums.dtype == torch.float64
         if pre_stats is not None:   # statistics of this minibatch precomputed (and all-reduced) for the epoch
             assert pre_stats.dtype == torch.float32 and pre_stats.numel() == 2 * n_obj + 2 and pre_stats.is_contiguous()
-            check(lib().mdl_ppo_finish(ctypes.byref(a), _stream()), "ppo_finish")
+            # ValueNorm update + loss gradients in one launch (round 6)
+            check(lib().mdl_ppo_finish_fused(ctypes.byref(a), P(self._ctr), _stream()), "ppo_finish_fused")
         elif comm is not None and comm.world_size > 1 and vnm is not None:
             check(lib().mdl_ppo_reduce(ctypes.byref(a), _stream()), "ppo_reduce")
             comm.all_reduce_sum_(self.stats[: 2 * n_obj + 1])

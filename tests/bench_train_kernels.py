@@ -20,16 +20,17 @@ def main(B=3200, L=33, iters=10):
     obs = torch.rand(B, L, 7, device=dev)
     ava = torch.ones(B, L, 2, device=dev)
     actions = (torch.rand(B, L, 1, device=dev) < 0.5).float()
-    # the trainer's gradient layout: one flat fp32 buffer, the backward's weight-gradient atomics spread over a
-    # 32-copy workspace (algos/mat_trainer.py; without it every workgroup adds into one copy)
+    # the trainer's gradient layout: one flat fp32 buffer and its workspace (algos/mat_trainer.py): private
+    # per-workgroup copies (round 6 default) or MAT_DCML_GRAD_MODE=atomic (32 shared copies, rounds 2-5)
     from mat_dcml_amd.ops import ppo_fused
     fp = ppo_fused.flatten_params(m)
     fg = torch.zeros_like(fp)
     for p, off in ppo_fused.param_offsets(m):
         p.grad = fg[off:off + p.numel()].view_as(p)
     copies = int(os.environ.get("MAT_DCML_GRAD_COPIES", "32"))
+    mode = os.environ.get("MAT_DCML_GRAD_MODE", "private")
     if copies > 0:
-        mat_train.attach_grad_workspace(m, fg, copies=copies)
+        mat_train.attach_grad_workspace(m, fg, copies=copies, mode=mode)
     enc, dec = mat_train.EncoderFused(m), mat_train.DecoderFused(m)
     ev = {k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for k in
           ("enc_fwd", "dec_fwd", "dec_bwd", "enc_bwd")}
@@ -37,10 +38,12 @@ def main(B=3200, L=33, iters=10):
     for it in range(iters + 2):
         ev["enc_fwd"][0].record(); v, rep = enc.forward(obs); ev["enc_fwd"][1].record()
         ev["dec_fwd"][0].record(); lp, ent = dec.forward(rep, actions, ava); ev["dec_fwd"][1].record()
+        m._mdl_gws_active = copies > 0
         ev["dec_bwd"][0].record(); drep = dec.backward(torch.ones_like(lp), torch.ones_like(ent)); ev["dec_bwd"][1].record()
         ev["enc_bwd"][0].record(); enc.backward(drep, torch.ones_like(v)); ev["enc_bwd"][1].record()
+        m._mdl_gws_active = False
         if copies > 0:
-            mat_train.reduce_grad_workspace(m)
+            mat_train.reduce_grad_workspace(m, accumulate=False)
         torch.cuda.synchronize()
         if it >= 2:
             for k, (s, e) in ev.items():

@@ -120,3 +120,42 @@ def test_missing_lib_dir_reaches_the_build(tmp_path):
     assert "LOCKFAIL" not in r.stdout, r.stdout + r.stderr
     assert (pkg / "_lib").is_dir()
     assert "rebuilding" in r.stdout and "BUILDFAIL" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="needs hipcc")
+def test_kernel_arg_structs_match_ctypes(tmp_path):
+    """The ctypes mirrors of the kernel argument structs (EncP / DecP / PPOArgs / AdamArgs / UpdArgs) must have the C
+    structs' sizes and field offsets: a field appended on one side only shifts every later pointer (round 6 grew
+    EncP / DecP / PPOArgs).  The C side is compiled for the host from the library's own headers."""
+    import ctypes
+    from mat_dcml_amd.ops import mat_train, ppo_fused
+    csrc = os.path.join(ROOT, "mat_dcml_amd", "csrc")
+    src = tmp_path / "sz.hip"
+    # the PPO / Adam / update structs live in ppo.hip: include it (its kernels compile for the host side as stubs)
+    src.write_text(f'''#include <cstdio>
+#include <cstddef>
+#include "{csrc}/mat_train_common.h"
+#include "{csrc}/ppo.hip"
+int main() {{
+  printf("EncP %zu %zu %zu\\n", sizeof(EncP), offsetof(EncP, g_mode), offsetof(EncP, sidx));
+  printf("DecP %zu %zu %zu\\n", sizeof(DecP), offsetof(DecP, g_mode), offsetof(DecP, sidx));
+  printf("PPOArgs %zu %zu %zu\\n", sizeof(PPOArgs), offsetof(PPOArgs, n_lp), offsetof(PPOArgs, adv_eps));
+  printf("AdamArgs %zu %zu %zu\\n", sizeof(AdamArgs), offsetof(AdamArgs, clip), offsetof(AdamArgs, npart));
+  printf("UpdArgs %zu %zu %zu\\n", sizeof(UpdArgs), offsetof(UpdArgs, a), offsetof(UpdArgs, bar));
+}}
+''')
+    exe = tmp_path / "sz"
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "-std=c++17", "-O0", "--offload-arch=gfx950", str(src), "-o", str(exe)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    # the host binary only prints sizeof / offsetof (no GPU needed)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60).stdout
+    got = {l.split()[0]: tuple(int(x) for x in l.split()[1:]) for l in out.strip().splitlines()}
+    want = {
+        "EncP": (ctypes.sizeof(mat_train.EncP), mat_train.EncP.g_mode.offset, mat_train.EncP.sidx.offset),
+        "DecP": (ctypes.sizeof(mat_train.DecP), mat_train.DecP.g_mode.offset, mat_train.DecP.sidx.offset),
+        "PPOArgs": (ctypes.sizeof(ppo_fused.PPOArgs), ppo_fused.PPOArgs.n_lp.offset, ppo_fused.PPOArgs.adv_eps.offset),
+        "AdamArgs": (ctypes.sizeof(ppo_fused.AdamArgs), ppo_fused.AdamArgs.clip.offset, ppo_fused.AdamArgs.npart.offset),
+        "UpdArgs": (ctypes.sizeof(mat_train.UpdArgs), mat_train.UpdArgs.a.offset, mat_train.UpdArgs.bar.offset),
+    }
+    assert got == want, (got, want)

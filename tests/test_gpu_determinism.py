@@ -10,7 +10,7 @@ bitwise-equal outputs — a missing barrier or an LDS race shows up as run-to-ru
   (relative 1e-5), and the max deviation is printed;
 * the trainer's fused PPO update (round 6, reference ``--cuda_deterministic``, DCML_MAT_Train.py:108-110): private
   per-workgroup gradient copies, 2^-32 fixed-point vector accumulators and fixed-order reductions make two whole PPO
-  iterations (rollout + 2 epochs, the fused reduce / clip / Adam / repack launch included) BITWISE identical —
+  iterations (rollout + 2 epochs, the fused reduce + clip / Adam / repack launches included) BITWISE identical —
   parameters, Adam moments and the optimizer scratch (grad norm, skipped-step count) — with the fused and the unfused
   update alike.
 """
@@ -91,28 +91,30 @@ def test_fused_training_repeatable(gpu):
     print(f"max relative run-to-run gradient deviation (fp32 atomic order): {worst:.2e}")
 
 
-def _ppo_run(gpu, iters=2, fused_update=True):
+def _ppo_run(gpu, iters=2, fused_update=True, mb_index="gather"):
     from mat_dcml_amd.config import get_config, parse_args
     from mat_dcml_amd.parallel.comm import Comm
     from mat_dcml_amd.runner.dcml_runner import DCMLRunner
-    old = os.environ.get("MAT_DCML_FUSED_UPDATE")
-    os.environ["MAT_DCML_FUSED_UPDATE"] = "1" if fused_update else "0"
+    env = {"MAT_DCML_FUSED_UPDATE": "1" if fused_update else "0", "MAT_DCML_MB_INDEX": mb_index}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         args = parse_args(["--n_workers", "32", "--n_rollout_threads", "32", "--episode_length", "10", "--ppo_epoch",
                            "2", "--num_mini_batch", "2", "--use_valuenorm", "--env_name", "DCML", "--seed", "3"],
                           get_config(), warn=False)
         r = DCMLRunner({"all_args": args, "device": gpu, "run_dir": None, "comm": Comm(device=gpu)})
+        tr = r.trainer
+        assert tr.fused and tr.deterministic and tr._upd_fused == fused_update
+        r.warmup()
+        for _ in range(iters):
+            r.train_iteration()
+        torch.cuda.synchronize()
     finally:
-        if old is None:
-            os.environ.pop("MAT_DCML_FUSED_UPDATE", None)
-        else:
-            os.environ["MAT_DCML_FUSED_UPDATE"] = old
-    tr = r.trainer
-    assert tr.fused and tr.deterministic and tr._upd_fused == fused_update
-    r.warmup()
-    for _ in range(iters):
-        r.train_iteration()
-    torch.cuda.synchronize()
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     opt = r.policy.optimizer
     return {"params": torch.cat([p.detach().reshape(-1) for p in r.policy.transformer.parameters()]),
             "exp_avg": opt.m.clone(), "exp_avg_sq": opt.v.clone(), "scratch": opt.scratch[:4].clone()}
@@ -126,12 +128,24 @@ def test_fused_ppo_iteration_bitwise_repeatable(gpu):
 
 
 def test_fused_update_matches_unfused_update(gpu):
-    """The one-launch reduce / clip / Adam / repack (csrc/ppo.hip update_fused_kernel) against the separate
-    grad_reduce_priv + adam_step + pack_weights launches: the same norm partials in the same order, so the runs agree
-    to the last bits of the Adam arithmetic (the two kernels' FMA contraction may differ)."""
+    """The fused reduce + clip / Adam / repack (csrc/ppo.hip mdl_update_fused: grad_reduce_priv + adam_pack) against
+    the separate grad_reduce_priv + adam_step + pack_weights launches: the same norm partials in the same order, so
+    the runs agree to the last bits of the Adam arithmetic (the two kernels' FMA contraction may differ)."""
     a, b = _ppo_run(gpu, fused_update=True), _ppo_run(gpu, fused_update=False)
     assert torch.equal(a["scratch"][1:3], b["scratch"][1:3]) or \
         abs(float(a["scratch"][1]) - float(b["scratch"][1])) <= 1e-6 * float(b["scratch"][1])
     d = ((a["params"] - b["params"]).norm() / b["params"].norm()).item()
     print(f"fused vs unfused update: relative parameter difference {d:.2e}")
     assert d < 1e-6, d
+
+
+def test_kernel_minibatch_index_matches_gather(gpu):
+    """MAT_DCML_MB_INDEX=kernel (the training kernels and the PPO loss read the buffer's rows through the epoch
+    permutation, csrc/mat_train_common.h src_tok, and standardise the advantages in-kernel) against the default
+    gather of each minibatch: the same rows in the same order, so the two runs agree to the advantage
+    standardisation's rounding (in-kernel (a - mean) * rstd vs the gather kernel's)."""
+    a, b = _ppo_run(gpu, mb_index="kernel"), _ppo_run(gpu, mb_index="gather")
+    d = ((a["params"] - b["params"]).norm() / b["params"].norm()).item()
+    dm = ((a["exp_avg"] - b["exp_avg"]).norm() / b["exp_avg"].norm()).item()
+    print(f"in-kernel minibatch index vs gather: relative parameter difference {d:.2e}, first moment {dm:.2e}")
+    assert d < 1e-5 and dm < 1e-3, (d, dm)
