@@ -244,15 +244,19 @@ def _native_build():
     return kernels.BUILD_ID
 
 
-# 32 workers: round-5 run with payment weight 3, selected on the held-out preset sets (profiles/r5_train32/README.md)
-DEFAULT_CKPT = {32: "profiles/r5_train32/transformer_500_beta3.pt"}
+# Trained checkpoints of the eval block, per worker count: (JSON key, path).  "trained" is always the reference reward
+# -(99 ct + payment) (reward_beta 1); 32 workers also report the round-5 payment-weight-3 run next to it.  Each was
+# selected on the held-out preset sets Sample_2..10 (profiles/r6_train*/README.md, profiles/r5_train32/README.md).
+DEFAULT_CKPT = {32: [("trained", "profiles/r6_train32/selected_beta1.pt"),
+                     ("trained_beta3", "profiles/r5_train32/transformer_500_beta3.pt")],
+                100: [("trained", "profiles/r6_train100/selected_beta1.pt")]}
 
 
 def eval_block(a, args, runner, dev):
     """"Eval task time": the reference benchmark protocol (``DCML_MAT_ALT_Benchmark.py:114-146``: preset replay,
     11-point available-worker sweep, 1000 deterministic decisions per point, batch decision stride 10) for
     (1) a fresh random-init MAT (``torch.manual_seed(1)``, BASELINE.md's random-init row), (2) the trained
-    checkpoint (``--model_dir``, default the committed 32-worker run) and (3) the fixed heuristic.  Independent of
+    checkpoints (``--model_dir``, default ``DEFAULT_CKPT[n_workers]``) and (3) the fixed heuristic.  Independent of
     ``--steps``: the benchmarked runner's weights are never used here."""
     from mat_dcml_amd.algos.policy import TransformerPolicy
     from mat_dcml_amd.envs.dcml.spaces import dcml_action_spaces
@@ -277,28 +281,29 @@ def eval_block(a, args, runner, dev):
     info = {"protocol": "DCML_MAT_ALT_Benchmark.py AW sweep: 11 points x 1000 preset decisions, stride 10, "
                         f"{a.n_workers} workers (available-worker steps scaled to the pool)"}
     info["random_init"] = summary(run_sweep(fresh_policy(), runner.dcml, dev, latency_b1=20, **kw))
-    ckpt = a.model_dir or DEFAULT_CKPT.get(a.n_workers)
-    if ckpt and os.path.exists(ckpt):
+    ckpts = [("trained", a.model_dir)] if a.model_dir else DEFAULT_CKPT.get(a.n_workers, [])
+    for key, ckpt in ckpts:
+        if not (ckpt and os.path.exists(ckpt)):
+            continue
         pol = fresh_policy()
         pol.restore(ckpt)
-        info["trained"] = summary(run_sweep(pol, runner.dcml, dev, latency_b1=20, **kw))
-        info["trained"]["checkpoint"] = ckpt
+        ent = info[key] = summary(run_sweep(pol, runner.dcml, dev, latency_b1=20 if key == "trained" else 0, **kw))
+        ent["checkpoint"] = ckpt
         # held-out preset sets (Sample_2..10, which the reference benchmark never reads) and, on Sample_1, where each
         # point lies against the heuristic's own ct-payment trade-off (K = floor(rho N), rho = 0.3 .. 1.0)
         rep = eval_report(pol, runner.dcml, dev, **{k: v for k, v in kw.items() if k != "verbose"})
-        info["trained"]["wins_vs_fixed_sample1"] = {k: rep["per_sample"][1][k]
-                                                    for k in ("ct_wins", "payment_wins", "both_wins")}
-        info["trained"]["heldout"] = rep.get("heldout")
+        ent["wins_vs_fixed_sample1"] = {k: rep["per_sample"][1][k] for k in ("ct_wins", "payment_wins", "both_wins")}
+        ent["heldout"] = rep.get("heldout")
         fr = rep.get("frontier") or []
-        info["trained"]["frontier"] = {"ratios": rep.get("frontier_ratios"),
-                                       "beyond_per_point": [f["beyond"] for f in fr],
-                                       "dominated_by_per_point": [f["dominated_by"] for f in fr],
-                                       "payment_margin_per_point": [f["margin"] for f in fr],
-                                       "outside_per_point": [f["outside"] for f in fr],
-                                       "dominates_per_point": [f["dominates"] for f in fr],
-                                       # only numeric positive margins count; points faster than every
-                                       # heuristic setting are counted apart, with no verdict
-                                       **{k + "_count": v for k, v in frontier_counts(fr).items()}}
+        ent["frontier"] = {"ratios": rep.get("frontier_ratios"),
+                           "beyond_per_point": [f["beyond"] for f in fr],
+                           "dominated_by_per_point": [f["dominated_by"] for f in fr],
+                           "payment_margin_per_point": [f["margin"] for f in fr],
+                           "outside_per_point": [f["outside"] for f in fr],
+                           "dominates_per_point": [f["dominates"] for f in fr],
+                           # only numeric positive margins count; points faster than every heuristic
+                           # setting are counted apart, with no verdict
+                           **{k + "_count": v for k, v in frontier_counts(fr).items()}}
     info["fixed_heuristic"] = summary(run_sweep(None, runner.dcml, dev, fixed=True, latency_b1=0, **kw))
     return info
 
