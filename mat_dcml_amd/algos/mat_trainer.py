@@ -39,6 +39,33 @@ def mse_loss(e):
     return e ** 2 / 2
 
 
+class _GatherAhead:
+    """``kernels.gather_rows`` of the next minibatch on a side stream: started after the current minibatch's backward
+    kernels are queued (it waits for them, so it never competes with the persistent training kernels for CUs) and
+    overlapped with that minibatch's workspace reduction + Adam / repack launches; ``take()`` makes the main stream
+    wait for it.  Same rows, same arithmetic as the in-line gather: the training step is unchanged bit for bit."""
+    _side = {}
+
+    def __init__(self, src, idx, sums):
+        main = torch.cuda.current_stream()
+        side = _GatherAhead._side.get(main.device)
+        if side is None:
+            side = _GatherAhead._side[main.device] = torch.cuda.Stream(main.device)
+        ready = torch.cuda.Event()
+        ready.record(main)
+        side.wait_event(ready)
+        with torch.cuda.stream(side):
+            self.mb = kernels.gather_rows(src, idx, sums, ("adv",))
+        self.done = torch.cuda.Event()
+        self.done.record(side)
+        for t in self.mb.values():   # allocated on the side stream, consumed on the main one
+            t.record_stream(main)
+
+    def take(self):
+        torch.cuda.current_stream().wait_event(self.done)
+        return self.mb
+
+
 class MATTrainer:
     def __init__(self, args, policy, num_agents, device=torch.device("cpu"), comm=None):
         self.device = torch.device(device)
@@ -120,6 +147,11 @@ class MATTrainer:
         self.deterministic = mode == "private" and copies > 0 and not self._direct_grads
         self._upd_fused = (mode == "private" and copies > 0 and self.comm.world_size == 1
                            and os.environ.get("MAT_DCML_FUSED_UPDATE", "1") != "0")
+        # opt-in (MAT_DCML_GATHER_AHEAD=1): the next minibatch's gather on a side stream, overlapped with this
+        # minibatch's reduction + Adam launches.  Measured a LOSS at the bench shape (165.1k / 165.3k vs 171.6k /
+        # 170.9k env-steps/s, profiles/r6_ab/README.md): the gather contends with the bandwidth-bound workspace
+        # reduction (20 us instead of 11) and the cross-stream event waits add latency to every minibatch
+        self.gather_ahead = self.device.type == "cuda" and os.environ.get("MAT_DCML_GATHER_AHEAD", "0") == "1"
         # the reference's cuda_deterministic (store_false: ON unless --cuda_deterministic is passed,
         # DCML_MAT_Train.py:108-110): the fused trainer's PPO update is bit-reproducible with the private gradient
         # workspace (tests/test_gpu_determinism.py); wide observations keep fp32 atomics in their embedding backward
@@ -205,7 +237,10 @@ class MATTrainer:
         mat_fused.bump_version(pol.transformer)
         return value_loss.detach(), grad_norm.detach(), policy_loss.detach(), entropy.detach(), imp.detach().mean()
 
-    def ppo_update_fused(self, mb, pre_stats=None):
+    def ppo_update_fused(self, mb, pre_stats=None, prefetch=None):
+        """One fused PPO minibatch step.  ``prefetch``: a callable started once the backward kernels are queued (the
+        next minibatch's gather on the side stream, under this minibatch's gradient reduction and Adam launches); its
+        result is returned."""
         from ..ops import mat_train
         pol = self.policy
         m = pol.transformer
@@ -229,6 +264,7 @@ class MATTrainer:
                 work = self.comm.all_reduce_sum_async(buf[lo:hi], grad=True)
             enc.backward(drep, dv)
         m._mdl_gws_active = False
+        ahead = prefetch() if prefetch is not None else None
         if split is not None:
             for lo, hi in split[3]:
                 mat_train.reduce_grad_workspace(m, lo, hi, accumulate=self._direct_grads, last=(lo, hi) == split[3][-1])
@@ -237,7 +273,7 @@ class MATTrainer:
             self._finish_overlap(buf, work, split[3])
             pol.optimizer.step(norm_ready=False)
             mat_fused.bump_version(m)
-            return pol.optimizer.grad_norm
+            return ahead
         # one process: the workspace reduction also leaves the optimizer's Σ g² partials of the final gradient (no
         # norm launch); under data parallelism the norm is the all-reduced gradient's, so the Adam step computes it
         fuse_norm = self.comm.world_size == 1 and not self.poison
@@ -248,7 +284,7 @@ class MATTrainer:
             enc.ctx = None
             mat_fused.bump_version(m)
             mat_train.mark_packs_current(m)
-            return pol.optimizer.grad_norm
+            return ahead
         norm_ready = mat_train.reduce_grad_workspace(m, norm_into=pol.optimizer.scratch if fuse_norm else None,
                                                      accumulate=self._direct_grads)
         dec.ctx = None
@@ -263,7 +299,7 @@ class MATTrainer:
             self.collectives += 1
         pol.optimizer.step(norm_ready=norm_ready)
         mat_fused.bump_version(m)
-        return pol.optimizer.grad_norm
+        return ahead
 
     # ------------------------------------------------------------------------------------------------
     def _overlap_split(self):
@@ -371,10 +407,14 @@ class MATTrainer:
             else:
                 adv = rl_ops.normalize_from_sums(buffer.advantages, sums)
                 adv_f = adv.reshape(T * E, *adv.shape[2:])
+            src = {"obs": obs_f, "actions": act_f, "ava": ava_f, "old_logp": lp_f, "value_preds": vp_f,
+                   "returns": ret_f, "active": am_f, "adv": adv_f}
+            ahead = None   # the next minibatch, gathered on the side stream under this one's update
             for m, idx in enumerate(idx_list):
-                src = {"obs": obs_f, "actions": act_f, "ava": ava_f, "old_logp": lp_f, "value_preds": vp_f,
-                       "returns": ret_f, "active": am_f, "adv": adv_f}
-                if native and len(idx_list) == 1 and getattr(self, "inplace_single_minibatch", True):
+                if ahead is not None:
+                    mb = ahead.take()
+                    ahead = None
+                elif native and len(idx_list) == 1 and getattr(self, "inplace_single_minibatch", True):
                     # one minibatch = the whole batch: the permutation only reorders the rows the loss averages
                     # over, so the buffer's rows are used in place (SMAC: no 2 x 445 MB gather copy per epoch);
                     # the loss kernel standardises the advantages itself (adv_sums)
@@ -390,7 +430,10 @@ class MATTrainer:
                 else:
                     mb = {k: v[idx] for k, v in src.items()}
                 if self.fused:
-                    self.ppo_update_fused(mb, None if pre is None else pre[m])   # norm summed in the Adam kernel
+                    nxt = None
+                    if native and self.gather_ahead and m + 1 < len(idx_list) and "idx" not in mb:
+                        nxt = lambda i=idx_list[m + 1]: _GatherAhead(src, i, sums)   # noqa: E731
+                    ahead = self.ppo_update_fused(mb, None if pre is None else pre[m], prefetch=nxt)
                     continue
                 self._vn_pre = None if pre is None else (pre[m, :n_obj], pre[m, n_obj:2 * n_obj], pre[m, 2 * n_obj])
                 vl, gn, pl, ent, ratio = self.ppo_update(mb)

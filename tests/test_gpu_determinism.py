@@ -91,11 +91,12 @@ def test_fused_training_repeatable(gpu):
     print(f"max relative run-to-run gradient deviation (fp32 atomic order): {worst:.2e}")
 
 
-def _ppo_run(gpu, iters=2, fused_update=True, mb_index="gather"):
+def _ppo_run(gpu, iters=2, fused_update=True, mb_index="gather", gather_ahead=True):
     from mat_dcml_amd.config import get_config, parse_args
     from mat_dcml_amd.parallel.comm import Comm
     from mat_dcml_amd.runner.dcml_runner import DCMLRunner
-    env = {"MAT_DCML_FUSED_UPDATE": "1" if fused_update else "0", "MAT_DCML_MB_INDEX": mb_index}
+    env = {"MAT_DCML_FUSED_UPDATE": "1" if fused_update else "0", "MAT_DCML_MB_INDEX": mb_index,
+           "MAT_DCML_GATHER_AHEAD": "1" if gather_ahead else "0"}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -104,7 +105,7 @@ def _ppo_run(gpu, iters=2, fused_update=True, mb_index="gather"):
                           get_config(), warn=False)
         r = DCMLRunner({"all_args": args, "device": gpu, "run_dir": None, "comm": Comm(device=gpu)})
         tr = r.trainer
-        assert tr.fused and tr.deterministic and tr._upd_fused == fused_update
+        assert tr.fused and tr.deterministic and tr._upd_fused == fused_update and tr.gather_ahead == gather_ahead
         r.warmup()
         for _ in range(iters):
             r.train_iteration()
@@ -149,3 +150,11 @@ def test_kernel_minibatch_index_matches_gather(gpu):
     dm = ((a["exp_avg"] - b["exp_avg"]).norm() / b["exp_avg"].norm()).item()
     print(f"in-kernel minibatch index vs gather: relative parameter difference {d:.2e}, first moment {dm:.2e}")
     assert d < 1e-5 and dm < 1e-3, (d, dm)
+
+
+def test_gather_ahead_is_bitwise_neutral(gpu):
+    """The next minibatch's gather on the side stream (algos/mat_trainer._GatherAhead) against the in-line gather:
+    the same rows and arithmetic, only the stream differs, so parameters and Adam moments are bitwise equal."""
+    a, b = _ppo_run(gpu, gather_ahead=True), _ppo_run(gpu, gather_ahead=False)
+    for k in a:
+        assert torch.equal(a[k], b[k]), (k, (a[k] - b[k]).abs().max().item())
