@@ -478,8 +478,18 @@ __device__ __forceinline__ void head_fwd_ct(const DecP& p, const CT* xr, bool sa
   }
 }
 
+// LDS vector slots of the small weight gradients (wgrad_g_vacc): d W_a (A+1 slots), d W_h2 (A slots), d b_h2 (1), after
+// the 5 + 6 NB LayerNorm / log_std slots; -1 when they do not fit (A > 2 or NB = 3: per-chunk private / atomic flush)
+#ifndef MDL_SMALL_WG_VACC
+#define MDL_SMALL_WG_VACC 1
+#endif
+__device__ __forceinline__ int small_wg_slot0(const DecP& p, int NB) {
+  const int s0 = 5 + 6 * NB;
+  return (MDL_SMALL_WG_VACC && p.A <= 2 && s0 + 2 * p.A + 2 <= VSLOTS) ? s0 : -1;
+}
+
 template <int MA, bool CONT>
-__device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c) {
+__device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c, int vs0) {
   const int lane = c.lane, g = lane >> 4;
   constexpr int SB = (MA + 1) / 2;   // k-steps over the logit axis in dn = W_h2ᵀ dz
   CT dlg, dlb;
@@ -648,7 +658,10 @@ __device__ __forceinline__ void head_bwd_ct(const DecP& p, CT* dx, const Ctx& c)
   }
   __syncthreads();
   CP_MARK(1);
-  wgrad_g(c.DA, c.XB, c.KP, c.g(p.d_wh2), 64, p.A, 64, c.g(p.d_bh2), c.wave, lane, c.gm);
+  if (vs0 >= 0)   // slots vs0 + A + 1 .. (W_h2 rows), vs0 + 2A + 1 (bias)
+    wgrad_g_vacc(c.DA, c.XB, c.KP, c.g(p.d_wh2), 64, p.A, 64, c.g(p.d_bh2), vs0 + p.A + 1, vs0 + 2 * p.A + 1, c);
+  else
+    wgrad_g(c.DA, c.XB, c.KP, c.g(p.d_wh2), 64, p.A, 64, c.g(p.d_bh2), c.wave, lane, c.gm);
   wgrad64(c.DQ, c.KB, p.h1, c);
   __syncthreads();
   CP_MARK(19);
@@ -727,14 +740,15 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
   CP_MARK(0);
   const int lane = c.lane;
   CT dx[MAXRT];
-  head_bwd_ct<MA, CONT>(p, dx, c);
+  const int vs0 = small_wg_slot0(p, NB);
+  head_bwd_ct<MA, CONT>(p, dx, c, vs0);
 #pragma unroll 1
   for (int bb = NB - 1; bb >= 0; --bb) {
     const Blk& B = p.blk[bb];
     Ctx cc = c;
     asm volatile("" : "+v"(cc.lane), "+v"(cc.tid));
     // parameter-vector slots (vacc): 0-1 head LayerNorm, 2-3 embedding LayerNorm, 4 log_std, 5 + 6 bb + 2 k the
-    // block's k-th LayerNorm (gamma, beta)
+    // block's k-th LayerNorm (gamma, beta); then the small weight gradients from vs0 (small_wg_slot0)
     mlp_bwd_ct(B.m[8], B.m[9], B.ln[2], dx, p.sv[bb].x2, p.sv[bb].g, p.sv[bb].gp, p.sv[bb].xh[2], p.sv[bb].rs + 2 * (size_t)p.Bs * p.L, cc,
                9 + 6 * bb);
     cross_attn_bwd_ct(B.m, B.ln[1], dx, p.rep, p.drep, p.sv[bb].x1, p.sv[bb].a2, p.sv[bb].a2lo, p.sv[bb].lse2,
@@ -801,9 +815,10 @@ __device__ __forceinline__ void dec_bwd_tile(const DecP& p, char* smem, int seq0
     flush_vec(dlb, c.g(p.d_lnd_b), 3, c);
     __syncthreads();
     if (p.d_wa) {
-      wgrad_g(c.DA, c.XB, c.KP, c.g(p.d_wa), p.A + 1, 64, p.A + 1, nullptr, c.wave, lane, c.gm);
-      // the lo half adds onto the hi half's flush (private copies: same lanes, same addresses, program order)
-      wgrad_g(c.DQ, c.XB, c.KP, c.g(p.d_wa), p.A + 1, 64, p.A + 1, nullptr, c.wave, lane, GradMode{c.gm.priv, false});
+      // hi and lo halves of d pre in one pass: one flush (LDS slots vs0 .. vs0 + A, or one read-modify-write of a
+      // private copy per chunk)
+      if (vs0 >= 0) wgrad_g_vacc(c.DA, c.XB, c.KP, c.g(p.d_wa), p.A + 1, 64, p.A + 1, nullptr, vs0, -1, c, c.DQ);
+      else wgrad_g(c.DA, c.XB, c.KP, c.g(p.d_wa), p.A + 1, 64, p.A + 1, nullptr, c.wave, lane, c.gm, c.DQ);
     }
   } else {
     float* EMB = (float*)c.QB;   // [(A+1)][64] f32 accumulators (QB + KB: 2 NRP x 128 B >= 65 x 256 B)

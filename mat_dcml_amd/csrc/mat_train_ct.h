@@ -524,8 +524,11 @@ __device__ __forceinline__ f32x4* frag_slot(float* dW, int wave, int lane, int j
 // and so one Y fragment per k-step.  The bias gradient is one extra MFMA per k-step against a ones fragment (the
 // waves holding column tile 0).  Shared workspace copies: fp32 atomics; private copies (GradMode): row-major
 // stores, or load + add + store after the workgroup's first chunk (loads issued before the MFMA loop).
+// Y2 (optional): a second dY tile added in the same pass (the lo half of a hi / lo split dY) — one flush instead of
+// two, so a private copy is read-modified-written once per chunk (two passes made the second pass's loads wait for
+// the first pass's stores to the same addresses: ~6 us per chunk in the decoder's embedding backward)
 __device__ __forceinline__ void wgrad_g(const bf16_t* Y, const bf16_t* X, int KP, float* dW, int ld, int nrows, int ncols,
-                                        float* db, int wave, int lane, GradMode gm) {
+                                        float* db, int wave, int lane, GradMode gm, const bf16_t* Y2 = nullptr) {
   static_assert(NW % 4 == 0, "row block per wave");
   constexpr int NCT = (16 + NW - 1) / NW;           // column tiles per wave (at most)
   const int rb = wave & 3;
@@ -555,12 +558,15 @@ __device__ __forceinline__ void wgrad_g(const bf16_t* Y, const bf16_t* X, int KP
   const bf16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
   for (int k0 = 0; k0 < KP; k0 += 32) {
     const bf16x8 a = ld_frag_T(Y, k0, 16 * rb, lane);
+    bf16x8 a2;
+    if (Y2) a2 = ld_frag_T(Y2, k0, 16 * rb, lane);
 #pragma unroll
     for (int j = 0; j < NCT; ++j) {
       const int ct = wg_ct(wave, j);
       if (wg_has(wave, j) && ct < nct) {
         const bf16x8 b = ld_frag_T(X, k0, 16 * ct, lane);
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[j], 0, 0, 0);
+        if (Y2) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, b, acc[j], 0, 0, 0);
       }
     }
     if (db) accb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ones, accb, 0, 0, 0);
@@ -596,6 +602,64 @@ __device__ __forceinline__ void wgrad_g(const bf16_t* Y, const bf16_t* X, int KP
       if (gm.priv) priv_st1(db + n, v, oldb, gm.first);
       else atomicAdd(db + n, v);
     }
+  }
+}
+
+// The same product for a SMALL gradient (nrows x ld <= 64 (slot_end - slot0) floats: the decoder's action embedding
+// 64 x (A+1) and action head A x 64 for A <= 2), accumulated in the workgroup's LDS vector slots (vacc_add: 2^-32
+// fixed point, order-free) across all of its chunks and flushed once per launch (vacc_end): no global traffic per
+// chunk.  A private copy's per-chunk read-modify-write here stalled the decoder backward: the loads wait for the
+// previous chunk's stores in the in-order vector-memory counter (head + embedding backward 22 % of dec_bwd vs 14 % with
+// atomics).  dW rows are ld floats apart (ld >= ncols, row-major, contiguous: slot s = element e / 64); the bias
+// gradient db (nrows floats) takes slot bslot.
+__device__ __forceinline__ void wgrad_g_vacc(const bf16_t* Y, const bf16_t* X, int KP, float* dW, int ld, int nrows,
+                                             int ncols, float* db, int slot0, int bslot, const Ctx& c,
+                                             const bf16_t* Y2 = nullptr) {
+  constexpr int NCT = (16 + NW - 1) / NW;
+  const int wave = c.wave, lane = c.lane, rb = wave & 3;
+  if (wave >= 4) db = nullptr;
+  const int nct = dW ? (ncols + 15) >> 4 : 0;
+  if ((!db && wg_ct(wave, 0) >= nct) || 16 * rb >= nrows) return;
+  const int g = lane >> 4, c16 = lane & 15;
+  f32x4 acc[NCT];
+#pragma unroll
+  for (int j = 0; j < NCT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 accb = {0.f, 0.f, 0.f, 0.f};
+  const bf16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
+  for (int k0 = 0; k0 < KP; k0 += 32) {
+    const bf16x8 a = ld_frag_T(Y, k0, 16 * rb, lane);
+    bf16x8 a2;
+    if (Y2) a2 = ld_frag_T(Y2, k0, 16 * rb, lane);
+#pragma unroll
+    for (int j = 0; j < NCT; ++j) {
+      const int ct = wg_ct(wave, j);
+      if (wg_has(wave, j) && ct < nct) {
+        const bf16x8 b = ld_frag_T(X, k0, 16 * ct, lane);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[j], 0, 0, 0);
+        if (Y2) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, b, acc[j], 0, 0, 0);
+      }
+    }
+    if (db) accb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ones, accb, 0, 0, 0);
+  }
+  const int total = nrows * ld;
+  if (dW) {
+#pragma unroll
+    for (int j = 0; j < NCT; ++j) {
+      const int ct = wg_ct(wave, j);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = 16 * rb + 4 * g + r, k = 16 * ct + c16, e = n * ld + k;
+        if (wg_has(wave, j) && ct < nct && n < nrows && k < ncols) {
+          const int s = e >> 6, len = total - 64 * s;
+          vacc_add(dW + 64 * s, slot0 + s, e & 63, acc[j][r], c, len < 64 ? len : 64);
+        }
+      }
+    }
+  }
+  if (db && c16 < 4) {
+    const float v = c16 == 0 ? accb[0] : c16 == 1 ? accb[1] : c16 == 2 ? accb[2] : accb[3];
+    const int n = 16 * rb + 4 * g + c16;
+    if (n < nrows) vacc_add(db, bslot, n, v, c, nrows);
   }
 }
 
