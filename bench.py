@@ -236,6 +236,8 @@ def _grad_path(tr, n):
     return {"workspace": getattr(m, "_mdl_gws_mode", None), "fused_update": bool(getattr(tr, "_upd_fused", False)),
             "minibatch_inputs": ("in-kernel index" if os.environ.get("MAT_DCML_MB_INDEX", "gather") == "kernel" else
                                  "gather" + (" (next minibatch's on a side stream)" if getattr(tr, "gather_ahead", False)
+                                             else " (next minibatch's inside the update launch)"
+                                             if getattr(tr, "fused_gather", False) and getattr(tr, "_upd_fused", False)
                                              else "")),
             "allreduce": None if n == 1 else ("overlap(decoder slice under enc_bwd)" if tr.grad_overlap else
                                               f"single blocking ({getattr(tr, 'grad_allreduce', 'rccl')})")}

@@ -152,6 +152,9 @@ class MATTrainer:
         # 170.9k env-steps/s, profiles/r6_ab/README.md): the gather contends with the bandwidth-bound workspace
         # reduction (20 us instead of 11) and the cross-stream event waits add latency to every minibatch
         self.gather_ahead = self.device.type == "cuda" and os.environ.get("MAT_DCML_GATHER_AHEAD", "0") == "1"
+        # the next minibatch's gather inside the fused update's adam_pack launch (extra workgroups next to the Adam
+        # ones, which leave most CUs idle): one launch fewer per minibatch after an epoch's first
+        self.fused_gather = self.device.type == "cuda" and os.environ.get("MAT_DCML_FUSED_GATHER", "1") != "0"
         # the reference's cuda_deterministic (store_false: ON unless --cuda_deterministic is passed,
         # DCML_MAT_Train.py:108-110): the fused trainer's PPO update is bit-reproducible with the private gradient
         # workspace (tests/test_gpu_determinism.py); wide observations keep fp32 atomics in their embedding backward
@@ -237,10 +240,11 @@ class MATTrainer:
         mat_fused.bump_version(pol.transformer)
         return value_loss.detach(), grad_norm.detach(), policy_loss.detach(), entropy.detach(), imp.detach().mean()
 
-    def ppo_update_fused(self, mb, pre_stats=None, prefetch=None):
-        """One fused PPO minibatch step.  ``prefetch``: a callable started once the backward kernels are queued (the
-        next minibatch's gather on the side stream, under this minibatch's gradient reduction and Adam launches); its
-        result is returned."""
+    def ppo_update_fused(self, mb, pre_stats=None, ahead=None):
+        """One fused PPO minibatch step.  ``ahead`` = (sources, row index, advantage sums) of the NEXT minibatch: its
+        gather is issued with this minibatch's update — inside the fused update's adam_pack launch (default), on a
+        side stream (``gather_ahead``, opt-in), or as its own launch after the update — and returned (a dict, or a
+        ``_GatherAhead`` to ``take()``)."""
         from ..ops import mat_train
         pol = self.policy
         m = pol.transformer
@@ -264,7 +268,7 @@ class MATTrainer:
                 work = self.comm.all_reduce_sum_async(buf[lo:hi], grad=True)
             enc.backward(drep, dv)
         m._mdl_gws_active = False
-        ahead = prefetch() if prefetch is not None else None
+        nxt = _GatherAhead(*ahead) if ahead is not None and self.gather_ahead else None
         if split is not None:
             for lo, hi in split[3]:
                 mat_train.reduce_grad_workspace(m, lo, hi, accumulate=self._direct_grads, last=(lo, hi) == split[3][-1])
@@ -273,18 +277,22 @@ class MATTrainer:
             self._finish_overlap(buf, work, split[3])
             pol.optimizer.step(norm_ready=False)
             mat_fused.bump_version(m)
-            return ahead
+            return nxt if nxt is not None or ahead is None else kernels.gather_rows(*ahead, ("adv",))
         # one process: the workspace reduction also leaves the optimizer's Σ g² partials of the final gradient (no
         # norm launch); under data parallelism the norm is the all-reduced gradient's, so the Adam step computes it
         fuse_norm = self.comm.world_size == 1 and not self.poison
         if fuse_norm and self._upd_fused:
             # round 6: workspace reduction, then clip + Adam + weight repack: two launches (csrc/ppo.hip)
-            mat_train.update_fused(m, pol.optimizer, accumulate=self._direct_grads)
+            ga = None
+            if ahead is not None and nxt is None and self.fused_gather and \
+                    all(t[0].numel() <= 1024 for t in ahead[0].values()):
+                ga, nxt = kernels.gather_args(*ahead, ("adv",))   # rows gathered by the adam_pack launch
+            mat_train.update_fused(m, pol.optimizer, accumulate=self._direct_grads, gather=ga)
             dec.ctx = None
             enc.ctx = None
             mat_fused.bump_version(m)
             mat_train.mark_packs_current(m)
-            return ahead
+            return nxt if nxt is not None or ahead is None else kernels.gather_rows(*ahead, ("adv",))
         norm_ready = mat_train.reduce_grad_workspace(m, norm_into=pol.optimizer.scratch if fuse_norm else None,
                                                      accumulate=self._direct_grads)
         dec.ctx = None
@@ -299,7 +307,7 @@ class MATTrainer:
             self.collectives += 1
         pol.optimizer.step(norm_ready=norm_ready)
         mat_fused.bump_version(m)
-        return ahead
+        return nxt if nxt is not None or ahead is None else kernels.gather_rows(*ahead, ("adv",))
 
     # ------------------------------------------------------------------------------------------------
     def _overlap_split(self):
@@ -409,10 +417,10 @@ class MATTrainer:
                 adv_f = adv.reshape(T * E, *adv.shape[2:])
             src = {"obs": obs_f, "actions": act_f, "ava": ava_f, "old_logp": lp_f, "value_preds": vp_f,
                    "returns": ret_f, "active": am_f, "adv": adv_f}
-            ahead = None   # the next minibatch, gathered on the side stream under this one's update
+            ahead = None   # the next minibatch, gathered during this one's update (fused launch or side stream)
             for m, idx in enumerate(idx_list):
                 if ahead is not None:
-                    mb = ahead.take()
+                    mb = ahead.take() if isinstance(ahead, _GatherAhead) else ahead
                     ahead = None
                 elif native and len(idx_list) == 1 and getattr(self, "inplace_single_minibatch", True):
                     # one minibatch = the whole batch: the permutation only reorders the rows the loss averages
@@ -431,9 +439,9 @@ class MATTrainer:
                     mb = {k: v[idx] for k, v in src.items()}
                 if self.fused:
                     nxt = None
-                    if native and self.gather_ahead and m + 1 < len(idx_list) and "idx" not in mb:
-                        nxt = lambda i=idx_list[m + 1]: _GatherAhead(src, i, sums)   # noqa: E731
-                    ahead = self.ppo_update_fused(mb, None if pre is None else pre[m], prefetch=nxt)
+                    if native and m + 1 < len(idx_list) and "idx" not in mb and (self.gather_ahead or self.fused_gather):
+                        nxt = (src, idx_list[m + 1], sums)
+                    ahead = self.ppo_update_fused(mb, None if pre is None else pre[m], ahead=nxt)
                     continue
                 self._vn_pre = None if pre is None else (pre[m, :n_obj], pre[m, n_obj:2 * n_obj], pre[m, 2 * n_obj])
                 vl, gn, pl, ent, ratio = self.ppo_update(mb)

@@ -13,6 +13,7 @@
 //   and one Adam update over the flat fp32 parameter / gradient / moment buffers (torch.optim.Adam maths,
 //   L2 weight decay added to the gradient).
 #include "common.h"
+#include "gather_rows.h"
 
 using namespace mdl;
 
@@ -520,6 +521,8 @@ struct UpdArgs {
   const PackEntU* tab; const int* mat_off; int nmat;   // packed matrices and their flat offsets
   const int* rest; int n_rest;                         // flat indices of every other parameter element
   unsigned int* bar;                                   // (unused: the one-launch variant's barrier words)
+  GatherArgs ga;   // the NEXT minibatch's gather (ga.n = 0: none), run by extra workgroups of the adam_pack launch
+  int ga_wg;       // their count
 };
 
 __device__ __forceinline__ float adam_elem(const AdamArgs& a, int i, float scale, float ib1, float ib2) {
@@ -538,6 +541,13 @@ __device__ __forceinline__ float adam_elem(const AdamArgs& a, int i, float scale
 __global__ __launch_bounds__(1024) void adam_pack_kernel(UpdArgs u) {
   __shared__ float snorm;
   __shared__ float Mf[4096];
+  const int base = (int)gridDim.x - u.ga_wg;
+  if ((int)blockIdx.x >= base) {   // the next minibatch's rows: independent of this update (and of its finite check)
+    const int wpb = blockDim.x >> 6;
+    gather_rows_wavewise(u.ga, ((int)blockIdx.x - base) * wpb + (int)(threadIdx.x >> 6), u.ga_wg * wpb,
+                         threadIdx.x & 63);
+    return;
+  }
   const AdamArgs& a = u.a;
   if (threadIdx.x < 64) {   // Σ of the ADAM_NB partials of grad_reduce_priv, fixed order
     float v = 0.f;
@@ -574,7 +584,7 @@ __global__ __launch_bounds__(1024) void adam_pack_kernel(UpdArgs u) {
       if (pe.ba) pe.ba[idx] = mdl::f2bf(Mf[kp * 64 + n]);
     }
   } else {
-    const int nb = gridDim.x - u.nmat;
+    const int nb = base - u.nmat;
     for (int r = (blockIdx.x - u.nmat) * blockDim.x + threadIdx.x; r < u.n_rest; r += nb * blockDim.x)
       adam_elem(a, u.rest[r], scale, ib1, ib2);
   }
@@ -582,11 +592,20 @@ __global__ __launch_bounds__(1024) void adam_pack_kernel(UpdArgs u) {
 
 MDL_API int mdl_update_fused(const UpdArgs* u, hipStream_t st) {
   if (u->copies < 1 || u->nmat < 0 || u->n_rest < 0 || (u->n & 3) || (u->stride & 3)) return -1;
-  hipLaunchKernelGGL(grad_reduce_priv_kernel, dim3(ADAM_NB), dim3(256), 0, st, u->g, u->ws, u->dst, 0, u->n, u->stride,
-                     u->copies, u->accumulate, u->a.sumsq);
+  UpdArgs v = *u;
+  v.ga_wg = 0;
+  if (v.ga.n > 0 && v.ga.rows > 0) {   // the next minibatch's gather: one wave per (entry, row) item, <= 384 WGs
+    if (const int rc = gather_check(v.ga)) return rc;
+    for (int k = 0; k < v.ga.n; ++k)
+      if (v.ga.e[k].width > 1024) return -3;   // wide rows: the standalone gather (gather_rows_kernel)
+    const int items = v.ga.n * v.ga.rows;
+    v.ga_wg = (items + 15) / 16 < 384 ? (items + 15) / 16 : 384;
+  }
+  hipLaunchKernelGGL(grad_reduce_priv_kernel, dim3(ADAM_NB), dim3(256), 0, st, v.g, v.ws, v.dst, 0, v.n, v.stride,
+                     v.copies, v.accumulate, v.a.sumsq);
   MDL_CHECK_LAUNCH();
-  const int rest_wg = (u->n_rest + 1023) / 1024;   // 1024-thread workgroups: a matrix's 4096 elements in 4 steps
-  hipLaunchKernelGGL(adam_pack_kernel, dim3(u->nmat + (rest_wg < 64 ? rest_wg : 64)), dim3(1024), 0, st, *u);
+  const int rest_wg = (v.n_rest + 1023) / 1024;   // 1024-thread workgroups: a matrix's 4096 elements in 4 steps
+  hipLaunchKernelGGL(adam_pack_kernel, dim3(v.nmat + (rest_wg < 64 ? rest_wg : 64) + v.ga_wg), dim3(1024), 0, st, v);
   MDL_CHECK_LAUNCH();
   return 0;
 }

@@ -7,6 +7,7 @@
 // (mo_shared_buffer.py / dmo_shared_buffer.py keep one mask per agent).  Loads of step t are independent of the
 // recurrence, so the compiler can issue them ahead (T is 50).
 #include "common.h"
+#include "gather_rows.h"
 
 __global__ __launch_bounds__(256) void gae_reverse_scan_kernel(
     const float* __restrict__ rew, const float* __restrict__ vpred, const float* __restrict__ masks,
@@ -308,88 +309,17 @@ MDL_API int mdl_mb_stats(const float* ret, const float* active, const int64_t* p
   return 0;
 }
 
-// gather_rows: dst_k[r, :] = src_k[idx[r], :] for up to 10 row-major fp32 tensors in ONE launch (blockIdx.y = k);
-// entries flagged `norm` are standardised on the fly with the masked_sums statistics:
-// (x - mean) / (std + eps), std the population std — the normalised advantage of the reference, computed only for
-// the rows a minibatch actually reads.
-constexpr int GATHER_MAX = 10;
-constexpr int GATHER_CHUNK = 4096;   // floats per work item (a multiple of 1024)
-struct GatherEnt { const float* src; float* dst; int width; int norm; };
-struct GatherArgs { GatherEnt e[GATHER_MAX]; const int64_t* idx; const double* sums; int rows; int n; float eps; };
-
-// Row-parallel gather: workgroup (x, entry y) copies rows x, x + gridDim.x, ... of entry y — float4 per lane when
-// the row width and both bases allow it (SMAC's obs rows are 27 x 1288 floats: the round-2 flat loop with one
-// integer division per element ran at ~0.2 TB/s), floats otherwise (DCML's 33 x 7).
+// gather_rows (csrc/gather_rows.h): one launch gathers a minibatch's rows of up to GATHER_MAX tensors (blockIdx.y =
+// the entry) and standardises the flagged ones (the advantages) on the fly.  The same body also runs inside the fused
+// update's adam_pack launch for the next minibatch (csrc/ppo.hip).
 __global__ __launch_bounds__(256) void gather_rows_kernel(GatherArgs a) {
-  const GatherEnt e = a.e[blockIdx.y];
-  float mean = 0.f, sd = 1.f;
-  if (e.norm) {
-    const double cnt = a.sums[2] < 1.0 ? 1.0 : a.sums[2];
-    const double m = a.sums[0] / cnt;
-    double var = a.sums[1] / cnt - m * m;
-    var = var < 0.0 ? 0.0 : var;
-    mean = (float)m;
-    sd = (float)sqrt(var) + a.eps;
-  }
-  const int w = e.width;
-  if (w < 1024) {   // narrow rows (DCML: 33 x 7): one flat element loop over the whole minibatch (coalesced across rows)
-    const int total = a.rows * w;
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
-      const int r = i / w, c = i - r * w;
-      float v = e.src[(size_t)a.idx[r] * w + c];
-      if (e.norm) v = (v - mean) / sd;
-      e.dst[i] = v;
-    }
-    return;
-  }
-  const bool vec = (w & 3) == 0 && ((reinterpret_cast<uintptr_t>(e.src) | reinterpret_cast<uintptr_t>(e.dst)) & 15) == 0;
-  // work item = (row, 4096-float chunk of the row): 16 floats per lane, the 4 float4 loads issued before the stores
-  const int nch = (w + GATHER_CHUNK - 1) / GATHER_CHUNK;
-  for (int item = blockIdx.x; item < a.rows * nch; item += gridDim.x) {
-    const int r = item / nch, c0 = (item - r * nch) * GATHER_CHUNK;
-    const int cn = min(GATHER_CHUNK, w - c0);
-    const float* src = e.src + (size_t)a.idx[r] * w + c0;
-    float* dst = e.dst + (size_t)r * w + c0;
-    if (vec) {
-      const float4* s4 = (const float4*)src;
-      float4* d4 = (float4*)dst;
-      float4 v[GATHER_CHUNK / 1024];
-#pragma unroll
-      for (int j = 0; j < GATHER_CHUNK / 1024; ++j) {
-        const int c = threadIdx.x + 256 * j;
-        v[j] = c < (cn >> 2) ? s4[c] : float4{0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-      for (int j = 0; j < GATHER_CHUNK / 1024; ++j) {
-        const int c = threadIdx.x + 256 * j;
-        if (e.norm) {
-          v[j].x = (v[j].x - mean) / sd; v[j].y = (v[j].y - mean) / sd;
-          v[j].z = (v[j].z - mean) / sd; v[j].w = (v[j].w - mean) / sd;
-        }
-        if (c < (cn >> 2)) d4[c] = v[j];
-      }
-    } else {
-      for (int c = threadIdx.x; c < cn; c += 256) {
-        float v = src[c];
-        if (e.norm) v = (v - mean) / sd;
-        dst[c] = v;
-      }
-    }
-  }
+  gather_entry(a, blockIdx.y, blockIdx.x, gridDim.x);
 }
 
 MDL_API int mdl_gather_rows(const GatherArgs* a, hipStream_t s) {
-  if (a->n < 1 || a->n > GATHER_MAX || a->rows < 0) return -1;
-  for (int k = 0; k < a->n; ++k)
-    if (a->e[k].width < 1 || (long long)a->rows * a->e[k].width >= (1ll << 31)) return -2;
+  if (const int rc = gather_check(*a)) return rc;
   if (a->rows == 0) return 0;
-  long long items = 0;   // wide rows: (row, chunk) items; narrow rows: 256-element blocks of the flat loop
-  for (int k = 0; k < a->n; ++k) {
-    const long long w = a->e[k].width;
-    items = std::max(items, w < 1024 ? ((long long)a->rows * w + 255) / 256 : (long long)a->rows * ((w + GATHER_CHUNK - 1) / GATHER_CHUNK));
-  }
-  const int gx = (int)(items < 1 ? 1 : (items < 8192 ? items : 8192));
-  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)gx, a->n), dim3(256), 0, s, *a);
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)gather_grid_x(*a, 256), a->n), dim3(256), 0, s, *a);
   MDL_CHECK_LAUNCH();
   return 0;
 }

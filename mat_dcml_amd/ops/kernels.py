@@ -311,23 +311,30 @@ class GatherArgs(ctypes.Structure):
 sig("mdl_gather_rows", vp, vp)
 
 
-def gather_rows(srcs, idx, norm_sums=None, norm_keys=(), eps=1e-5):
-    """{name: src (N, …) fp32 contiguous} -> {name: src[idx]} in one launch; entries in ``norm_keys`` are
-    standardised with ``norm_sums`` (from ``masked_sums``) on the fly."""
+def gather_args(srcs, idx, norm_sums=None, norm_keys=(), eps=1e-5):
+    """The GatherArgs of ``gather_rows`` and its freshly allocated outputs (the launch is the caller's: the standalone
+    ``mdl_gather_rows`` or the fused update's adam_pack, csrc/ppo.hip).  The struct keeps raw pointers: the caller
+    holds ``srcs``, ``idx`` and ``norm_sums`` until the launch has run."""
     assert idx.dtype == torch.int64 and idx.is_contiguous() and len(srcs) <= 10
     a = GatherArgs()
-    out, keep = {}, []
+    out = {}
     for k, (name, src) in enumerate(srcs.items()):
         assert src.is_contiguous() and src.dtype == torch.float32
         dst = torch.empty((idx.numel(), *src.shape[1:]), dtype=torch.float32, device=src.device)
         width = src[0].numel()
         a.e[k] = GatherEnt(src.data_ptr(), dst.data_ptr(), width, int(name in norm_keys))
         out[name] = dst
-        keep.append(src)
     if norm_keys:
         assert norm_sums is not None and norm_sums.dtype == torch.float64
     a.idx, a.sums, a.rows, a.n, a.eps = idx.data_ptr(), norm_sums.data_ptr() if norm_sums is not None else 0, \
         idx.numel(), len(srcs), eps
+    return a, out
+
+
+def gather_rows(srcs, idx, norm_sums=None, norm_keys=(), eps=1e-5):
+    """{name: src (N, …) fp32 contiguous} -> {name: src[idx]} in one launch; entries in ``norm_keys`` are
+    standardised with ``norm_sums`` (from ``masked_sums``) on the fly."""
+    a, out = gather_args(srcs, idx, norm_sums, norm_keys, eps)
     check(lib().mdl_gather_rows(ctypes.byref(a), _stream()), "gather_rows")
     return out
 

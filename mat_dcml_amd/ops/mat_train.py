@@ -691,7 +691,8 @@ def reduce_grad_workspace(model, lo=0, hi=None, norm_into=None, accumulate=True,
 class UpdArgs(ctypes.Structure):   # csrc/ppo.hip mdl_update_fused
     _fields_ = [("g", VP), ("ws", VP), ("dst", VP), ("n", ctypes.c_int), ("stride", ctypes.c_longlong),
                 ("copies", ctypes.c_int), ("accumulate", ctypes.c_int), ("a", AdamArgs), ("tab", VP),
-                ("mat_off", VP), ("nmat", ctypes.c_int), ("rest", VP), ("n_rest", ctypes.c_int), ("bar", VP)]
+                ("mat_off", VP), ("nmat", ctypes.c_int), ("rest", VP), ("n_rest", ctypes.c_int), ("bar", VP),
+                ("ga", kernels.GatherArgs), ("ga_wg", ctypes.c_int)]
 
 
 sig("mdl_update_fused", ctypes.POINTER(UpdArgs), VP)
@@ -719,12 +720,14 @@ class _UpdState:
         self.nmat = len(offs)
 
 
-def update_fused(model, opt, accumulate=False):
+def update_fused(model, opt, accumulate=False, gather=None):
     """Single-GPU end of a minibatch in TWO launches (csrc/ppo.hip mdl_update_fused: grad_reduce_priv +
     adam_pack): fold the private gradient workspace into the flat gradient with the Σ g² partials, then clip + Adam
     over every parameter and repack the 64 x 64 linears' bf16 fragments the training kernels read — replacing
     grad_reduce, adam_norm / adam_step and pack_weights (and the memset).  The caller bumps the model version; the
-    ModelPack is marked current (its packs were written here)."""
+    ModelPack is marked current (its packs were written here).
+    ``gather``: a ``kernels.gather_args`` struct — the NEXT minibatch's rows, gathered by extra workgroups of the
+    adam_pack launch (rows <= 1024 floats wide), so the next minibatch starts without a gather launch of its own."""
     st = getattr(model, "_mdl_upd", None)
     if st is None or st.mp is not getattr(model, "_mdl_pack", None):
         st = _UpdState(model, opt)
@@ -738,6 +741,8 @@ def update_fused(model, opt, accumulate=False):
                 copies=grid, accumulate=int(bool(accumulate)), a=opt.next_args(), tab=st.mp.table.data_ptr(),
                 mat_off=st.mat_off.data_ptr(), nmat=st.nmat, rest=st.rest.data_ptr(), n_rest=st.rest.numel(),
                 bar=st.bar.data_ptr())
+    if gather is not None:
+        u.ga = gather
     check(lib().mdl_update_fused(ctypes.byref(u), kernels._stream()), "update_fused")
     return st
 

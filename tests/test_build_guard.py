@@ -128,7 +128,7 @@ def test_kernel_arg_structs_match_ctypes(tmp_path):
     structs' sizes and field offsets: a field appended on one side only shifts every later pointer (round 6 grew
     EncP / DecP / PPOArgs).  The C side is compiled for the host from the library's own headers."""
     import ctypes
-    from mat_dcml_amd.ops import mat_train, ppo_fused
+    from mat_dcml_amd.ops import kernels, mat_train, ppo_fused
     csrc = os.path.join(ROOT, "mat_dcml_amd", "csrc")
     src = tmp_path / "sz.hip"
     # the PPO / Adam / update structs live in ppo.hip: include it (its kernels compile for the host side as stubs)
@@ -141,7 +141,8 @@ int main() {{
   printf("DecP %zu %zu %zu\\n", sizeof(DecP), offsetof(DecP, g_mode), offsetof(DecP, sidx));
   printf("PPOArgs %zu %zu %zu\\n", sizeof(PPOArgs), offsetof(PPOArgs, n_lp), offsetof(PPOArgs, adv_eps));
   printf("AdamArgs %zu %zu %zu\\n", sizeof(AdamArgs), offsetof(AdamArgs, clip), offsetof(AdamArgs, npart));
-  printf("UpdArgs %zu %zu %zu\\n", sizeof(UpdArgs), offsetof(UpdArgs, a), offsetof(UpdArgs, bar));
+  printf("UpdArgs %zu %zu %zu %zu\\n", sizeof(UpdArgs), offsetof(UpdArgs, a), offsetof(UpdArgs, bar), offsetof(UpdArgs, ga_wg));
+  printf("GatherArgs %zu %zu %zu\\n", sizeof(GatherArgs), offsetof(GatherArgs, idx), offsetof(GatherArgs, eps));
 }}
 ''')
     exe = tmp_path / "sz"
@@ -156,6 +157,8 @@ int main() {{
         "DecP": (ctypes.sizeof(mat_train.DecP), mat_train.DecP.g_mode.offset, mat_train.DecP.sidx.offset),
         "PPOArgs": (ctypes.sizeof(ppo_fused.PPOArgs), ppo_fused.PPOArgs.n_lp.offset, ppo_fused.PPOArgs.adv_eps.offset),
         "AdamArgs": (ctypes.sizeof(ppo_fused.AdamArgs), ppo_fused.AdamArgs.clip.offset, ppo_fused.AdamArgs.npart.offset),
-        "UpdArgs": (ctypes.sizeof(mat_train.UpdArgs), mat_train.UpdArgs.a.offset, mat_train.UpdArgs.bar.offset),
+        "UpdArgs": (ctypes.sizeof(mat_train.UpdArgs), mat_train.UpdArgs.a.offset, mat_train.UpdArgs.bar.offset,
+                    mat_train.UpdArgs.ga_wg.offset),
+        "GatherArgs": (ctypes.sizeof(kernels.GatherArgs), kernels.GatherArgs.idx.offset, kernels.GatherArgs.eps.offset),
     }
     assert got == want, (got, want)

@@ -91,12 +91,12 @@ def test_fused_training_repeatable(gpu):
     print(f"max relative run-to-run gradient deviation (fp32 atomic order): {worst:.2e}")
 
 
-def _ppo_run(gpu, iters=2, fused_update=True, mb_index="gather", gather_ahead=True):
+def _ppo_run(gpu, iters=2, fused_update=True, mb_index="gather", gather_ahead=False, fused_gather=True):
     from mat_dcml_amd.config import get_config, parse_args
     from mat_dcml_amd.parallel.comm import Comm
     from mat_dcml_amd.runner.dcml_runner import DCMLRunner
     env = {"MAT_DCML_FUSED_UPDATE": "1" if fused_update else "0", "MAT_DCML_MB_INDEX": mb_index,
-           "MAT_DCML_GATHER_AHEAD": "1" if gather_ahead else "0"}
+           "MAT_DCML_GATHER_AHEAD": "1" if gather_ahead else "0", "MAT_DCML_FUSED_GATHER": "1" if fused_gather else "0"}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -152,9 +152,12 @@ def test_kernel_minibatch_index_matches_gather(gpu):
     assert d < 1e-5 and dm < 1e-3, (d, dm)
 
 
-def test_gather_ahead_is_bitwise_neutral(gpu):
-    """The next minibatch's gather on the side stream (algos/mat_trainer._GatherAhead) against the in-line gather:
-    the same rows and arithmetic, only the stream differs, so parameters and Adam moments are bitwise equal."""
-    a, b = _ppo_run(gpu, gather_ahead=True), _ppo_run(gpu, gather_ahead=False)
-    for k in a:
-        assert torch.equal(a[k], b[k]), (k, (a[k] - b[k]).abs().max().item())
+def test_gather_placement_is_bitwise_neutral(gpu):
+    """The next minibatch's gather inside the fused update's adam_pack launch (default, csrc/gather_rows.h
+    gather_rows_wavewise) and on a side stream (algos/mat_trainer._GatherAhead) against the standalone in-line
+    gather: the same rows and the same standardisation arithmetic, so parameters and Adam moments are bitwise equal."""
+    base = _ppo_run(gpu, gather_ahead=False, fused_gather=False)
+    for kw in (dict(fused_gather=True), dict(gather_ahead=True, fused_gather=False)):
+        a = _ppo_run(gpu, **kw)
+        for k in a:
+            assert torch.equal(a[k], base[k]), (kw, k, (a[k] - base[k]).abs().max().item())
