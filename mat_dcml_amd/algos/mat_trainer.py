@@ -277,7 +277,7 @@ class MATTrainer:
             self._finish_overlap(buf, work, split[3])
             pol.optimizer.step(norm_ready=False)
             mat_fused.bump_version(m)
-            return nxt if nxt is not None or ahead is None else kernels.gather_rows(*ahead, ("adv",))
+            return self._next_minibatch(ahead, nxt)
         # one process: the workspace reduction also leaves the optimizer's Σ g² partials of the final gradient (no
         # norm launch); under data parallelism the norm is the all-reduced gradient's, so the Adam step computes it
         fuse_norm = self.comm.world_size == 1 and not self.poison
@@ -292,7 +292,7 @@ class MATTrainer:
             enc.ctx = None
             mat_fused.bump_version(m)
             mat_train.mark_packs_current(m)
-            return nxt if nxt is not None or ahead is None else kernels.gather_rows(*ahead, ("adv",))
+            return self._next_minibatch(ahead, nxt)
         norm_ready = mat_train.reduce_grad_workspace(m, norm_into=pol.optimizer.scratch if fuse_norm else None,
                                                      accumulate=self._direct_grads)
         dec.ctx = None
@@ -300,14 +300,20 @@ class MATTrainer:
         if self.poison:
             buf[:1].fill_(float("nan"))   # the fused Adam kernel skips non-finite steps
         if self.comm.world_size > 1:
-            # ONE all-reduce of the whole 0.6 MB flat gradient per minibatch: at this size RCCL over xGMI is
-            # latency-bound, so splitting it to overlap the decoder slice with the encoder backward only added a
-            # collective (round-1 variant)
+            # ONE blocking all-reduce of the whole 0.6 MB flat gradient per minibatch (the default; --grad_overlap
+            # all-reduces the decoder slice asynchronously under enc_bwd instead, the branch above)
             self.comm.grad_mean_(buf)
             self.collectives += 1
         pol.optimizer.step(norm_ready=norm_ready)
         mat_fused.bump_version(m)
-        return nxt if nxt is not None or ahead is None else kernels.gather_rows(*ahead, ("adv",))
+        return self._next_minibatch(ahead, nxt)
+
+    @staticmethod
+    def _next_minibatch(ahead, nxt):
+        """The next minibatch: the one already gathered (``nxt``), else gathered now (its own launch), else None."""
+        if nxt is not None or ahead is None:
+            return nxt
+        return kernels.gather_rows(*ahead, ("adv",))
 
     # ------------------------------------------------------------------------------------------------
     def _overlap_split(self):
