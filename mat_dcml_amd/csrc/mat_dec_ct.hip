@@ -418,6 +418,7 @@ __device__ __forceinline__ void head_fwd_ct(const DecP& p, const CT* xr, bool sa
   AFr H;
   loadA(H, p.h1.fa, lane);
   const CT bh = ld_vec(p.h1.b, lane), gam = ld_vec(p.lnh.g, lane), bet = ld_vec(p.lnh.b, lane);
+  CP_MARK(31);
 #pragma unroll
   for (int k = 0; k < MAXRT; ++k) {
     const int rt = c.wave + NW * k;
@@ -442,8 +443,10 @@ __device__ __forceinline__ void head_fwd_ct(const DecP& p, const CT* xr, bool sa
         gelu_ct(hh);
         ln_fwd_ct(hh, xh, n, gam, bet);
       }
+      CP_MARK(32);
       f32x4 L[MA];
       head_logits_ct<MA>(p, W, n, L, lane);
+      CP_MARK(33);
       if (CONT) {   // per-dimension Normal(mean, std): this lane's dims a = 16ma + 4g + r
 #pragma unroll
         for (int ma = 0; ma < MA; ++ma)
@@ -474,6 +477,7 @@ __device__ __forceinline__ void head_fwd_ct(const DecP& p, const CT* xr, bool sa
         p.logp[tok] = lp;
         p.ent[tok] = en;
       }
+      CP_MARK(34);
     }
   }
 }

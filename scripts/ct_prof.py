@@ -18,7 +18,9 @@ NAMES = {0: "tile start (zero LDS)", 1: "head bwd (tiles)", 19: "head bwd wgrads
          11: "self bwd proj+LN", 13: "self recompute qkv + wgrad proj", 14: "self attn bwd q (+ stage x)",
          15: "self attn bwd kv", 16: "self dX", 17: "self wgrad qkv", 30: "embedding bwd",
          20: "self qkv fwd", 21: "self attn fwd", 22: "self proj+LN fwd", 23: "mlp fwd (wave 0)", 24: "cross qkv fwd",
-         25: "cross attn fwd", 26: "cross proj+LN fwd", 27: "head fwd", 28: "embedding fwd"}
+         25: "cross attn fwd", 26: "cross proj+LN fwd", 27: "head fwd (rest)", 28: "embedding fwd",
+         31: "head fwd: weight loads", 32: "head fwd: W_h1 + GELU + LN + saves", 33: "head fwd: logits",
+         34: "head fwd: softmax stats + stores"}
 
 
 def read(fn):
