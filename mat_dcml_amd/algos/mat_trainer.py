@@ -409,6 +409,12 @@ class MATTrainer:
         # HIP path: advantage statistics by a fixed-order fp64 reduction kernel, and each minibatch gathered by ONE
         # launch that also standardises the advantages of the rows it reads (no full normalised copy)
         native = self.fused and kernels.use_hip(obs_f)
+        from ..ops import mat_train
+        if native and mat_train.WIDE_OBS_BF16 and obs_f.shape[-1] > mat_train.MAX_FUSED_OBS and \
+                self.num_mini_batch == 1:
+            # wide observations (SMAC) as bf16 ONCE per update, not per epoch: the obs-embedding kernels read half
+            # the bytes (the encoder would round them itself, identically, on every call)
+            obs_f = obs_f.to(torch.bfloat16)
         for epoch in range(self.ppo_epoch):
             if epoch == 0 or self.recompute_gae_every_epoch:
                 next_values = pol.get_values(None, buffer.obs[-1], buffer.available_actions[-1])

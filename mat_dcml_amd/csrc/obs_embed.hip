@@ -33,6 +33,8 @@ struct OEArgs {
   float* M;                    // [64][od] workspace (zeroed by the host)
   float* ud;                   // [2][64] u, db workspace (zeroed by the host)
   float *d_we, *d_be, *d_g, *d_b;
+  const bf16_t* xh;            // [N][od] bf16 observations (non-null: read instead of x — half the bytes, and x is
+                               // exact in bf16 so the lo half of the hi / lo split vanishes)
 };
 
 // W' = W_e diag(g) as bf16 A fragments + c1 (from the rounded values) / c0.  One block per output feature f.
@@ -78,7 +80,8 @@ constexpr int OE_WAVES = 4;
 // one tile per workgroup (parallelism) and a deeper prefetch
 template <int TPW> struct OECfg { static constexpr int PF = TPW == 1 ? 5 : 2; };
 template <int TPW>
-struct OEStep { float4 x0[TPW], x1[TPW]; bf16x8 w[4]; };
+struct OEStep { float4 x0[TPW], x1[TPW]; uint4 xb[TPW]; bf16x8 w[4]; };
+template <bool XB>
 __device__ __forceinline__ void oe_mma(const float (&v)[8], const bf16x8 (&w)[4], bool ok, f32x4 (&acc)[4], float& sx,
                                        float& sxx) {
   bf16x8 hi, lo;
@@ -89,15 +92,23 @@ __device__ __forceinline__ void oe_mma(const float (&v)[8], const bf16x8 (&w)[4]
     sxx += xv * xv;
     const uint16_t h = f2bf(xv);
     hi[j] = (short)h;
-    lo[j] = (short)f2bf(xv - bf2f(h));
+    if (!XB) lo[j] = (short)f2bf(xv - bf2f(h));
   }
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) {
     acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[mt], hi, acc[mt], 0, 0, 0);
-    acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[mt], lo, acc[mt], 0, 0, 0);
+    if (!XB) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[mt], lo, acc[mt], 0, 0, 0);
   }
 }
-template <int TPW>
+__device__ __forceinline__ void oe_unpack8(const uint4 u, float (&v)[8]) {
+  const uint32_t q[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[2 * j] = __uint_as_float(q[j] << 16);
+    v[2 * j + 1] = __uint_as_float(q[j] & 0xFFFF0000u);
+  }
+}
+template <int TPW, bool XB>
 __global__ __launch_bounds__(64 * OE_WAVES) void obs_embed_fwd_kernel(OEArgs a) {
   constexpr int PF = OECfg<TPW>::PF;
   __shared__ f32x4 part[OE_WAVES - 1][TPW][4][64];
@@ -106,19 +117,21 @@ __global__ __launch_bounds__(64 * OE_WAVES) void obs_embed_fwd_kernel(OEArgs a) 
   int tok[TPW];
   bool ok[TPW];
   const float* xr[TPW];
+  const bf16_t* xbr[TPW];
   f32x4 acc[TPW][4];
   float sx[TPW], sxx[TPW];
 #pragma unroll
   for (int t = 0; t < TPW; ++t) {
     tok[t] = (blockIdx.x * TPW + t) * OE_TOK + c;
     ok[t] = tok[t] < a.N;
-    xr[t] = a.x + (size_t)(ok[t] ? tok[t] : 0) * a.od;
+    if (XB) xbr[t] = a.xh + (size_t)(ok[t] ? tok[t] : 0) * a.od;
+    else xr[t] = a.x + (size_t)(ok[t] ? tok[t] : 0) * a.od;
     sx[t] = sxx[t] = 0.f;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) acc[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   int s = wave;
-  if ((a.od & 3) == 0) {   // float4 rows: the steps whose 32 dims are all inside the row, PF at a time
+  if ((a.od & (XB ? 7 : 3)) == 0) {   // 16-byte rows: the steps whose 32 dims are all inside the row, PF at a time
     const int nfull = a.od >> 5;
     for (; s + OE_WAVES * (PF - 1) < nfull; s += OE_WAVES * PF) {
       OEStep<TPW> st[PF];
@@ -127,8 +140,12 @@ __global__ __launch_bounds__(64 * OE_WAVES) void obs_embed_fwd_kernel(OEArgs a) 
         const int k0 = 32 * (s + OE_WAVES * u) + 8 * g;
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
-          st[u].x0[t] = *(const float4*)(xr[t] + k0);
-          st[u].x1[t] = *(const float4*)(xr[t] + k0 + 4);
+          if (XB) {
+            st[u].xb[t] = *(const uint4*)(xbr[t] + k0);
+          } else {
+            st[u].x0[t] = *(const float4*)(xr[t] + k0);
+            st[u].x1[t] = *(const float4*)(xr[t] + k0 + 4);
+          }
         }
         const bf16_t* wp = a.wpack + ((size_t)(s + OE_WAVES * u) * 4 * 64 + lane) * 8;
 #pragma unroll
@@ -139,9 +156,14 @@ __global__ __launch_bounds__(64 * OE_WAVES) void obs_embed_fwd_kernel(OEArgs a) 
       for (int u = 0; u < PF; ++u)
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
-          const float v[8] = {st[u].x0[t].x, st[u].x0[t].y, st[u].x0[t].z, st[u].x0[t].w,
-                              st[u].x1[t].x, st[u].x1[t].y, st[u].x1[t].z, st[u].x1[t].w};
-          oe_mma(v, st[u].w, ok[t], acc[t], sx[t], sxx[t]);
+          float v[8];
+          if (XB) {
+            oe_unpack8(st[u].xb[t], v);
+          } else {
+            v[0] = st[u].x0[t].x; v[1] = st[u].x0[t].y; v[2] = st[u].x0[t].z; v[3] = st[u].x0[t].w;
+            v[4] = st[u].x1[t].x; v[5] = st[u].x1[t].y; v[6] = st[u].x1[t].z; v[7] = st[u].x1[t].w;
+          }
+          oe_mma<XB>(v, st[u].w, ok[t], acc[t], sx[t], sxx[t]);
         }
     }
   }
@@ -154,14 +176,21 @@ __global__ __launch_bounds__(64 * OE_WAVES) void obs_embed_fwd_kernel(OEArgs a) 
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
       float v[8];
-      if ((a.od & 3) == 0 && k0 + 8 <= a.od) {
+      if (XB) {
+        if ((a.od & 7) == 0 && k0 + 8 <= a.od) {
+          oe_unpack8(*(const uint4*)(xbr[t] + k0), v);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = k0 + j < a.od ? bf2f(xbr[t][k0 + j]) : 0.f;
+        }
+      } else if ((a.od & 3) == 0 && k0 + 8 <= a.od) {
         const float4 p = *(const float4*)(xr[t] + k0), q = *(const float4*)(xr[t] + k0 + 4);
         v[0] = p.x; v[1] = p.y; v[2] = p.z; v[3] = p.w; v[4] = q.x; v[5] = q.y; v[6] = q.z; v[7] = q.w;
       } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = k0 + j < a.od ? xr[t][k0 + j] : 0.f;
       }
-      oe_mma(v, w, ok[t], acc[t], sx[t], sxx[t]);
+      oe_mma<XB>(v, w, ok[t], acc[t], sx[t], sxx[t]);
     }
   }
   if (wave > 0) {
@@ -224,6 +253,16 @@ __device__ __forceinline__ void oeb_load(const OEArgs& a, int t, int t_hi, int c
     const float4 d0 = dp[0], d1 = dp[1];
     T.p[0] = d0.x * rr; T.p[1] = d0.y * rr; T.p[2] = d0.z * rr; T.p[3] = d0.w * rr;
     T.p[4] = d1.x * rr; T.p[5] = d1.y * rr; T.p[6] = d1.z * rr; T.p[7] = d1.w * rr;
+    if (a.xh) {   // bf16 observations
+      const bf16_t* xb = a.xh + (size_t)t * a.od;
+      if ((a.od & 7) == 0 && k0 + 8 <= a.od) {
+        oe_unpack8(*(const uint4*)(xb + k0), T.x);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) T.x[j] = k0 + j < a.od ? bf2f(xb[k0 + j]) : 0.f;
+      }
+      return;
+    }
     const float* xr = a.x + (size_t)t * a.od;
     if ((a.od & 3) == 0 && k0 + 8 <= a.od) {
       const float4 x0 = *(const float4*)(xr + k0), x1 = *(const float4*)(xr + k0 + 4);
@@ -271,7 +310,8 @@ __global__ __launch_bounds__(256) void obs_embed_bwd_m_kernel(OEArgs a) {
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) {
       acc.v[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, ld_frag_T(Xh, 0, 16 * ct, lane), acc.v[ct], 0, 0, 0);
-      acc.v[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, ld_frag_T(Xl, 0, 16 * ct, lane), acc.v[ct], 0, 0, 0);
+      if (!a.xh)   // bf16 observations: the lo half is zero
+        acc.v[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, ld_frag_T(Xl, 0, 16 * ct, lane), acc.v[ct], 0, 0, 0);
     }
     __syncthreads();
   }
@@ -336,10 +376,14 @@ MDL_API int mdl_obs_embed_pack(const OEArgs* a, hipStream_t st) {
 MDL_API int mdl_obs_embed_fwd(const OEArgs* a, hipStream_t st) {
   if (a->N <= 0) return 0;
   const int tiles = (a->N + OE_TOK - 1) / OE_TOK;
-  if (tiles >= 4 * 1024)   // enough tiles to fill the chip four per workgroup
-    hipLaunchKernelGGL(obs_embed_fwd_kernel<4>, dim3((tiles + 3) / 4), dim3(64 * OE_WAVES), 0, st, *a);
-  else
-    hipLaunchKernelGGL(obs_embed_fwd_kernel<1>, dim3(tiles), dim3(64 * OE_WAVES), 0, st, *a);
+  const bool xb = a->xh != nullptr;
+  if (tiles >= 4 * 1024) {   // enough tiles to fill the chip four per workgroup
+    if (xb) hipLaunchKernelGGL((obs_embed_fwd_kernel<4, true>), dim3((tiles + 3) / 4), dim3(64 * OE_WAVES), 0, st, *a);
+    else hipLaunchKernelGGL((obs_embed_fwd_kernel<4, false>), dim3((tiles + 3) / 4), dim3(64 * OE_WAVES), 0, st, *a);
+  } else {
+    if (xb) hipLaunchKernelGGL((obs_embed_fwd_kernel<1, true>), dim3(tiles), dim3(64 * OE_WAVES), 0, st, *a);
+    else hipLaunchKernelGGL((obs_embed_fwd_kernel<1, false>), dim3(tiles), dim3(64 * OE_WAVES), 0, st, *a);
+  }
   MDL_CHECK_LAUNCH();
   return 0;
 }

@@ -84,13 +84,17 @@ sig("mdl_ct_bwd_grid", ctypes.c_int, ctypes.c_int)
 class OEArgs(ctypes.Structure):   # csrc/obs_embed.hip
     _fields_ = [(n, ctypes.c_int) for n in ("N", "od", "KS")] + \
                [(n, VP) for n in ("x", "we", "be", "g", "b", "wpack", "c01", "pre", "stat", "dpre", "M", "ud", "d_we",
-                                  "d_be", "d_g", "d_b")]
+                                  "d_be", "d_g", "d_b", "xh")]
 
 
 sig("mdl_obs_embed_pack", ctypes.POINTER(OEArgs), VP)
 sig("mdl_obs_embed_fwd", ctypes.POINTER(OEArgs), VP)
 sig("mdl_obs_embed_bwd", ctypes.POINTER(OEArgs), VP)
 MAX_FUSED_OBS = 16      # obs_dim embedded inside the fused encoder; wider observations use csrc/obs_embed.hip
+# Wide observations (SMAC's 1,288 features) enter the embedding as bf16: half the bytes of its one large operand.
+# Rollout and learner both round them, so the PPO ratio is unaffected (tests/test_gpu_logprob_consistency.py smac).
+# SMAC bench 75.8k / 76.8k -> 77.8k / 77.8k env-steps/s (profiles/r6_ab/).  MAT_DCML_WIDE_OBS_BF16=0: fp32 inputs.
+WIDE_OBS_BF16 = os.environ.get("MAT_DCML_WIDE_OBS_BF16", "1") == "1"
 
 
 class ObsEmbed:
@@ -111,7 +115,11 @@ class ObsEmbed:
         self.version = None
 
     def _args(self, N=0, x=None, pre=None, stat=None, dpre=None):
-        return OEArgs(N=N, od=self.od, KS=self.KS, x=_ptr(x), we=self.lin.weight.data_ptr(), be=self.lin.bias.data_ptr(),
+        xh = x if x is not None and x.dtype == torch.bfloat16 else None
+        if xh is not None:
+            x = None
+        return OEArgs(N=N, od=self.od, KS=self.KS, x=_ptr(x), xh=_ptr(xh), we=self.lin.weight.data_ptr(),
+                      be=self.lin.bias.data_ptr(),
                       g=self.ln.weight.data_ptr(), b=self.ln.bias.data_ptr(), wpack=self.wpack.data_ptr(),
                       c01=self.c01.data_ptr(), pre=_ptr(pre), stat=_ptr(stat), dpre=_ptr(dpre), M=self.M.data_ptr(),
                       ud=self.ud.data_ptr(), d_we=_gptr(self.lin.weight), d_be=_gptr(self.lin.bias),
@@ -351,7 +359,8 @@ class EncoderFused:
         if not save:   # rollout / value passes: small batches — spread them over every CU (nothing is saved, so
             SQ, NRP = _spread(B, L, SQ, NRP, dev)   # the backward's tiling need not match)
         n_tok = B * L
-        obs = obs.float().contiguous()
+        wide_bf16 = od > MAX_FUSED_OBS and (WIDE_OBS_BF16 or obs.dtype == torch.bfloat16)
+        obs = (obs.to(torch.bfloat16) if wide_bf16 else obs.float()).contiguous()
         pre = stat = None
         if od > MAX_FUSED_OBS:   # wide observations: embedding pre-activation from the obs-embedding kernel
             if idx is not None:  # (the wide embedding reads dense rows)

@@ -441,6 +441,35 @@ def test_obs_embed_forward_matches_torch(gpu, N):
     assert torch.allclose(stat[:, 1], torch.rsqrt(var + 1e-5), atol=1e-4, rtol=1e-3)
 
 
+@pytest.mark.parametrize("N", [864, 70_000])
+def test_obs_embed_bf16_observations_match_fp32_path(gpu, N):
+    """bf16 observations (OEArgs.xh, MAT_DCML_WIDE_OBS_BF16) against the fp32 path on the same, bf16-representable
+    values: the fp32 path's hi / lo split has an all-zero lo half there, so forward (pre, mu, rstd) and the backward's
+    parameter gradients must agree bit for bit — the bf16 path only reads half the bytes."""
+    torch.manual_seed(1)
+    od = 1288
+    m = MultiAgentTransformer(od, od, 36, 27, 2, 64, 2).to(gpu)
+    with torch.no_grad():
+        ln, lin = m.encoder.obs_encoder[0], m.encoder.obs_encoder[1]
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.2, 0.2)
+    oe = mat_train.ObsEmbed(m)
+    xb = (torch.randn(N, od, device=gpu) * 2.0 + 0.3).to(torch.bfloat16)
+    outs = []
+    for x in (xb, xb.float()):
+        for prm in (ln.weight, ln.bias, lin.weight, lin.bias):
+            prm.grad = torch.zeros_like(prm)
+        pre, stat = oe.forward(x)
+        dpre = torch.randn(N, 64, device=gpu, generator=torch.Generator(device=gpu).manual_seed(2))
+        oe.backward(x, stat, dpre)
+        torch.cuda.synchronize()
+        outs.append([pre.clone(), stat.clone()] + [p.grad.clone() for p in (ln.weight, ln.bias, lin.weight, lin.bias)])
+    for a, b in zip(*outs[:2]):
+        # the backward's fp32 atomics (M, u) sum in a run-dependent order: the gradients agree to that rounding
+        assert torch.equal(a, b) or (a - b).abs().max().item() <= 1e-5 * b.abs().max().item(), (a - b).abs().max()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
 def test_single_minibatch_epoch_in_place_matches_gather(gpu):
     """A one-minibatch PPO epoch trains on the buffer's rows in place (no permuted gather copy): two identically
     seeded runners, one forced through the gather, report the same losses up to fp32 summation order, and their
