@@ -151,7 +151,16 @@ def use_hip(t: torch.Tensor) -> bool:
     return True
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_CUR_DEV = getattr(torch._C, "_cuda_getDevice", None)
+
+
 def _stream():
+    """The current HIP stream of the current device as a ctypes pointer.  torch.cuda.current_stream() builds a Stream
+    object (device-index resolution included): ~9 us of host time per launch, 4 launches per rollout step — the
+    rollout's host side runs only ~1.5x ahead of the GPU, so the raw accessor is used where this torch has it."""
+    if _RAW_STREAM is not None and _CUR_DEV is not None:
+        return ctypes.c_void_p(_RAW_STREAM(_CUR_DEV()))
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
