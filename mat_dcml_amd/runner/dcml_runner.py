@@ -249,20 +249,27 @@ class DCMLRunner:
         from ..ops import kernels
         t = b.step
         lo, hi = rows if rows is not None else (0, b.E)
+        # the buffer-side views of slot t (persistent tensors): built once per (slot, rows), not per step — the
+        # rollout's host side runs only ~1.6x ahead of the GPU, and each view is a torch object to create
+        key = (t, lo, hi)
+        cache = self.__dict__.setdefault("_ins_views", {})
+        dv = cache.get(key)
+        if dv is None:
+            dv = cache[key] = ([b.share_obs[t + 1][lo:hi], b.obs[t + 1][lo:hi], b.available_actions[t + 1][lo:hi],
+                                b.actions[t][lo:hi], b.action_log_probs[t][lo:hi], b.value_preds[t][lo:hi]],
+                               b.rewards[t][lo:hi], b.masks[t + 1][lo:hi], b.rewards[t].is_contiguous(),
+                               self._ep_reward[lo:hi], self._ep_delay[lo:hi], self._ep_pay[lo:hi])
+        dsts, rew_slot, mask_slot, rew_ok, ep_r, ep_d, ep_p = dv
         sh = share if share.dim() == 2 else share[:, 0]
-        pairs = [(sh, b.share_obs[t + 1][lo:hi]), (obs, b.obs[t + 1][lo:hi]),
-                 (ava, b.available_actions[t + 1][lo:hi]), (actions, b.actions[t][lo:hi]),
-                 (logp, b.action_log_probs[t][lo:hi]), (values, b.value_preds[t][lo:hi])]
+        pairs = list(zip((sh, obs, ava, actions, logp, values), dsts))
         for src, dst in pairs:
             if (src.dtype != torch.float32 or src.numel() != dst.numel() or not src.is_contiguous()
                     or not dst.is_contiguous()):
                 return False
-        if done.dtype != torch.bool or not b.rewards[t].is_contiguous():
+        if done.dtype != torch.bool or not rew_ok:
             return False
         kernels.rollout_insert(pairs, reward.contiguous(), delay.contiguous(), pay.contiguous(), done.contiguous(),
-                               b.rewards[t][lo:hi], b.masks[t + 1][lo:hi], self._ep_reward[lo:hi],
-                               self._ep_delay[lo:hi], self._ep_pay[lo:hi],
-                               self._done_stats if stats is None else stats)
+                               rew_slot, mask_slot, ep_r, ep_d, ep_p, self._done_stats if stats is None else stats)
         if advance:
             b.step = (t + 1) % b.T
         return True
