@@ -258,7 +258,10 @@ def decode(model, rep, ava=None, deterministic=False, stride=1, rand=None):
     cont, avail = pk["cont"], pk["avail"]
     out_a = torch.empty(B, L, A if cont else 1, device=dev)
     out_lp = torch.empty(B, L, (A - 1 if avail else A) if cont else 1, device=dev)
-    geo = lib().mdl_mat_decode_geometry(model.n_block, L, min(B, _EPW_CAP))
+    gkey = (model.n_block, L, min(B, _EPW_CAP))
+    geo = _GEO.get(gkey)
+    if geo is None:
+        geo = _GEO[gkey] = lib().mdl_mat_decode_geometry(*gkey)
     epw, rmax = geo & 0xFF, geo >> 8
     if epw <= 0:
         raise RuntimeError(f"mat_decode: L={L} does not fit in LDS")
@@ -273,9 +276,17 @@ def decode(model, rep, ava=None, deterministic=False, stride=1, rand=None):
     if _spec_set[0] != SPEC_DECODE:
         lib().mdl_decode_spec_enable(int(SPEC_DECODE))
         _spec_set[0] = SPEC_DECODE
-    model._mdl_decode_path = wave_path(prm, model.n_block)
+    # the path report (two plan queries + formatting) once per call shape, not per rollout step
+    pkey = (B, L, A, model.n_block, int(bool(deterministic)), int(stride), cont, avail, gen, rand is not None,
+            ava is not None, WAVE_DECODE, SPEC_DECODE, id(pk))
+    if getattr(model, "_mdl_decode_path_key", None) != pkey:
+        model._mdl_decode_path = wave_path(prm, model.n_block)
+        model._mdl_decode_path_key = pkey
     check(lib().mdl_mat_decode(ctypes.byref(prm), model.n_block, kernels._stream()), "mat_decode")
     return out_a, out_lp
+
+
+_GEO = {}   # mdl_mat_decode_geometry results (a pure function of its arguments)
 
 
 def wave_path(prm, n_block):
